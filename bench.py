@@ -1,0 +1,146 @@
+"""Benchmark: images/sec of one U-Net training step (forward + BCE loss + backward
+[+ RCCL all-reduce] + Adam) on synthetic 512x512 data, Base config
+(UNetWithBackbone resnet34, no attention, batch 16 per GPU), BASELINE.json
+configs[1] (N=1) / configs[2] (N>1, weak scaling, 16 per rank).
+
+python bench.py --gpus N --steps K --warmup W   (N>1: launched by torch.distributed.run)
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+
+
+def cpu_baseline(batch: int, h: int, steps: int, threads: int):
+    """Time the oracle (fp32 torch-CPU restatement of the reference path) on host cores."""
+    import oracle
+    torch.set_num_threads(threads)
+    pkg = importlib.import_module("image-segmentation-project_amd")
+    xs, ms = pkg.synthetic_cells(batch, h, h, seed=1234)
+    x, y = torch.from_numpy(xs), torch.from_numpy(ms)
+    m = oracle.ReferenceUNet()
+    m.load_state_dict(oracle.closed_form_state_dict(m))
+    m.train()
+    opt = oracle.make_adam(m)
+    crit = oracle.get_loss_function({"loss_fn": "bce"})
+    oracle.train_step(m, opt, crit, x[:2], y[:2])  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        oracle.train_step(m, opt, crit, x, y)
+    dt = time.perf_counter() - t0
+    return {"value": round(batch * steps / dt, 3), "unit": "images/sec", "cores": threads, "kind": "port",
+            "sample": f"{steps} fp32 train steps (fwd+bce+bwd+Adam) of batch {batch} at {h}x{h}, "
+                      f"oracle/unet_ref.py on {threads} host threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=16, help="images per GPU")
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    pkg = importlib.import_module("image-segmentation-project_amd")
+    ddp = importlib.import_module("image-segmentation-project_amd.ddp")
+
+    torch.manual_seed(0)
+    model = pkg.UNetWithBackbone(n_classes=1, backbone="resnet34", pretrained=False, use_attention=False).to(dev)
+    if world > 1:
+        ddp.enable_data_parallel(model)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-5)
+    crit = pkg.get_loss_function({"loss_fn": "bce"})
+    xs, ms = pkg.synthetic_cells(args.batch, args.size, args.size, seed=1234 + rank)
+    x = torch.from_numpy(xs).to(dev)
+    y = torch.from_numpy(ms).to(dev)
+    model.train()
+
+    def step():
+        out = model(x)
+        loss = crit(out, y)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        return out, loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out, loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    # metric side: mIoU (reference aggregation) of the last step's pre-step logits
+    miou = pkg.calculate_metrics_from_logits(out.detach(), y)["iou"]
+    imgs = args.batch * args.steps * world
+    flops_step = model.step_flops((args.batch, 1, args.size, args.size), training=True)
+    ms_step = dt / args.steps * 1e3
+    achieved_tflops = flops_step / (dt / args.steps) / 1e12
+    line = {
+        "metric": "images/sec + mIoU, 512x512 U-Net bf16 at 1/2/4/8 MI355X",
+        "value": round(imgs / dt, 3),
+        "unit": "images/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (Gaussian cells, seed 1234+rank), random-init weights",
+        "miou": round(miou, 6),
+        "config": {"workload": "Base U-Net resnet34 no-attention train step (fwd+bce+bwd+Adam)",
+                   "global_batch": args.batch * world, "image": f"{args.size}x{args.size}",
+                   "parallelism": f"dp{world}"},
+        "roofline": {"bound": "mfma", "achieved": round(achieved_tflops, 2), "peak": MFMA_BF16_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved_tflops / MFMA_BF16_PEAK_TFLOPS, 4),
+                     "traffic": None, "scope": "whole step (algorithmic 163.1 GFLOP/img / step time)"},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.batch, args.size, args.cpu_steps, args.cpu_threads)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

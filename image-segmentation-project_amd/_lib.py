@@ -1,0 +1,100 @@
+"""ctypes binding of libunet_hip.so (the C ABI declared in include/unet_hip.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (``make -C csrc``).
+There is no CPU fallback: if the library or a ROCm GPU is missing, every op
+raises ``RuntimeError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libunet_hip.so")
+
+_lib = None
+
+c_int, c_int64, c_float, c_double, c_void_p, c_char_p = (
+    ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_double, ctypes.c_void_p, ctypes.c_char_p)
+
+
+class UnetConfig(ctypes.Structure):
+    _fields_ = [("N", c_int), ("H", c_int), ("W", c_int), ("width", c_int), ("n_classes", c_int),
+                ("bn_eps", c_float), ("bn_momentum", c_float)]
+
+
+# name -> (restype, argtypes); every exported symbol of include/unet_hip.h
+SIGNATURES = {
+    "unet_last_error": (c_char_p, []),
+    "unet_version": (c_char_p, []),
+    "unet_plan_create": (c_int, [ctypes.POINTER(UnetConfig), ctypes.POINTER(c_void_p)]),
+    "unet_plan_destroy": (None, [c_void_p]),
+    "unet_plan_workspace_bytes": (c_int64, [c_void_p]),
+    "unet_plan_num_params": (c_int, [c_void_p]),
+    "unet_plan_param_name": (c_int, [c_void_p, c_int, ctypes.c_char_p, c_int]),
+    "unet_plan_param_shape": (c_int, [c_void_p, c_int, ctypes.POINTER(c_int64)]),
+    "unet_plan_param_offset": (c_int64, [c_void_p, c_int]),
+    "unet_plan_grad_numel": (c_int64, [c_void_p]),
+    "unet_plan_num_bn": (c_int, [c_void_p]),
+    "unet_plan_num_buckets": (c_int, [c_void_p]),
+    "unet_plan_bucket_range": (c_int, [c_void_p, c_int, ctypes.POINTER(c_int64), ctypes.POINTER(c_int64)]),
+    "unet_plan_flops": (c_double, [c_void_p, c_int]),
+    "unet_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "unet_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "unet_bucket_wait": (c_int, [c_void_p, c_int, c_void_p]),
+    "unet_loss_forward": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_float, c_float, c_void_p, c_void_p,
+                                  c_void_p]),
+    "unet_loss_backward": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_float, c_float, c_void_p, c_void_p,
+                                   c_void_p, c_void_p]),
+    "unet_mask_metrics": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
+    "unet_conv_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]
+                      + [c_int] * 12 + [c_void_p]),
+    "unet_conv_wgrad": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p] + [c_int] * 12 + [c_void_p]),
+    "unet_pack_weight": (c_int, [c_void_p, c_void_p] + [c_int] * 5 + [c_void_p]),
+    "unet_unpack_grad": (c_int, [c_void_p, c_void_p] + [c_int] * 5 + [c_void_p]),
+    "unet_maxpool_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p] + [c_int] * 4 + [c_void_p]),
+    "unet_maxpool_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 4 + [c_void_p]),
+}
+
+
+def load(path: str = LIB_PATH):
+    """Load (once) and type the shared library.  Raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"libunet_hip.so not found at {path}: build it with `python -c 'import __graft_entry__ as g; "
+            f"g.build()'` (make -C image-segmentation-project_amd/csrc). There is no CPU fallback.")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().unet_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (code {rc}): {msg}")
+
+
+def require_gpu(*tensors):
+    """The product path has no CPU fallback: fail loudly."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("libunet_hip needs a ROCm GPU (MI355X / gfx950); no CPU fallback exists")
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("libunet_hip ops take device tensors; call .to('cuda') first")
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()

@@ -1,0 +1,249 @@
+"""``UNetWithBackbone`` for MI355X — same constructor, forward and state_dict as
+/root/reference/advanced_models.py:64-357 (resnet34 encoder, no attention).
+
+The module tree below exists only to own parameters and buffers under the
+reference's names (``input_conv``, ``bn1``, ``enc1..4`` = torchvision ResNet34
+``layer1..4``, ``upconv4..0``, ``decoder4..1`` = ``_decoder_block`` Sequentials,
+``conv_final``), so ``state_dict()``/``load_state_dict()``/``copy.deepcopy`` and a
+caller-built ``torch.optim.Adam(model.parameters())`` behave exactly as with the
+reference (``train.py:207-226``, ``cross_validation.py:84-100``).  ``forward``
+never runs these submodules: it hands raw device pointers to the native
+executor in ``libunet_hip.so`` (bf16 NHWC activations, MFMA implicit-GEMM
+convolutions, fused BN/ReLU/residual kernels) through one autograd Function.
+"""
+from __future__ import annotations
+
+import ctypes
+import warnings
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+
+
+class _BasicBlock(nn.Module):
+    """Parameter container with torchvision BasicBlock names (conv1/bn1/conv2/bn2/downsample)."""
+
+    def __init__(self, cin: int, cout: int, stride: int):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(cout)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = nn.Conv2d(cout, cout, 3, 1, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(cout)
+        self.downsample = None
+        if stride != 1 or cin != cout:
+            self.downsample = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
+        self.stride = stride
+
+
+def _layer(cin, cout, n, stride):
+    return nn.Sequential(_BasicBlock(cin, cout, stride), *[_BasicBlock(cout, cout, 1) for _ in range(n - 1)])
+
+
+def _decoder_block(cin, cout):
+    # advanced_models.py:197-205 layout: indices 0,1,3,4 carry state
+    return nn.Sequential(nn.Conv2d(cin, cout, 3, padding=1), nn.BatchNorm2d(cout), nn.ReLU(inplace=True),
+                         nn.Conv2d(cout, cout, 3, padding=1), nn.BatchNorm2d(cout), nn.ReLU(inplace=True))
+
+
+class _Plan:
+    """Owns one native plan (per input shape) and its persistent workspace."""
+
+    def __init__(self, n, h, w, width, n_classes, device):
+        lib = _lib.load()
+        cfg = _lib.UnetConfig(n, h, w, width, n_classes, 1e-5, 0.1)
+        handle = ctypes.c_void_p()
+        _lib.check(lib.unet_plan_create(ctypes.byref(cfg), ctypes.byref(handle)), "unet_plan_create")
+        self.lib, self.handle = lib, handle
+        self.shape = (n, h, w)
+        ws_bytes = lib.unet_plan_workspace_bytes(handle)
+        self.workspace = torch.empty(ws_bytes, dtype=torch.uint8, device=device)
+        self.grad_numel = lib.unet_plan_grad_numel(handle)
+        nparam = lib.unet_plan_num_params(handle)
+        buf = ctypes.create_string_buffer(256)
+        self.param_names, self.param_offsets, self.param_shapes = [], [], []
+        shape = (ctypes.c_int64 * 4)()
+        for i in range(nparam):
+            _lib.check(lib.unet_plan_param_name(handle, i, buf, 256), "param_name")
+            self.param_names.append(buf.value.decode())
+            nd = lib.unet_plan_param_shape(handle, i, shape)
+            self.param_shapes.append(tuple(shape[k] for k in range(nd)))
+            self.param_offsets.append(lib.unet_plan_param_offset(handle, i))
+        self.buckets = []
+        b0, b1 = ctypes.c_int64(), ctypes.c_int64()
+        for b in range(lib.unet_plan_num_buckets(handle)):
+            _lib.check(lib.unet_plan_bucket_range(handle, b, ctypes.byref(b0), ctypes.byref(b1)), "bucket_range")
+            self.buckets.append((b0.value, b1.value))
+        self.flops_train = lib.unet_plan_flops(handle, 1)
+        self.flops_fwd = lib.unet_plan_flops(handle, 0)
+        self.generation = 0
+
+    def __del__(self):
+        try:
+            if self.handle:
+                self.lib.unet_plan_destroy(self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+
+class _UNetFunction(torch.autograd.Function):
+    """logits = UNet(x; params).  Backward runs the whole native backward pass and
+    returns every parameter gradient as a view of one flat fp32 buffer."""
+
+    @staticmethod
+    def forward(ctx, model, x, *params):
+        plan = model._plan_for(x)
+        logits = model._run_forward(plan, x, training=True)
+        ctx.model = model
+        ctx.plan = plan
+        ctx.generation = plan.generation
+        ctx.save_for_backward(x)
+        return logits
+
+    @staticmethod
+    def backward(ctx, grad_logits):
+        (x,) = ctx.saved_tensors
+        model, plan = ctx.model, ctx.plan
+        if plan.generation != ctx.generation:
+            raise RuntimeError("UNetWithBackbone: another forward overwrote the saved activations "
+                               "before backward (one forward per backward on the same input shape)")
+        grads = model._run_backward(plan, x, grad_logits.contiguous())
+        views = [grads[o:o + p.numel()].view_as(p) for o, p in zip(plan.param_offsets, model._param_list)]
+        return (None, None, *views)
+
+
+class UNetWithBackbone(nn.Module):
+    """Drop-in for ``advanced_models.UNetWithBackbone`` (resnet34, use_attention=False).
+
+    ``width`` is a build extension (1 = reference channels); ``backbone`` other
+    than 'resnet34' and ``use_attention=True`` are the SURVEY.md §8(f) "next"
+    rows and raise ``NotImplementedError``.
+    """
+
+    def __init__(self, n_classes=1, backbone="resnet34", pretrained=True, use_attention=True, width=1):
+        super().__init__()
+        if backbone != "resnet34":
+            raise NotImplementedError(f"backbone={backbone!r}: only 'resnet34' is built for MI355X (SURVEY.md §8)")
+        if use_attention:
+            raise NotImplementedError("use_attention=True (AttentionGate/ChannelAttention) is not built yet; "
+                                      "pass use_attention=False (the configuration every experiment trains)")
+        if n_classes != 1:
+            raise NotImplementedError("n_classes must be 1 (binary segmentation, advanced_models.py:160)")
+        if pretrained:
+            warnings.warn("pretrained=True needs ImageNet weights from the network (unavailable offline); "
+                          "the encoder keeps its random init — load a state_dict instead", RuntimeWarning)
+        self.use_attention = use_attention
+        self.backbone_name = backbone
+        self.width = width
+        c0, c1, c2, c3 = 64 * width, 128 * width, 256 * width, 512 * width
+        self.input_conv = nn.Conv2d(1, c0, kernel_size=7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(c0)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.enc1 = _layer(c0, c0, 3, 1)
+        self.enc2 = _layer(c0, c1, 4, 2)
+        self.enc3 = _layer(c1, c2, 6, 2)
+        self.enc4 = _layer(c2, c3, 3, 2)
+        self.upconv4 = nn.ConvTranspose2d(c3, c2, kernel_size=2, stride=2)
+        self.decoder4 = _decoder_block(2 * c2, c2)
+        self.upconv3 = nn.ConvTranspose2d(c2, c1, kernel_size=2, stride=2)
+        self.decoder3 = _decoder_block(2 * c1, c1)
+        self.upconv2 = nn.ConvTranspose2d(c1, c0, kernel_size=2, stride=2)
+        self.decoder2 = _decoder_block(2 * c0, c0)
+        self.upconv1 = nn.ConvTranspose2d(c0, c0 // 2, kernel_size=2, stride=2)
+        self.decoder1 = _decoder_block(c0 + c0 // 2, c0 // 2)
+        self.upconv0 = nn.ConvTranspose2d(c0 // 2, c0 // 4, kernel_size=2, stride=2)
+        self.conv_final = nn.Conv2d(c0 // 4, n_classes, kernel_size=1)
+        self._plans = {}
+        self._ddp = None  # set by ddp.enable_data_parallel
+
+    # ------------------------------------------------------------------ plumbing
+    def __getstate__(self):  # deepcopy / pickle: native plans are rebuilt lazily
+        state = self.__dict__.copy()
+        state["_plans"] = {}
+        return state
+
+    @property
+    def _param_list(self):
+        return [p for _, p in self.named_parameters()]
+
+    def _plan_for(self, x) -> _Plan:
+        if x.dim() != 4 or x.shape[1] != 1:
+            raise ValueError(f"expected input [N,1,H,W], got {tuple(x.shape)}")
+        n, _, h, w = x.shape
+        key = (n, h, w, x.device)
+        plan = self._plans.get(key)
+        if plan is None:
+            plan = _Plan(n, h, w, self.width, 1, x.device)
+            names = [k for k, _ in self.named_parameters()]
+            if names != plan.param_names:
+                raise RuntimeError("native parameter table does not match the module's named_parameters()")
+            for p, s in zip(self._param_list, plan.param_shapes):
+                if tuple(p.shape) != s:
+                    raise RuntimeError(f"parameter shape mismatch {tuple(p.shape)} vs {s}")
+            self._plans = {k: v for k, v in self._plans.items() if k[:3] == key[:3]}  # one live shape
+            self._plans[key] = plan
+        return plan
+
+    def _pointer_arrays(self):
+        params = self._param_list
+        for p in params:
+            if not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()):
+                raise RuntimeError("UNetWithBackbone parameters must be contiguous fp32 on the GPU")
+        pa = (ctypes.c_void_p * len(params))(*[p.data_ptr() for p in params])
+        bufs = [b for _, b in self.named_buffers()]
+        ba = (ctypes.c_void_p * len(bufs))(*[b.data_ptr() for b in bufs])
+        return pa, ba
+
+    def _run_forward(self, plan, x, training: bool):
+        _lib.require_gpu(x)
+        x = x.contiguous().float()
+        n, _, h, w = x.shape
+        logits = torch.empty((n, 1, h, w), dtype=torch.float32, device=x.device)
+        pa, ba = self._pointer_arrays()
+        plan.generation += 1
+        rc = plan.lib.unet_forward(plan.handle, x.data_ptr(), pa, ba, plan.workspace.data_ptr(), logits.data_ptr(),
+                                   1 if training else 0, _lib.stream_handle(x.device))
+        _lib.check(rc, "unet_forward")
+        if training:
+            nbt = [b for k, b in self.named_buffers() if k.endswith("num_batches_tracked")]
+            torch._foreach_add_(nbt, 1)
+        return logits
+
+    def _run_backward(self, plan, x, grad_logits):
+        grads = torch.empty(plan.grad_numel, dtype=torch.float32, device=x.device)
+        pa, _ = self._pointer_arrays()
+        rc = plan.lib.unet_backward(plan.handle, x.contiguous().data_ptr(), grad_logits.data_ptr(), pa,
+                                    plan.workspace.data_ptr(), grads.data_ptr(), _lib.stream_handle(x.device))
+        _lib.check(rc, "unet_backward")
+        if self._ddp is not None:
+            self._ddp.reduce(plan, grads)
+        return grads
+
+    # ------------------------------------------------------------------ API
+    def forward(self, x, return_features=False):
+        if return_features:
+            raise NotImplementedError("return_features (advanced_models.py:352-356) is not on the hot path")
+        _lib.require_gpu(x)
+        x = x.contiguous().float()
+        if self.training:
+            if torch.is_grad_enabled():
+                return _UNetFunction.apply(self, x, *self._param_list)
+            return self._run_forward(self._plan_for(x), x, training=True)
+        with torch.no_grad():
+            return self._run_forward(self._plan_for(x), x, training=False)
+
+    def step_flops(self, x_shape, training=True) -> float:
+        """Algorithmic FLOPs of one step at input shape [N,1,H,W]."""
+        n, _, h, w = x_shape
+        lib = _lib.load()
+        cfg = _lib.UnetConfig(n, h, w, self.width, 1, 1e-5, 0.1)
+        handle = ctypes.c_void_p()
+        _lib.check(lib.unet_plan_create(ctypes.byref(cfg), ctypes.byref(handle)), "unet_plan_create")
+        try:
+            return lib.unet_plan_flops(handle, 1 if training else 0)
+        finally:
+            lib.unet_plan_destroy(handle)

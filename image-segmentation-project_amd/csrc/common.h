@@ -1,0 +1,79 @@
+// Shared device helpers for the gfx950 U-Net kernels (bf16 NHWC activations,
+// fp32 accumulation, 64-wide wavefronts).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "kernels.h"
+
+using unet::bf16_t;  // raw bf16 storage
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
+
+__device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(((unsigned)v) << 16);
+}
+// round-to-nearest-even, NaN preserving (v_cvt_pk_bf16_f32)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  return __builtin_bit_cast(bf16_t, (__bf16)f);
+}
+__device__ __forceinline__ unsigned pack_bf2(float a, float b) {
+  return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+}
+__device__ __forceinline__ void unpack8(const uint4& u, float* f) {
+  f[0] = __uint_as_float(u.x << 16); f[1] = __uint_as_float(u.x & 0xffff0000u);
+  f[2] = __uint_as_float(u.y << 16); f[3] = __uint_as_float(u.y & 0xffff0000u);
+  f[4] = __uint_as_float(u.z << 16); f[5] = __uint_as_float(u.z & 0xffff0000u);
+  f[6] = __uint_as_float(u.w << 16); f[7] = __uint_as_float(u.w & 0xffff0000u);
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  return make_uint4(pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]), pack_bf2(f[4], f[5]),
+                    pack_bf2(f[6], f[7]));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be
+// bijective"): blocks that the dispatcher deals to one XCD get consecutive ids.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  if (nwg < 16) return bid;
+  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, loc = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+// BatchNorm per-channel statistics are fp64 sums (sum, sumsq) so that
+// var = E[y^2]-mean^2 does not cancel: stats[0..C) = sum, stats[C..2C) = sumsq.
+// Per-channel affine form of BN: y_hat*gamma+beta == y*scale + shift.
+__device__ __forceinline__ void bn_scale_shift(const unet::BnLaunch& p, int c, float& scale,
+                                               float& shift, float& mean_out, float& invstd_out,
+                                               float& var_out) {
+  float mean, var;
+  if (p.training) {
+    const double m = p.stats[c] / p.count;
+    double v = p.stats[p.C + c] / p.count - m * m;
+    if (v < 0.0) v = 0.0;
+    mean = (float)m;
+    var = (float)v;
+  } else {
+    mean = p.run_mean[c];
+    var = p.run_var[c];
+  }
+  const float inv = 1.0f / sqrtf(var + p.eps);
+  scale = p.gamma[c] * inv;
+  shift = p.beta[c] - mean * scale;
+  mean_out = mean;
+  invstd_out = inv;
+  var_out = var;
+}

@@ -1,0 +1,605 @@
+// Implicit-GEMM convolution kernels for gfx950 (CDNA4), bf16 NHWC, fp32 accumulate.
+//
+// One template covers every conv-shaped op on the U-Net hot path
+// (SURVEY.md §8(a) rows a2-a6):
+//   MODE_FWD   y[n,oh,ow,:] = sum_{r,s} x[n, oh*st-pad+r, ow*st-pad+s, :] . W[:,r,s,:]
+//              (3x3 s1/s2 encoder+decoder convs, 1x1 s2 downsample, and the
+//              k2s2 convT *dgrad*, which is an ordinary k2s2 conv of dY)
+//   MODE_TRANS the transposed (gather) form, output split into stride^2 parity
+//              classes so that every tap inside a class is dense (no zero MACs):
+//              3x3 s1/s2 conv *dgrad* and the ConvTranspose2d(k2,s2) *forward*.
+//   ALOAD_STEM the 7x7/s2 stem: im2col of the fp32 single-channel image built in
+//              the loader (K = 49 taps padded to 64).
+// GEMM view: D[co][pixel] = sum_k Wp[co][k] * X[pixel][k]; the MFMA A operand
+// is the packed weight tile (rows = output channels), B the activation tile
+// (cols = pixels), so each lane's accumulator holds 4 consecutive channels of
+// one pixel -> 8-byte NHWC stores and per-channel BN sums in the epilogue.
+//
+// Weight-gradient kernel (conv_wgrad): dW[co][tap][c] = sum_px dY[px][co] *
+// X_tap[px][c]; both operands are pixel-major in HBM, so they are staged as
+// [pixel][channel] LDS tiles and fed to the MFMA with ds_read_b64_tr_b16
+// (hardware transpose, cdna_hip_programming.md T10); split-K over pixels with
+// fp32 atomics into a [Cout][R*S*C] accumulator.
+#include "common.h"
+#include "kernels.h"
+
+namespace unet {
+
+// ---------------------------------------------------------------------------
+// LDS swizzles (cdna_hip_programming.md §2/T2) for ds_read_b128 fragment reads
+// of the 16x16x32 MFMA: lane l reads row (l&15), 16-B chunk (l>>4) [+4*kk].
+// gfx950 serves ds_read_b128 in four non-contiguous 16-lane groups; both
+// swizzles put every group's 16 addresses on 16 distinct 16-B bank slots.
+// ---------------------------------------------------------------------------
+template <int BK>
+__device__ __forceinline__ int frag_off(int row, int chunk) {
+  if constexpr (BK == 64) {  // 128-B rows, 8 chunks
+    return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
+  } else {  // 64-B rows, 4 chunks; g = (0,2,3,1) packed as 0x78
+    return row * 64 + ((chunk ^ ((0x78 >> (((row >> 2) & 3) << 1)) & 3)) << 4);
+  }
+}
+
+struct TapIter {
+  // MODE_FWD: all R*S taps.  MODE_TRANS: taps r = r0 + st*j valid for class py.
+  int r0, s0, nr, ns, st;
+};
+
+template <int MODE, int ALOAD, int BM, int BN, int BK, int WM, int WN>
+__global__ void __launch_bounds__(256)
+conv_fwd_kernel(ConvFwdArgs a) {
+  constexpr int WTM = BM / WM;  // pixels per wave
+  constexpr int WTN = BN / WN;  // channels per wave
+  constexpr int FM = WTM / 16;
+  constexpr int FN = WTN / 16;
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(FM >= 1 && FN >= 1, "fragment tiling");
+  constexpr int CPR = BK / 8;                       // 16-B chunks per LDS row
+  constexpr int ROWB = BK * 2;                      // bytes per LDS row
+  constexpr int A_ROWS_PER_PASS = 256 / CPR;
+  constexpr int A_PASSES = (BM + A_ROWS_PER_PASS - 1) / A_ROWS_PER_PASS;
+  constexpr int B_PASSES = (BN + A_ROWS_PER_PASS - 1) / A_ROWS_PER_PASS;
+  constexpr int A_BYTES = BM * ROWB;
+  constexpr int B_BYTES = BN * ROWB;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave % WM;
+  const int wn = wave / WM;
+
+  // ---- tile coordinates ----
+  const int nwg = gridDim.x;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int nblk = bid % a.nblocks;
+  const int mblk = bid / a.nblocks;
+  const int cls = blockIdx.z;
+  const int st = a.stride;
+  const int py = (MODE == MODE_TRANS) ? cls / st : 0;
+  const int px_ = (MODE == MODE_TRANS) ? cls % st : 0;
+  const int Pc = a.Pc, Qc = a.Qc;
+  const int Mtot = a.N * Pc * Qc;
+  const int m0 = mblk * BM;
+  const int n0 = nblk * BN;
+
+  TapIter ti;
+  if constexpr (MODE == MODE_TRANS) {
+    ti.st = st;
+    ti.r0 = (py + a.pad) % st;
+    ti.s0 = (px_ + a.pad) % st;
+    ti.nr = (a.R - ti.r0 + st - 1) / st;
+    ti.ns = (a.S - ti.s0 + st - 1) / st;
+  } else if constexpr (ALOAD == ALOAD_STEM) {
+    ti.st = 1; ti.r0 = 0; ti.s0 = 0; ti.nr = 1; ti.ns = 1;  // one K step of 64 taps
+  } else {
+    ti.st = 1; ti.r0 = 0; ti.s0 = 0; ti.nr = a.R; ti.ns = a.S;
+  }
+  const int cchunks = (ALOAD == ALOAD_STEM) ? 1 : a.C / BK;
+  const int KT = ti.nr * ti.ns * cchunks;
+  const int Ktot = (ALOAD == ALOAD_STEM) ? 64 : a.R * a.S * a.C;  // packed weight row length
+
+  // ---- per-thread A-row bookkeeping (fixed rows across K steps) ----
+  const int ach = tid % CPR;
+  int an[A_PASSES], aa[A_PASSES], ab[A_PASSES];
+#pragma unroll
+  for (int i = 0; i < A_PASSES; ++i) {
+    const int row = tid / CPR + i * A_ROWS_PER_PASS;
+    const int m = m0 + row;
+    if (row < BM && m < Mtot) {
+      const int n = m / (Pc * Qc);
+      const int rem = m - n * (Pc * Qc);
+      an[i] = n;
+      aa[i] = rem / Qc;
+      ab[i] = rem - aa[i] * Qc;
+    } else {
+      an[i] = -1; aa[i] = 0; ab[i] = 0;
+    }
+  }
+
+  uint4 ra[A_PASSES];
+  uint4 rb[B_PASSES];
+
+  auto load_tiles = [&](int kt) {
+    const int cc = kt % cchunks;
+    const int tap = kt / cchunks;
+    const int jr = tap / ti.ns, js = tap - jr * ti.ns;
+    const int r = ti.r0 + ti.st * jr;
+    const int s = ti.s0 + ti.st * js;
+    const int c0 = cc * BK;
+    // activations
+#pragma unroll
+    for (int i = 0; i < A_PASSES; ++i) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      const int row = tid / CPR + i * A_ROWS_PER_PASS;
+      if (row < BM && an[i] >= 0) {
+        if constexpr (ALOAD == ALOAD_STEM) {
+          // im2col of the fp32 image: k = ach*8 + e -> (kr, ks) = (k/7, k%7)
+          const float* img = reinterpret_cast<const float*>(a.x);
+          float f[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int k = ach * 8 + e;
+            const int kr = k / 7, ks = k - kr * 7;
+            const int ih = aa[i] * st - a.pad + kr;
+            const int iw = ab[i] * st - a.pad + ks;
+            f[e] = (k < 49 && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+                       ? img[((size_t)an[i] * a.H + ih) * a.W + iw] : 0.f;
+          }
+          v = pack8(f);
+        } else {
+          int ih, iw;
+          if constexpr (MODE == MODE_FWD) {
+            ih = aa[i] * st - a.pad + r;
+            iw = ab[i] * st - a.pad + s;
+          } else {
+            ih = aa[i] + (py + a.pad - r) / st;
+            iw = ab[i] + (px_ + a.pad - s) / st;
+          }
+          if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) {
+            const bf16_t* p = a.x + ((size_t)(an[i] * a.H + ih) * a.W + iw) * a.ldx + c0 + ach * 8;
+            v = *reinterpret_cast<const uint4*>(p);
+          }
+        }
+      }
+      ra[i] = v;
+    }
+    // packed weights [Cout][Ktot], k = (r*S + s)*C + c
+    const int kbase = (ALOAD == ALOAD_STEM) ? 0 : (r * a.S + s) * a.C + c0;
+#pragma unroll
+    for (int i = 0; i < B_PASSES; ++i) {
+      const int row = tid / CPR + i * A_ROWS_PER_PASS;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (row < BN && n0 + row < a.Cout) {
+        v = *reinterpret_cast<const uint4*>(a.w + (size_t)(n0 + row) * Ktot + kbase + ach * 8);
+      }
+      rb[i] = v;
+    }
+  };
+
+  auto store_tiles = [&](int buf) {
+    char* As = smem + buf * STAGE;
+    char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < A_PASSES; ++i) {
+      const int row = tid / CPR + i * A_ROWS_PER_PASS;
+      if (row < BM) *reinterpret_cast<uint4*>(As + frag_off<BK>(row, ach)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_PASSES; ++i) {
+      const int row = tid / CPR + i * A_ROWS_PER_PASS;
+      if (row < BN) *reinterpret_cast<uint4*>(Bs + frag_off<BK>(row, ach)) = rb[i];
+    }
+  };
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (KT > 0) {  // KT == 0: a stride-2 parity class with no taps (1x1 s2 dgrad)
+    load_tiles(0);
+    store_tiles(0);
+  }
+  __syncthreads();
+
+  for (int kt = 0; kt < KT; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < KT) load_tiles(kt + 1);
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int ch = kk * 4 + (lane >> 4);
+      bf16x8 wf[FN], xf[FM];
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+        wf[i] = *reinterpret_cast<const bf16x8*>(Bs + frag_off<BK>(wn * WTN + i * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+        xf[j] = *reinterpret_cast<const bf16x8*>(As + frag_off<BK>(wm * WTM + j * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < KT) store_tiles(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: bias, addend, bf16 store, BN partial sums ----
+  float csum[FN][4], csq[FN][4];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { csum[i][e] = 0.f; csq[i][e] = 0.f; }
+
+#pragma unroll
+  for (int j = 0; j < FM; ++j) {
+    const int m = m0 + wm * WTM + j * 16 + (lane & 15);
+    const bool mvalid = m < Mtot;
+    size_t yoff = 0, aoff = 0;
+    if (mvalid) {
+      const int n = m / (Pc * Qc);
+      const int rem = m - n * (Pc * Qc);
+      const int pa = rem / Qc, pb = rem - pa * Qc;
+      const int oh = (MODE == MODE_TRANS) ? pa * st + py : pa;
+      const int ow = (MODE == MODE_TRANS) ? pb * st + px_ : pb;
+      const size_t pix = (size_t)(n * a.P + oh) * a.Q + ow;
+      yoff = pix * a.ldy;
+      aoff = pix * a.ldadd;
+    }
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+      const int co = n0 + wn * WTN + i * 16 + ((lane >> 4) << 2);
+      if (mvalid && co < a.Cout) {
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if (a.bias) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += a.bias[co + e];
+        }
+        if (a.add) {
+          const uint2 u = *reinterpret_cast<const uint2*>(a.add + aoff + co);
+          v[0] += __uint_as_float(u.x << 16); v[1] += __uint_as_float(u.x & 0xffff0000u);
+          v[2] += __uint_as_float(u.y << 16); v[3] += __uint_as_float(u.y & 0xffff0000u);
+        }
+        uint2 o;
+        o.x = pack_bf2(v[0], v[1]);
+        o.y = pack_bf2(v[2], v[3]);
+        *reinterpret_cast<uint2*>(a.y + yoff + co) = o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { csum[i][e] += v[e]; csq[i][e] += v[e] * v[e]; }
+      }
+    }
+  }
+
+  if (a.stats) {
+    // reduce over the 16 pixel lanes sharing (lane>>4), then over the WM waves
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          csum[i][e] += __shfl_xor(csum[i][e], o, 64);
+          csq[i][e] += __shfl_xor(csq[i][e], o, 64);
+        }
+      }
+    float* red = reinterpret_cast<float*>(smem);  // [WM][BN][2]
+    __syncthreads();
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int cl = wn * WTN + i * 16 + ((lane >> 4) << 2) + e;
+          red[(wm * BN + cl) * 2 + 0] = csum[i][e];
+          red[(wm * BN + cl) * 2 + 1] = csq[i][e];
+        }
+    }
+    __syncthreads();
+    for (int cl = tid; cl < BN; cl += 256) {
+      const int co = n0 + cl;
+      if (co < a.Cout) {
+        float s = 0.f, q = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) { s += red[(w * BN + cl) * 2]; q += red[(w * BN + cl) * 2 + 1]; }
+        atomicAdd(a.stats + co, (double)s);
+        atomicAdd(a.stats + a.Cout + co, (double)q);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// weight gradient
+// ---------------------------------------------------------------------------
+// [pixel][channel] tile, 32-B units XOR-swizzled per row so that every
+// ds_read_b64_tr_b16 half-wave (rows {8g..8g+3} x 2 groups) and every
+// ds_write_b128 row sweep is bank-conflict free.
+template <int TC>  // channels per tile row: 32 or 64 per panel
+__device__ __forceinline__ int tr_off(int row, int col) {
+  if constexpr (TC == 32) {
+    const int unit = col >> 4;
+    return row * 64 + (((unit ^ ((row >> 3) & 1))) << 5) + ((col & 15) << 1);
+  } else {
+    const int panel = col >> 6;
+    const int c = col & 63;
+    const int unit = c >> 4;
+    const int f = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+    (void)panel;
+    return row * 128 + ((unit ^ f) << 5) + ((c & 15) << 1);
+  }
+}
+
+template <int TC, int NCOL, int ROWS>
+struct TrTile {
+  // byte offset of (row, col) inside a tile of ROWS rows x NCOL channels,
+  // made of NCOL/TC panels of TC channels each.
+  static __device__ __forceinline__ int off(int row, int col) {
+    const int panel = col / TC;
+    return panel * (ROWS * TC * 2) + tr_off<TC>(row, col % TC);
+  }
+};
+
+__device__ __forceinline__ bf16x8 tr_read8(const char* base_lo, const char* base_hi) {
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, base_lo));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, base_hi));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+template <int XLOAD, int BMO, int BNC, int BKP, int WM, int WN>
+__global__ void __launch_bounds__(256)
+conv_wgrad_kernel(ConvWgradArgs a) {
+  constexpr int TCA = BMO >= 64 ? 64 : 32;
+  constexpr int TCB = BNC >= 64 ? 64 : 32;
+  constexpr int WTM = BMO / WM;
+  constexpr int WTN = BNC / WN;
+  constexpr int FM = WTM / 16;
+  constexpr int FN = WTN / 16;
+  static_assert(WM * WN == 4, "4 waves");
+  constexpr int A_BYTES = BKP * BMO * 2;
+  constexpr int B_BYTES = BKP * BNC * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int ACPR = BMO / 8;  // 16-B chunks per dY pixel row
+  constexpr int BCPR = BNC / 8;
+  constexpr int A_LOADS = (BKP * ACPR + 255) / 256;
+  constexpr int B_LOADS = (BKP * BCPR + 255) / 256;
+  typedef TrTile<TCA, BMO, BKP> TA;
+  typedef TrTile<TCB, BNC, BKP> TB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int cob = blockIdx.x % a.co_blocks;
+  const int rest = blockIdx.x / a.co_blocks;
+  const int cblk = rest % a.c_blocks;
+  const int tap = rest / a.c_blocks;
+  const int co0 = cob * BMO;
+  const int c0 = cblk * BNC;
+  const int r = (XLOAD == XLOAD_STEM) ? 0 : tap / a.S;
+  const int s = (XLOAD == XLOAD_STEM) ? 0 : tap - r * a.S;
+  const int PQ = a.P * a.Q;
+  const int Mtot = a.N * PQ;
+  const int mbeg = blockIdx.z * a.px_per_split;
+  const int mend = min(Mtot, mbeg + a.px_per_split);
+  const int KT = (mend - mbeg + BKP - 1) / BKP;
+
+  uint4 ra[A_LOADS], rb[B_LOADS];
+
+  auto load_tiles = [&](int kt) {
+    const int kb = mbeg + kt * BKP;
+#pragma unroll
+    for (int i = 0; i < A_LOADS; ++i) {
+      const int idx = tid + i * 256;
+      const int row = idx / ACPR, ch = idx % ACPR;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      const int m = kb + row;
+      if (row < BKP && m < mend && co0 + ch * 8 < a.Cout)
+        v = *reinterpret_cast<const uint4*>(a.dy + (size_t)m * a.lddy + co0 + ch * 8);
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < B_LOADS; ++i) {
+      const int idx = tid + i * 256;
+      const int row = idx / BCPR, ch = idx % BCPR;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      const int m = kb + row;
+      if (row < BKP && m < mend) {
+        const int n = m / PQ;
+        const int rem = m - n * PQ;
+        const int p = rem / a.Q, q = rem - p * a.Q;
+        if constexpr (XLOAD == XLOAD_STEM) {
+          const float* img = reinterpret_cast<const float*>(a.x);
+          float f[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int k = c0 + ch * 8 + e;
+            const int kr = k / 7, ks = k - kr * 7;
+            const int ih = p * a.stride - a.pad + kr, iw = q * a.stride - a.pad + ks;
+            f[e] = (k < 49 && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+                       ? img[((size_t)n * a.H + ih) * a.W + iw] : 0.f;
+          }
+          v = pack8(f);
+        } else {
+          const int ih = p * a.stride - a.pad + r, iw = q * a.stride - a.pad + s;
+          if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W && c0 + ch * 8 < a.C)
+            v = *reinterpret_cast<const uint4*>(a.x + ((size_t)(n * a.H + ih) * a.W + iw) * a.ldx + c0 + ch * 8);
+        }
+      }
+      rb[i] = v;
+    }
+  };
+  auto store_tiles = [&](int buf) {
+    char* As = smem + buf * STAGE;
+    char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < A_LOADS; ++i) {
+      const int idx = tid + i * 256;
+      const int row = idx / ACPR, ch = idx % ACPR;
+      if (row < BKP) *reinterpret_cast<uint4*>(As + TA::off(row, ch * 8)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_LOADS; ++i) {
+      const int idx = tid + i * 256;
+      const int row = idx / BCPR, ch = idx % BCPR;
+      if (row < BKP) *reinterpret_cast<uint4*>(Bs + TB::off(row, ch * 8)) = rb[i];
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (KT > 0) {
+    load_tiles(0);
+    store_tiles(0);
+  }
+  __syncthreads();
+  const int g = lane >> 4, li = lane & 15;
+  const int trq = li >> 2, trp = li & 3;
+  for (int kt = 0; kt < KT; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < KT) load_tiles(kt + 1);
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < BKP / 32; ++kk) {
+      const int row_lo = kk * 32 + 8 * g + trq;
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int col = wm * WTM + i * 16 + 4 * trp;
+        af[i] = tr_read8(As + TA::off(row_lo, col), As + TA::off(row_lo + 4, col));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = wn * WTN + j * 16 + 4 * trp;
+        bfr[j] = tr_read8(Bs + TB::off(row_lo, col), Bs + TB::off(row_lo + 4, col));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < KT) store_tiles(buf ^ 1);
+    __syncthreads();
+  }
+  if (KT == 0) return;
+
+  // D[co][c]: lane holds column c = .. + li, rows co = .. + 4g + e
+  const int Krow = (XLOAD == XLOAD_STEM) ? 64 : a.R * a.S * a.C;
+  const int kcol0 = (XLOAD == XLOAD_STEM) ? 0 : tap * a.C;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int c = c0 + wn * WTN + j * 16 + li;
+      const int cmax = (XLOAD == XLOAD_STEM) ? 64 : a.C;
+      if (c < cmax) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int co = co0 + wm * WTM + i * 16 + 4 * g + e;
+          if (co < a.Cout) atomicAdd(a.dw + (size_t)co * Krow + kcol0 + c, acc[i][j][e]);
+        }
+      }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host-side launch selection
+// ---------------------------------------------------------------------------
+template <int MODE, int ALOAD, int BM, int BN, int BK, int WM, int WN>
+static hipError_t launch_fwd_cfg(const ConvFwdArgs& a0, int classes, hipStream_t st) {
+  ConvFwdArgs a = a0;
+  a.nblocks = (a.Cout + BN - 1) / BN;
+  const int M = a.N * a.Pc * a.Qc;
+  a.mblocks = (M + BM - 1) / BM;
+  const size_t lds = 2 * (size_t)(BM + BN) * BK * 2;
+  size_t need = lds;
+  const size_t red = (size_t)WM * BN * 2 * sizeof(float);
+  if (red > need) need = red;
+  dim3 grid(a.mblocks * a.nblocks, 1, classes);
+  hipLaunchKernelGGL((conv_fwd_kernel<MODE, ALOAD, BM, BN, BK, WM, WN>), grid, dim3(256), need, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_conv_fwd(const ConvFwdArgs& a0, int mode, hipStream_t st) {
+  ConvFwdArgs a = a0;
+  int classes = 1;
+  if (mode == MODE_TRANS) {
+    if (a.P % a.stride || a.Q % a.stride) return hipErrorInvalidValue;
+    a.Pc = a.P / a.stride;
+    a.Qc = a.Q / a.stride;
+    classes = a.stride * a.stride;
+  } else {
+    a.Pc = a.P;
+    a.Qc = a.Q;
+  }
+  if (mode == MODE_STEM) {
+    return launch_fwd_cfg<MODE_FWD, ALOAD_STEM, 128, 64, 64, 2, 2>(a, 1, st);
+  }
+  if (a.C % 32) return hipErrorInvalidValue;
+  const bool bk64 = (a.C % 64) == 0;
+  const int M = a.N * a.Pc * a.Qc * classes;
+#define SEL(MD)                                                                              \
+  if (a.Cout <= 32) {                                                                        \
+    return bk64 ? launch_fwd_cfg<MD, ALOAD_NHWC, 128, 32, 64, 4, 1>(a, classes, st)          \
+                : launch_fwd_cfg<MD, ALOAD_NHWC, 128, 32, 32, 4, 1>(a, classes, st);         \
+  } else if (a.Cout <= 64 || M < 32768) {                                                    \
+    return bk64 ? launch_fwd_cfg<MD, ALOAD_NHWC, 128, 64, 64, 2, 2>(a, classes, st)          \
+                : launch_fwd_cfg<MD, ALOAD_NHWC, 128, 64, 32, 2, 2>(a, classes, st);         \
+  } else {                                                                                   \
+    return bk64 ? launch_fwd_cfg<MD, ALOAD_NHWC, 128, 128, 64, 2, 2>(a, classes, st)         \
+                : launch_fwd_cfg<MD, ALOAD_NHWC, 128, 128, 32, 2, 2>(a, classes, st);        \
+  }
+  if (mode == MODE_FWD) { SEL(MODE_FWD) } else { SEL(MODE_TRANS) }
+#undef SEL
+}
+
+template <int XLOAD, int BMO, int BNC, int BKP, int WM, int WN>
+static hipError_t launch_wgrad_cfg(const ConvWgradArgs& a0, hipStream_t st) {
+  ConvWgradArgs a = a0;
+  a.co_blocks = (a.Cout + BMO - 1) / BMO;
+  const int ccount = (XLOAD == XLOAD_STEM) ? 64 : a.C;
+  a.c_blocks = (ccount + BNC - 1) / BNC;
+  const int taps = (XLOAD == XLOAD_STEM) ? 1 : a.R * a.S;
+  const int tiles = a.co_blocks * a.c_blocks * taps;
+  const long long M = (long long)a.N * a.P * a.Q;
+  // split-K over pixels: enough blocks to fill 256 CUs, but keep >= 1024 flop per
+  // fp32 atomic byte (chip atomic rate ~1.3 TB/s, MI355X_MICROARCH.md).
+  long long splits = (2048 + tiles - 1) / tiles;
+  const long long max_by_atomic = M / 512 > 0 ? M / 512 : 1;  // >= 512 px per block
+  if (splits > max_by_atomic) splits = max_by_atomic;
+  if (splits < 1) splits = 1;
+  long long per = (M + splits - 1) / splits;
+  per = (per + BKP - 1) / BKP * BKP;
+  splits = (M + per - 1) / per;
+  a.px_per_split = (int)per;
+  dim3 grid(tiles, 1, (unsigned)splits);
+  const size_t lds = 2 * (size_t)BKP * (BMO + BNC) * 2;
+  hipLaunchKernelGGL((conv_wgrad_kernel<XLOAD, BMO, BNC, BKP, WM, WN>), grid, dim3(256), lds, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st) {
+  if (stem) return launch_wgrad_cfg<XLOAD_STEM, 64, 64, 64, 2, 2>(a, st);
+  if (a.C % 32 || a.Cout % 32) return hipErrorInvalidValue;
+  const bool co64 = a.Cout % 64 == 0, c64 = a.C % 64 == 0;
+  if (a.Cout >= 128 && a.C >= 128)
+    return launch_wgrad_cfg<XLOAD_NHWC, 128, 128, 32, 2, 2>(a, st);
+  if (co64 && c64) return launch_wgrad_cfg<XLOAD_NHWC, 64, 64, 64, 2, 2>(a, st);
+  if (co64) return launch_wgrad_cfg<XLOAD_NHWC, 64, 32, 64, 4, 1>(a, st);
+  if (c64) return launch_wgrad_cfg<XLOAD_NHWC, 32, 64, 64, 1, 4>(a, st);
+  return launch_wgrad_cfg<XLOAD_NHWC, 32, 32, 64, 2, 2>(a, st);
+}
+
+}  // namespace unet

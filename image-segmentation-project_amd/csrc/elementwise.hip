@@ -1,0 +1,717 @@
+// HBM-bound kernels of the U-Net hot path (gfx950): BatchNorm apply / backward,
+// residual add + ReLU, maxpool 3/2/1, the fused upconv0+conv_final head, the
+// pixel-wise BCE/Dice loss + mask metrics, and weight (un)packing.
+//
+// Every activation access is 16 B per lane (8 bf16 channels, NHWC) so one
+// wave instruction moves 1 KiB; per-channel reductions are kept in registers
+// per thread (each thread owns one 8-channel chunk for its whole pixel loop),
+// folded through LDS once per block and published with fp64 atomics.
+#include "common.h"
+#include "kernels.h"
+
+namespace unet {
+
+constexpr float kMaskThreshold = 8.94069742685133e-08f;  // 0x33C00001, SURVEY.md §0
+
+static inline int grid_for(int64_t work, int per_block, int cap = 2048) {
+  int64_t g = (work + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+// ---------------------------------------------------------------------------
+// BN apply (+ residual) (+ ReLU), forward.  Block 0 also finalises the batch
+// statistics: save_mean/save_invstd for the backward and the running stats
+// (momentum 0.1, unbiased variance), matching torch.nn.BatchNorm2d training.
+// ---------------------------------------------------------------------------
+__device__ void bn_finalize_block0(const BnLaunch& p, int tid, int nthreads) {
+  for (int c = tid; c < p.C; c += nthreads) {
+    float sc, sh, m, inv, var;
+    bn_scale_shift(p, c, sc, sh, m, inv, var);
+    if (p.training) {
+      p.save_mean[c] = m;
+      p.save_invstd[c] = inv;
+      const double n = p.count;
+      const float unb = (float)((double)var * (n / (n > 1.0 ? n - 1.0 : 1.0)));
+      p.run_mean[c] = (1.f - p.momentum) * p.run_mean[c] + p.momentum * m;
+      p.run_var[c] = (1.f - p.momentum) * p.run_var[c] + p.momentum * unb;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) bn_apply_kernel(BnApplyArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* sc1 = sm;
+  float* sh1 = sm + a.C;
+  float* sc2 = sm + 2 * a.C;
+  float* sh2 = sm + 3 * a.C;
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+    float m, inv, var;
+    bn_scale_shift(a.bn, c, sc1[c], sh1[c], m, inv, var);
+    if (a.res_mode == 2) bn_scale_shift(a.bn2, c, sc2[c], sh2[c], m, inv, var);
+  }
+  __syncthreads();
+  const int CC = a.C >> 3;
+  const int64_t total = a.npix * CC;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t pix = e / CC;
+    const int c8 = (int)(e - pix * CC) << 3;
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4*>(a.y + pix * a.ldy + c8), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = v[k] * sc1[c8 + k] + sh1[c8 + k];
+    if (a.res_mode) {
+      float r[8];
+      unpack8(*reinterpret_cast<const uint4*>(a.res + pix * a.ldr + c8), r);
+      if (a.res_mode == 2) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] = r[k] * sc2[c8 + k] + sh2[c8 + k];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += r[k];
+    }
+    if (a.relu) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
+    }
+    *reinterpret_cast<uint4*>(a.out + pix * a.ldo + c8) = pack8(v);
+  }
+  if (blockIdx.x == 0) {
+    __syncthreads();
+    bn_finalize_block0(a.bn, threadIdx.x, blockDim.x);
+    if (a.res_mode == 2) bn_finalize_block0(a.bn2, threadIdx.x, blockDim.x);
+  }
+}
+
+hipError_t launch_bn_apply(const BnApplyArgs& a, hipStream_t st) {
+  if (a.C % 8) return hipErrorInvalidValue;
+  const int64_t total = a.npix * (a.C / 8);
+  const int g = grid_for(total, 256 * 4);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(g), dim3(256), 4 * a.C * sizeof(float), st, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// BN backward.  Thread layout: chunk = tid % CC (8 channels), row = tid / CC;
+// each thread keeps its channel sums in registers over its pixel stride.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void load_dz(const BnBwdArgs& a, int64_t pix, int c8, float* dz) {
+  unpack8(*reinterpret_cast<const uint4*>(a.da + pix * a.ldda + c8), dz);
+  if (a.relu) {
+    float av[8];
+    unpack8(*reinterpret_cast<const uint4*>(a.act + pix * a.ldact + c8), av);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dz[k] = av[k] > 0.f ? dz[k] : 0.f;
+  }
+}
+
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a) {
+  const int CC = a.C >> 3;
+  const int rows = blockDim.x / CC;
+  const int chunk = threadIdx.x % CC;
+  const int row = threadIdx.x / CC;
+  const int c8 = chunk << 3;
+  const bool two = a.y2 != nullptr;
+  float s1[8], s2[8], t2[8];
+  float mu[8], is[8], mu2[8], is2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    s1[k] = s2[k] = t2[k] = 0.f;
+    mu[k] = a.mean[c8 + k]; is[k] = a.invstd[c8 + k];
+    mu2[k] = two ? a.mean2[c8 + k] : 0.f; is2[k] = two ? a.invstd2[c8 + k] : 0.f;
+  }
+  if (row < rows) {
+    for (int64_t pix = (int64_t)blockIdx.x * rows + row; pix < a.npix; pix += (int64_t)gridDim.x * rows) {
+      float dz[8], y[8];
+      load_dz(a, pix, c8, dz);
+      unpack8(*reinterpret_cast<const uint4*>(a.y + pix * a.ldy + c8), y);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { s1[k] += dz[k]; s2[k] += dz[k] * (y[k] - mu[k]) * is[k]; }
+      if (two) {
+        unpack8(*reinterpret_cast<const uint4*>(a.y2 + pix * a.ldy2 + c8), y);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t2[k] += dz[k] * (y[k] - mu2[k]) * is2[k];
+      }
+    }
+  }
+  // fold rows through LDS: red[row][C]
+  extern __shared__ __attribute__((aligned(16))) float red[];
+  const int nsum = two ? 3 : 2;
+  for (int q = 0; q < nsum; ++q) {
+    const float* src = q == 0 ? s1 : (q == 1 ? s2 : t2);
+    if (row < rows) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[row * a.C + c8 + k] = src[k];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+      float acc = 0.f;
+      for (int r = 0; r < rows; ++r) acc += red[r * a.C + c];
+      double* dst = q == 0 ? a.sums : (q == 1 ? a.sums + a.C : a.sums2 + a.C);
+      atomicAdd(dst + c, (double)acc);
+    }
+    __syncthreads();
+  }
+}
+
+hipError_t launch_bn_bwd_reduce(const BnBwdArgs& a, hipStream_t st) {
+  if (a.C % 8 || a.C / 8 > 256) return hipErrorInvalidValue;
+  const int CC = a.C / 8;
+  const int rows = 256 / CC;
+  const int threads = rows * CC;
+  const int g = grid_for(a.npix, rows * 8, 1024);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(g), dim3(threads), (size_t)rows * a.C * sizeof(float), st, a);
+  return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, double inv_n) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  // per channel: k1 = gamma*invstd, m1 = mean(dZ), m2 = mean(dZ*xhat), mu, invstd (x2 for bn2)
+  float* k1 = sm;
+  float* m1 = sm + a.C;
+  float* m2 = sm + 2 * a.C;
+  float* mu = sm + 3 * a.C;
+  float* is = sm + 4 * a.C;
+  float* k1b = sm + 5 * a.C;
+  float* m2b = sm + 6 * a.C;
+  float* mub = sm + 7 * a.C;
+  float* isb = sm + 8 * a.C;
+  const bool two = a.y2 != nullptr;
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+    k1[c] = a.gamma[c] * a.invstd[c];
+    m1[c] = (float)(a.sums[c] * inv_n);
+    m2[c] = (float)(a.sums[a.C + c] * inv_n);
+    mu[c] = a.mean[c];
+    is[c] = a.invstd[c];
+    if (two) {
+      k1b[c] = a.gamma2[c] * a.invstd2[c];
+      m2b[c] = (float)(a.sums2[a.C + c] * inv_n);
+      mub[c] = a.mean2[c];
+      isb[c] = a.invstd2[c];
+    }
+    if (blockIdx.x == 0) {
+      a.dgamma[c] = (float)a.sums[a.C + c];
+      a.dbeta[c] = (float)a.sums[c];
+      if (two) {
+        a.dgamma2[c] = (float)a.sums2[a.C + c];
+        a.dbeta2[c] = (float)a.sums[c];  // same dZ feeds both BNs
+      }
+    }
+  }
+  __syncthreads();
+  const int CC = a.C >> 3;
+  const int64_t total = a.npix * CC;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t pix = e / CC;
+    const int c8 = (int)(e - pix * CC) << 3;
+    float dz[8], y[8], o[8];
+    load_dz(a, pix, c8, dz);
+    unpack8(*reinterpret_cast<const uint4*>(a.y + pix * a.ldy + c8), y);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = c8 + k;
+      o[k] = k1[c] * (dz[k] - m1[c] - (y[k] - mu[c]) * is[c] * m2[c]);
+    }
+    *reinterpret_cast<uint4*>(a.dy + pix * a.lddy + c8) = pack8(o);
+    if (two) {
+      unpack8(*reinterpret_cast<const uint4*>(a.y2 + pix * a.ldy2 + c8), y);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int c = c8 + k;
+        o[k] = k1b[c] * (dz[k] - m1[c] - (y[k] - mub[c]) * isb[c] * m2b[c]);
+      }
+      *reinterpret_cast<uint4*>(a.dy2 + pix * a.lddy2 + c8) = pack8(o);
+    }
+    if (a.dres) *reinterpret_cast<uint4*>(a.dres + pix * a.lddres + c8) = pack8(dz);
+  }
+}
+
+hipError_t launch_bn_bwd_apply(const BnBwdArgs& a, hipStream_t st) {
+  if (a.C % 8) return hipErrorInvalidValue;
+  const int64_t total = a.npix * (a.C / 8);
+  const int g = grid_for(total, 256 * 4);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(g), dim3(256), 9 * a.C * sizeof(float), st, a,
+                     1.0 / (double)a.npix);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// MaxPool2d(3, 2, 1): torch CPU semantics — first maximum in (kh, kw) scan
+// order wins (strict >), NaN propagates.  Index 0..8 kept as uint8.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) maxpool_fwd_kernel(MaxPoolArgs a) {
+  const int CC = a.C >> 3;
+  const int64_t total = (int64_t)a.N * a.P * a.Q * CC;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t opix = e / CC;
+    const int c8 = (int)(e - opix * CC) << 3;
+    const int q = (int)(opix % a.Q);
+    const int p = (int)((opix / a.Q) % a.P);
+    const int n = (int)(opix / ((int64_t)a.P * a.Q));
+    float best[8];
+    int bi[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; bi[k] = -1; }
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = 2 * p - 1 + kh;
+      if (ih < 0 || ih >= a.H) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int iw = 2 * q - 1 + kw;
+        if (iw < 0 || iw >= a.W) continue;
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4*>(a.x + ((int64_t)(n * a.H + ih) * a.W + iw) * a.ldx + c8), v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (bi[k] < 0 || v[k] > best[k] || (v[k] != v[k] && best[k] == best[k])) {
+            best[k] = v[k];
+            bi[k] = kh * 3 + kw;
+          }
+        }
+      }
+    }
+    *reinterpret_cast<uint4*>(a.y + opix * a.ldy + c8) = pack8(best);
+    uint2 ix;
+    ix.x = (unsigned)bi[0] | ((unsigned)bi[1] << 8) | ((unsigned)bi[2] << 16) | ((unsigned)bi[3] << 24);
+    ix.y = (unsigned)bi[4] | ((unsigned)bi[5] << 8) | ((unsigned)bi[6] << 16) | ((unsigned)bi[7] << 24);
+    *reinterpret_cast<uint2*>(a.idx + opix * a.C + c8) = ix;
+  }
+}
+
+__global__ void __launch_bounds__(256) maxpool_bwd_kernel(MaxPoolArgs a) {
+  const int CC = a.C >> 3;
+  const int64_t total = (int64_t)a.N * a.H * a.W * CC;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t ipix = e / CC;
+    const int c8 = (int)(e - ipix * CC) << 3;
+    const int w = (int)(ipix % a.W);
+    const int h = (int)((ipix / a.W) % a.H);
+    const int n = (int)(ipix / ((int64_t)a.H * a.W));
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    const int p_lo = h >= 1 ? h / 2 : 0;   // windows with 2p-1 <= h <= 2p+1
+    const int p_hi = min((h + 1) / 2, a.P - 1);
+    const int q_lo = w >= 1 ? w / 2 : 0;
+    const int q_hi = min((w + 1) / 2, a.Q - 1);
+    for (int p = p_lo; p <= p_hi; ++p) {
+      const int kh = h - (2 * p - 1);
+      if (kh < 0 || kh > 2) continue;
+      for (int q = q_lo; q <= q_hi; ++q) {
+        const int kw = w - (2 * q - 1);
+        if (kw < 0 || kw > 2) continue;
+        const int64_t opix = ((int64_t)n * a.P + p) * a.Q + q;
+        const uint2 ix = *reinterpret_cast<const uint2*>(a.idx + opix * a.C + c8);
+        float g[8];
+        unpack8(*reinterpret_cast<const uint4*>(a.dy + opix * a.lddy + c8), g);
+        const int want = kh * 3 + kw;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const unsigned word = k < 4 ? ix.x : ix.y;
+          const int b = (word >> ((k & 3) * 8)) & 0xff;
+          if (b == want) acc[k] += g[k];
+        }
+      }
+    }
+    if (a.add) {
+      float r[8];
+      unpack8(*reinterpret_cast<const uint4*>(a.add + ipix * a.ldadd + c8), r);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += r[k];
+    }
+    *reinterpret_cast<uint4*>(a.dx + ipix * a.lddx + c8) = pack8(acc);
+  }
+}
+
+hipError_t launch_maxpool_fwd(const MaxPoolArgs& a, hipStream_t st) {
+  if (a.C % 8) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)a.N * a.P * a.Q * (a.C / 8);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total, 256 * 2)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+hipError_t launch_maxpool_bwd(const MaxPoolArgs& a, hipStream_t st) {
+  if (a.C % 8) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)a.N * a.H * a.W * (a.C / 8);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total, 256 * 2)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Fused head: upconv0 (ConvTranspose2d k2s2, Cin->Co) + conv_final (1x1, Co->1).
+// No non-linearity sits between the two (advanced_models.py:337-350), so the
+// pair contracts to V[c][ab] = sum_o Wf[o] W0[c][o][ab] and a constant.
+// ---------------------------------------------------------------------------
+constexpr int kHeadMaxCin = 64;
+
+__device__ void head_contract(const HeadArgs& a, float* V, float* cst) {
+  for (int t = threadIdx.x; t < a.Cin * 4; t += blockDim.x) {
+    const int c = t >> 2, ab = t & 3;
+    float v = 0.f;
+    for (int o = 0; o < a.Co; ++o) v += a.wf[o] * a.w0[((size_t)c * a.Co + o) * 4 + ab];
+    V[t] = v;
+  }
+  if (threadIdx.x == 0) {
+    float c0 = a.bf[0];
+    for (int o = 0; o < a.Co; ++o) c0 += a.wf[o] * a.b0[o];
+    *cst = c0;
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) head_fwd_kernel(HeadArgs a) {
+  __shared__ float V[kHeadMaxCin * 4];
+  __shared__ float cst;
+  head_contract(a, V, &cst);
+  const int64_t total = (int64_t)a.N * a.H * a.W;
+  for (int64_t pix = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; pix < total;
+       pix += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(pix % a.W);
+    const int i = (int)((pix / a.W) % a.H);
+    const int n = (int)(pix / ((int64_t)a.H * a.W));
+    float o[4] = {cst, cst, cst, cst};
+    for (int c8 = 0; c8 < a.Cin; c8 += 8) {
+      float x[8];
+      unpack8(*reinterpret_cast<const uint4*>(a.x + pix * a.ldx + c8), x);
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int ab = 0; ab < 4; ++ab) o[ab] += x[k] * V[(c8 + k) * 4 + ab];
+    }
+    const int W2 = 2 * a.W;
+    float* row0 = a.logits + ((int64_t)n * 2 * a.H + 2 * i) * W2 + 2 * j;
+    *reinterpret_cast<float2*>(row0) = make_float2(o[0], o[1]);
+    *reinterpret_cast<float2*>(row0 + W2) = make_float2(o[2], o[3]);
+  }
+}
+
+// thread = (8-channel chunk, pixel row); U[c][ab] partials live in registers.
+__global__ void __launch_bounds__(256) head_bwd_kernel(HeadArgs a) {
+  __shared__ float V[kHeadMaxCin * 4];
+  __shared__ float cst;
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [rows][Cin*4 + 1]
+  head_contract(a, V, &cst);
+  const int CC = a.Cin >> 3;
+  const int rows = blockDim.x / CC;
+  const int chunk = threadIdx.x % CC, row = threadIdx.x / CC;
+  const int c8 = chunk << 3;
+  const int64_t total = (int64_t)a.N * a.H * a.W;
+  float U[8][4];
+  float S = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+#pragma unroll
+    for (int ab = 0; ab < 4; ++ab) U[k][ab] = 0.f;
+  float Vl[8][4];
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+#pragma unroll
+    for (int ab = 0; ab < 4; ++ab) Vl[k][ab] = V[(c8 + k) * 4 + ab];
+  const int W2 = 2 * a.W;
+  if (row < rows) {
+    for (int64_t pix = (int64_t)blockIdx.x * rows + row; pix < total; pix += (int64_t)gridDim.x * rows) {
+      const int j = (int)(pix % a.W);
+      const int i = (int)((pix / a.W) % a.H);
+      const int n = (int)(pix / ((int64_t)a.H * a.W));
+      const float* row0 = a.dl + ((int64_t)n * 2 * a.H + 2 * i) * W2 + 2 * j;
+      const float2 d01 = *reinterpret_cast<const float2*>(row0);
+      const float2 d23 = *reinterpret_cast<const float2*>(row0 + W2);
+      const float d[4] = {d01.x, d01.y, d23.x, d23.y};
+      if (chunk == 0) S += (d[0] + d[1]) + (d[2] + d[3]);
+      float x[8], g[8];
+      unpack8(*reinterpret_cast<const uint4*>(a.x + pix * a.ldx + c8), x);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        g[k] = d[0] * Vl[k][0] + d[1] * Vl[k][1] + d[2] * Vl[k][2] + d[3] * Vl[k][3];
+#pragma unroll
+        for (int ab = 0; ab < 4; ++ab) U[k][ab] += x[k] * d[ab];
+      }
+      *reinterpret_cast<uint4*>(a.dx + pix * a.lddx + c8) = pack8(g);
+    }
+  }
+  const int L = a.Cin * 4 + 1;
+  if (row < rows) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int ab = 0; ab < 4; ++ab) red[row * L + (c8 + k) * 4 + ab] = U[k][ab];
+    if (chunk == 0) red[row * L + a.Cin * 4] = S;
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < L; t += blockDim.x) {
+    float v = 0.f;
+    for (int r = 0; r < rows; ++r) v += red[r * L + t];
+    atomicAdd(a.usum + t, (double)v);
+  }
+}
+
+__global__ void head_grads_kernel(HeadArgs a) {
+  const double S = a.usum[a.Cin * 4];
+  for (int t = threadIdx.x; t < a.Cin * a.Co * 4; t += blockDim.x) {
+    const int ab = t & 3, o = (t >> 2) % a.Co, c = (t >> 2) / a.Co;
+    a.gw0[t] = (float)((double)a.wf[o] * a.usum[c * 4 + ab]);
+  }
+  for (int o = threadIdx.x; o < a.Co; o += blockDim.x) {
+    a.gb0[o] = (float)((double)a.wf[o] * S);
+    double g = (double)a.b0[o] * S;
+    for (int c = 0; c < a.Cin; ++c)
+      for (int ab = 0; ab < 4; ++ab) g += (double)a.w0[((size_t)c * a.Co + o) * 4 + ab] * a.usum[c * 4 + ab];
+    a.gwf[o] = (float)g;
+  }
+  if (threadIdx.x == 0) a.gbf[0] = (float)S;
+}
+
+hipError_t launch_head_fwd(const HeadArgs& a, hipStream_t st) {
+  if (a.Cin > kHeadMaxCin || a.Cin % 8) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)a.N * a.H * a.W;
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(grid_for(total, 256 * 2)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+hipError_t launch_head_bwd(const HeadArgs& a, hipStream_t st) {
+  if (a.Cin > kHeadMaxCin || a.Cin % 8) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)a.N * a.H * a.W;
+  const int CC = a.Cin / 8, rows = 256 / CC;
+  const size_t lds = (size_t)rows * (a.Cin * 4 + 1) * sizeof(float);
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(grid_for(total, rows * 8, 1024)), dim3(rows * CC), lds, st, a);
+  return hipGetLastError();
+}
+hipError_t launch_head_grads(const HeadArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(head_grads_kernel, dim3(1), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// per-channel sums (ConvTranspose bias gradients)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) channel_sum_kernel(const bf16_t* x, int ldx, int64_t npix, int C,
+                                                         double* acc) {
+  const int CC = C >> 3;
+  const int rows = blockDim.x / CC;
+  const int chunk = threadIdx.x % CC, row = threadIdx.x / CC;
+  const int c8 = chunk << 3;
+  float s[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s[k] = 0.f;
+  if (row < rows) {
+    for (int64_t pix = (int64_t)blockIdx.x * rows + row; pix < npix; pix += (int64_t)gridDim.x * rows) {
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + pix * ldx + c8), v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s[k] += v[k];
+    }
+  }
+  extern __shared__ __attribute__((aligned(16))) float red[];
+  if (row < rows) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[row * C + c8 + k] = s[k];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float t = 0.f;
+    for (int r = 0; r < rows; ++r) t += red[r * C + c];
+    atomicAdd(acc + c, (double)t);
+  }
+}
+
+hipError_t launch_channel_sum(const bf16_t* x, int ldx, int64_t npix, int C, double* acc, hipStream_t st) {
+  if (C % 8 || C / 8 > 256) return hipErrorInvalidValue;
+  const int CC = C / 8, rows = 256 / CC;
+  hipLaunchKernelGGL(channel_sum_kernel, dim3(grid_for(npix, rows * 8, 1024)), dim3(rows * CC),
+                     (size_t)rows * C * sizeof(float), st, x, ldx, npix, C, acc);
+  return hipGetLastError();
+}
+
+__global__ void d2f_kernel(const double* s, float* d, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) d[i] = (float)s[i];
+}
+hipError_t launch_d2f(const double* src, float* dst, int n, hipStream_t st) {
+  hipLaunchKernelGGL(d2f_kernel, dim3((n + 255) / 256), dim3(256), 0, st, src, dst, n);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// weight packing: fp32 torch layouts -> bf16 kernel layouts (one launch)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) pack_kernel(PackTable t) {
+  const PackEntry e = t.e[blockIdx.y];
+  const int Co = e.Co, Ci = e.Ci, R = e.R, S = e.S;
+  int64_t total;
+  if (e.kind == PK_STEM) total = (int64_t)Co * 64;
+  else total = (int64_t)Co * Ci * R * S;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    switch (e.kind) {
+      case PK_CONV_FWD: {  // dst[co][r][s][ci] <- W[co][ci][r][s]
+        const int ci = (int)(i % Ci); int64_t q = i / Ci;
+        const int s = (int)(q % S); q /= S;
+        const int r = (int)(q % R); const int co = (int)(q / R);
+        v = e.src[(((int64_t)co * Ci + ci) * R + r) * S + s];
+        break;
+      }
+      case PK_CONV_DGRAD: {  // dst[ci][r][s][co] <- W[co][ci][r][s]
+        const int co = (int)(i % Co); int64_t q = i / Co;
+        const int s = (int)(q % S); q /= S;
+        const int r = (int)(q % R); const int ci = (int)(q / R);
+        v = e.src[(((int64_t)co * Ci + ci) * R + r) * S + s];
+        break;
+      }
+      case PK_CONVT_FWD: {  // dst[co][a][b][ci] <- W[ci][co][a][b]
+        const int ci = (int)(i % Ci); int64_t q = i / Ci;
+        const int b = (int)(q % S); q /= S;
+        const int aa = (int)(q % R); const int co = (int)(q / R);
+        v = e.src[(((int64_t)ci * Co + co) * R + aa) * S + b];
+        break;
+      }
+      case PK_CONVT_DGRAD: {  // dst[ci][a][b][co] <- W[ci][co][a][b]
+        const int co = (int)(i % Co); int64_t q = i / Co;
+        const int b = (int)(q % S); q /= S;
+        const int aa = (int)(q % R); const int ci = (int)(q / R);
+        v = e.src[(((int64_t)ci * Co + co) * R + aa) * S + b];
+        break;
+      }
+      default: {  // PK_STEM: dst[co][k], k < 49 -> W[co][0][k/7][k%7]
+        const int k = (int)(i % 64), co = (int)(i / 64);
+        v = k < 49 ? e.src[(int64_t)co * 49 + k] : 0.f;
+      }
+    }
+    e.dst[i] = f2bf(v);
+  }
+}
+
+hipError_t launch_pack(const PackTable& t, hipStream_t st) {
+  if (t.n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pack_kernel, dim3(128, t.n), dim3(256), 0, st, t);
+  return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(256) unpack_kernel(UnpackTable t) {
+  const UnpackEntry e = t.e[blockIdx.y];
+  const int Co = e.Co, Ci = e.Ci, R = e.R, S = e.S;
+  const int64_t total = (int64_t)Co * Ci * R * S;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float v;
+    if (e.kind == UP_CONV) {  // dst[co][ci][r][s] <- acc[co][r][s][ci]
+      const int s = (int)(i % S); int64_t q = i / S;
+      const int r = (int)(q % R); q /= R;
+      const int ci = (int)(q % Ci); const int co = (int)(q / Ci);
+      v = e.acc[(((int64_t)co * R + r) * S + s) * Ci + ci];
+    } else if (e.kind == UP_CONVT) {  // dst W[ci][co][a][b] <- acc[ci][a][b][co]  (Ci = in ch)
+      const int b = (int)(i % S); int64_t q = i / S;
+      const int aa = (int)(q % R); q /= R;
+      const int co = (int)(q % Co); const int ci = (int)(q / Co);
+      v = e.acc[(((int64_t)ci * R + aa) * S + b) * Co + co];
+    } else {  // UP_STEM: dst[co][0][r][s] <- acc[co][r*7+s] (row length 64)
+      const int k = (int)(i % 49), co = (int)(i / 49);
+      v = e.acc[(int64_t)co * 64 + k];
+    }
+    e.dst[i] = v;
+  }
+}
+
+hipError_t launch_unpack(const UnpackTable& t, hipStream_t st) {
+  if (t.n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(unpack_kernel, dim3(64, t.n), dim3(256), 0, st, t);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// pixel-wise loss and mask metrics (losses.py:13-37,161-171; utils.py:120-151)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) loss_sums_kernel(const float* x, const float* t, int64_t n,
+                                                       double* sums, int from_prob) {
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = x[i], y = t[i];
+    float pred;
+    if (!from_prob) {
+      // torch: (1 - y) * x - log_sigmoid(x),  log_sigmoid(x) = min(x,0) - log1p(exp(-|x|))
+      const float ls = fminf(v, 0.f) - log1pf(expf(-fabsf(v)));
+      s[0] += (1.f - y) * v - ls;
+      const float sg = 1.f / (1.f + expf(-v));
+      s[1] += sg * y;
+      s[2] += sg;
+      s[3] += y;
+      pred = v >= kMaskThreshold ? 1.f : 0.f;  // == (sigmoid_cpu(v) > 0.5)
+    } else {
+      pred = v > 0.5f ? 1.f : 0.f;
+    }
+    s[4] += pred * y;
+    s[5] += pred * (1.f - y);
+    s[6] += (1.f - pred) * y;
+    s[7] += (1.f - pred) * (1.f - y);
+  }
+  __shared__ double red[4][8];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const double v = wave_sum_d((double)s[k]);
+    if (lane == 0) red[wave][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    const int k = threadIdx.x;
+    atomicAdd(sums + k, red[0][k] + red[1][k] + red[2][k] + red[3][k]);
+  }
+}
+
+hipError_t launch_loss_sums(const float* logits, const float* target, int64_t n, double* sums, int from_prob,
+                            hipStream_t st) {
+  hipLaunchKernelGGL(loss_sums_kernel, dim3(grid_for(n, 256 * 8, 1024)), dim3(256), 0, st, logits, target, n,
+                     sums, from_prob);
+  return hipGetLastError();
+}
+
+__global__ void loss_value_kernel(const double* s, int64_t n, int kind, float alpha, float smooth, float* out) {
+  if (threadIdx.x != 0) return;
+  const double bce = s[0] / (double)n;
+  const double dice = 1.0 - (2.0 * s[1] + smooth) / (s[2] + s[3] + smooth);
+  double v;
+  if (kind == LOSS_BCE) v = bce;
+  else if (kind == LOSS_DICE) v = dice;
+  else v = alpha * bce + (1.0 - alpha) * dice;
+  *out = (float)v;
+}
+hipError_t launch_loss_value(const double* sums, int64_t n, int kind, float alpha, float smooth, float* out,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(loss_value_kernel, dim3(1), dim3(64), 0, st, sums, n, kind, alpha, smooth, out);
+  return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(256) loss_grad_kernel(const float* x, const float* t, int64_t n, const double* s,
+                                                       int kind, float alpha, float smooth, const float* gscale,
+                                                       float* dl) {
+  const float g = gscale ? *gscale : 1.f;
+  const float wb = kind == LOSS_BCE ? 1.f : (kind == LOSS_COMBO ? alpha : 0.f);
+  const float wd = kind == LOSS_DICE ? 1.f : (kind == LOSS_COMBO ? 1.f - alpha : 0.f);
+  const double U = s[2] + s[3] + smooth;
+  const float inv_u2 = (float)(1.0 / (U * U));
+  const float twoI = (float)(2.0 * s[1] + smooth);
+  const float Uf = (float)U;
+  const float inv_n = (float)(1.0 / (double)n);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = x[i], y = t[i];
+    const float sg = 1.f / (1.f + expf(-v));
+    float d = wb * (sg - y) * inv_n;
+    if (wd != 0.f) {
+      const float dds = -(2.f * y * Uf - twoI) * inv_u2;  // d(1 - dice)/d sigma_i
+      d += wd * dds * sg * (1.f - sg);
+    }
+    dl[i] = g * d;
+  }
+}
+hipError_t launch_loss_grad(const float* logits, const float* target, int64_t n, const double* sums, int kind,
+                            float alpha, float smooth, const float* gscale, float* dl, hipStream_t st) {
+  hipLaunchKernelGGL(loss_grad_kernel, dim3(grid_for(n, 256 * 4, 4096)), dim3(256), 0, st, logits, target, n, sums,
+                     kind, alpha, smooth, gscale, dl);
+  return hipGetLastError();
+}
+
+}  // namespace unet

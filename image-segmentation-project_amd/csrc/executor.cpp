@@ -1,0 +1,923 @@
+// Native executor for the resnet34 U-Net training step (forward + backward).
+//
+// The plan mirrors UNetWithBackbone(backbone='resnet34', use_attention=False)
+// (/root/reference/advanced_models.py:64-100,157-160,197-205,264-357) with the
+// torchvision ResNet34 encoder.  It owns: the parameter table in reference
+// state_dict order, the workspace layout (bf16 NHWC activations, skip-concat
+// buffers that the up-convs write into directly, BN sums, packed weights and
+// fp32 weight-gradient accumulators), and the launch sequence.  Python passes
+// raw device pointers; nothing here allocates device memory.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/unet_hip.h"
+#include "kernels.h"
+
+namespace unet {
+
+thread_local std::string g_err;
+void set_err(const std::string& s) { g_err = s; }
+
+#define CK(expr)                                                                      \
+  do {                                                                                \
+    hipError_t e_ = (expr);                                                           \
+    if (e_ != hipSuccess) {                                                           \
+      set_err(std::string(#expr) + " -> " + hipGetErrorString(e_) + " @" + __FILE__ + \
+              ":" + std::to_string(__LINE__));                                        \
+      return (int)e_;                                                                 \
+    }                                                                                 \
+  } while (0)
+
+struct Act {  // bf16 NHWC view: ws + off, channel stride ld
+  size_t off = 0;
+  int ld = 0, C = 0, H = 0, W = 0;
+};
+
+struct Param {
+  std::string name;
+  std::vector<int64_t> shape;
+  int64_t numel = 0, flat = 0;
+};
+
+struct Bn {
+  int gamma, beta;        // param indices
+  int idx;                // BN ordinal (buffers 3*idx + 0/1)
+  int C;
+  size_t stats, bsums, save;  // ws offsets: fp64 [2C] fwd, fp64 [2C] bwd, fp32 mean|invstd
+};
+
+enum { L_CONV = 0, L_CONVT = 1, L_STEM = 2 };
+struct Conv {
+  int w, b = -1;  // param indices
+  int kind, Ci, Co, R, S, stride, pad;
+  size_t pk_fwd = 0, pk_dgrad = 0, wacc = 0;  // ws offsets
+  size_t bias_acc = 0;                        // fp64 [Co] (convT bias grads)
+};
+
+struct Block {
+  int conv1, bn1, conv2, bn2, ds = -1, dsbn = -1;
+  Act in, y1, h, y2, yds, out;
+  Act d_out, dy1, dh, dy2, dyds, dres;  // grads
+  Act d_in;                             // == previous block's d_out (or dP0)
+  Act skip_add;                         // skip-concat gradient slice for the input (or empty)
+};
+
+struct Dec {
+  int up, conv1, bn1, conv2, bn2;
+  Act up_in, up_out;  // up_out = cat slice
+  Act cat, y1, h, y2, out;
+  Act d_out, dy2, dh, dy1, dcat, d_up_in;
+};
+
+}  // namespace unet
+
+using namespace unet;
+
+struct unet_plan {
+  unet_config cfg;
+  std::vector<Param> params;
+  std::vector<Bn> bns;
+  std::vector<Conv> convs;
+  std::vector<Block> blocks;  // 16 encoder blocks
+  std::vector<Dec> decs;      // decoder4..decoder1 (index 0 = level 4)
+  int stem_conv, stem_bn, up0_w, up0_b, fin_w, fin_b;
+  Act x1, y0, p0, d_x1, d_y0, d_p0;
+  size_t pidx = 0;
+  size_t ws_bytes = 0;
+  size_t zero_fwd_off = 0, zero_fwd_bytes = 0;
+  size_t zero_bwd_off = 0, zero_bwd_bytes = 0;
+  size_t head_usum = 0;
+  int64_t grad_numel = 0;
+  std::vector<std::pair<int64_t, int64_t>> buckets;  // flat element ranges
+  std::vector<std::vector<int>> bucket_convs;        // convs to unpack per bucket
+  hipEvent_t events[8] = {};
+  int nevents = 0;
+  double flops_fwd = 0, flops_train = 0;
+};
+
+namespace {
+
+struct Alloc {
+  size_t top = 0;
+  size_t take(size_t bytes) {
+    const size_t off = top;
+    top += (bytes + 255) & ~size_t(255);
+    return off;
+  }
+};
+
+int add_param(unet_plan* p, const std::string& name, std::vector<int64_t> shape) {
+  Param q;
+  q.name = name;
+  q.shape = shape;
+  q.numel = 1;
+  for (auto s : shape) q.numel *= s;
+  q.flat = p->grad_numel;
+  p->grad_numel += q.numel;
+  p->params.push_back(q);
+  return (int)p->params.size() - 1;
+}
+
+int add_bn(unet_plan* p, const std::string& prefix, int C) {
+  Bn b;
+  b.gamma = add_param(p, prefix + ".weight", {C});
+  b.beta = add_param(p, prefix + ".bias", {C});
+  b.idx = (int)p->bns.size();
+  b.C = C;
+  p->bns.push_back(b);
+  return b.idx;
+}
+
+int add_conv(unet_plan* p, const std::string& prefix, int kind, int Ci, int Co, int R, int stride, int pad,
+             bool bias) {
+  Conv c;
+  c.kind = kind;
+  c.Ci = Ci; c.Co = Co; c.R = R; c.S = R; c.stride = stride; c.pad = pad;
+  if (kind == L_CONVT) c.w = add_param(p, prefix + ".weight", {Ci, Co, R, R});
+  else c.w = add_param(p, prefix + ".weight", {Co, Ci, R, R});
+  if (bias) c.b = add_param(p, prefix + ".bias", {Co});
+  p->convs.push_back(c);
+  return (int)p->convs.size() - 1;
+}
+
+Act act(Alloc& A, int N, int H, int W, int C) {
+  Act a;
+  a.off = A.take((size_t)N * H * W * C * 2);
+  a.ld = C; a.C = C; a.H = H; a.W = W;
+  return a;
+}
+Act slice(const Act& base, int c0, int C) {
+  Act a = base;
+  a.off = base.off + (size_t)c0 * 2;
+  a.C = C;
+  return a;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// plan construction
+// ---------------------------------------------------------------------------
+static int build_plan(unet_plan* p) {
+  const unet_config& c = p->cfg;
+  const int N = c.N, H = c.H, W = c.W, w = c.width;
+  if (H % 32 || W % 32 || N <= 0 || w <= 0) {
+    set_err("unet_plan_create: H and W must be multiples of 32 (advanced_models.py:317-347 crops "
+            "only fix the last two levels)");
+    return 1;
+  }
+  if (c.n_classes != 1) { set_err("unet_plan_create: only n_classes == 1 is supported"); return 1; }
+  const int c0 = 64 * w, c1 = 128 * w, c2 = 256 * w, c3 = 512 * w;
+  const int chan[4] = {c0, c1, c2, c3};
+  const int nblk[4] = {3, 4, 6, 3};
+
+  // ---- parameters, in reference registration order ----
+  p->stem_conv = add_conv(p, "input_conv", L_STEM, 1, c0, 7, 2, 3, false);
+  p->stem_bn = add_bn(p, "bn1", c0);
+  struct BlkSpec { int conv1, bn1, conv2, bn2, ds, dsbn, cin, cout, stride, stage; };
+  std::vector<BlkSpec> specs;
+  int cin = c0;
+  for (int s = 0; s < 4; ++s) {
+    for (int b = 0; b < nblk[s]; ++b) {
+      const std::string pre = "enc" + std::to_string(s + 1) + "." + std::to_string(b);
+      const int stride = (b == 0 && s > 0) ? 2 : 1;
+      const int cout = chan[s];
+      BlkSpec bs;
+      bs.conv1 = add_conv(p, pre + ".conv1", L_CONV, cin, cout, 3, stride, 1, false);
+      bs.bn1 = add_bn(p, pre + ".bn1", cout);
+      bs.conv2 = add_conv(p, pre + ".conv2", L_CONV, cout, cout, 3, 1, 1, false);
+      bs.bn2 = add_bn(p, pre + ".bn2", cout);
+      bs.ds = bs.dsbn = -1;
+      if (stride != 1 || cin != cout) {
+        bs.ds = add_conv(p, pre + ".downsample.0", L_CONV, cin, cout, 1, stride, 0, false);
+        bs.dsbn = add_bn(p, pre + ".downsample.1", cout);
+      }
+      bs.cin = cin; bs.cout = cout; bs.stride = stride; bs.stage = s;
+      specs.push_back(bs);
+      cin = cout;
+    }
+  }
+  const int enc_end_param = (int)p->params.size();
+  // decoder: level 4 (deepest) .. 1
+  struct DecSpec { int up, conv1, bn1, conv2, bn2, upin, upout, skipc, outc; };
+  std::vector<DecSpec> dspecs;
+  {
+    const int upin[4] = {c3, c2, c1, c0};
+    const int upout[4] = {c2, c1, c0, c0 / 2};
+    const int skipc[4] = {c2, c1, c0, c0};
+    const int outc[4] = {c2, c1, c0, c0 / 2};
+    for (int l = 0; l < 4; ++l) {
+      const int lvl = 4 - l;
+      DecSpec d;
+      d.up = add_conv(p, "upconv" + std::to_string(lvl), L_CONVT, upin[l], upout[l], 2, 2, 0, true);
+      const std::string pre = "decoder" + std::to_string(lvl);
+      const int catc = skipc[l] + upout[l];
+      d.conv1 = add_conv(p, pre + ".0", L_CONV, catc, outc[l], 3, 1, 1, true);
+      d.bn1 = add_bn(p, pre + ".1", outc[l]);
+      d.conv2 = add_conv(p, pre + ".3", L_CONV, outc[l], outc[l], 3, 1, 1, true);
+      d.bn2 = add_bn(p, pre + ".4", outc[l]);
+      d.upin = upin[l]; d.upout = upout[l]; d.skipc = skipc[l]; d.outc = outc[l];
+      dspecs.push_back(d);
+    }
+  }
+  p->up0_w = add_param(p, "upconv0.weight", {c0 / 2, c0 / 4, 2, 2});
+  p->up0_b = add_param(p, "upconv0.bias", {c0 / 4});
+  p->fin_w = add_param(p, "conv_final.weight", {c.n_classes, c0 / 4, 1, 1});
+  p->fin_b = add_param(p, "conv_final.bias", {c.n_classes});
+
+  // ---- DDP buckets in backward completion order ----
+  auto stage_range = [&](int s) {
+    int lo = -1, hi = -1;
+    const std::string pre = "enc" + std::to_string(s + 1) + ".";
+    for (int i = 0; i < (int)p->params.size(); ++i)
+      if (p->params[i].name.rfind(pre, 0) == 0) { if (lo < 0) lo = i; hi = i; }
+    return std::make_pair(lo, hi);
+  };
+  {
+    const int64_t dec_begin = p->params[enc_end_param].flat;
+    p->buckets.push_back({dec_begin, p->grad_numel});
+    auto r4 = stage_range(3), r3 = stage_range(2);
+    p->buckets.push_back({p->params[r4.first].flat, p->params[r4.second].flat + p->params[r4.second].numel});
+    p->buckets.push_back({p->params[r3.first].flat, p->params[r3.second].flat + p->params[r3.second].numel});
+    p->buckets.push_back({0, p->params[r3.first].flat});
+  }
+
+  // ---- workspace ----
+  Alloc A;
+  // zeroed at forward start: BN fwd sums
+  p->zero_fwd_off = A.take(0);
+  for (auto& b : p->bns) b.stats = A.take((size_t)2 * b.C * sizeof(double));
+  p->zero_fwd_bytes = A.top - p->zero_fwd_off;
+  // zeroed at backward start: BN bwd sums, convT bias sums, head sums, wgrad accumulators
+  p->zero_bwd_off = A.take(0);
+  for (auto& b : p->bns) b.bsums = A.take((size_t)2 * b.C * sizeof(double));
+  for (auto& cv : p->convs)
+    if (cv.kind == L_CONVT) cv.bias_acc = A.take((size_t)cv.Co * sizeof(double));
+  p->head_usum = A.take((size_t)(c0 / 2 * 4 + 1) * sizeof(double));
+  for (auto& cv : p->convs) {
+    size_t n;
+    if (cv.kind == L_STEM) n = (size_t)cv.Co * 64;
+    else n = (size_t)cv.Co * cv.Ci * cv.R * cv.S;
+    cv.wacc = A.take(n * sizeof(float));
+  }
+  p->zero_bwd_bytes = A.top - p->zero_bwd_off;
+  for (auto& b : p->bns) b.save = A.take((size_t)2 * b.C * sizeof(float));
+  for (auto& cv : p->convs) {
+    if (cv.kind == L_STEM) {
+      cv.pk_fwd = A.take((size_t)cv.Co * 64 * 2);
+    } else {
+      const size_t n = (size_t)cv.Co * cv.Ci * cv.R * cv.S * 2;
+      cv.pk_fwd = A.take(n);
+      cv.pk_dgrad = A.take(n);
+    }
+  }
+
+  // forward activations
+  const int H2 = H / 2, W2 = W / 2, H4 = H / 4, W4 = W / 4;
+  Act cat1 = act(A, N, H2, W2, c0 + c0 / 2);
+  p->x1 = slice(cat1, 0, c0);
+  p->y0 = act(A, N, H2, W2, c0);
+  p->p0 = act(A, N, H4, W4, c0);
+  p->pidx = A.take((size_t)N * H4 * W4 * c0);
+  Act cats[4];  // cats[l] for decoder level index l (0 = level 4)
+  cats[3] = cat1;
+  cats[2] = act(A, N, H4, W4, 2 * c0);
+  cats[1] = act(A, N, H / 8, W / 8, 2 * c1);
+  cats[0] = act(A, N, H / 16, W / 16, 2 * c2);
+  Act x5 = act(A, N, H / 32, W / 32, c3);
+
+  Act prev = p->p0;
+  for (size_t i = 0; i < specs.size(); ++i) {
+    const BlkSpec& s = specs[i];
+    Block b;
+    b.conv1 = s.conv1; b.bn1 = s.bn1; b.conv2 = s.conv2; b.bn2 = s.bn2; b.ds = s.ds; b.dsbn = s.dsbn;
+    const int Hs = H4 >> s.stage, Ws = W4 >> s.stage;
+    b.in = prev;
+    b.y1 = act(A, N, Hs, Ws, s.cout);
+    b.h = act(A, N, Hs, Ws, s.cout);
+    b.y2 = act(A, N, Hs, Ws, s.cout);
+    if (s.ds >= 0) b.yds = act(A, N, Hs, Ws, s.cout);
+    const bool last = (i + 1 == specs.size()) || specs[i + 1].stage != s.stage;
+    if (last) {
+      if (s.stage == 3) b.out = x5;
+      else b.out = slice(cats[2 - s.stage], 0, s.cout);  // x2->cat2, x3->cat3, x4->cat4
+    } else {
+      b.out = act(A, N, Hs, Ws, s.cout);
+    }
+    p->blocks.push_back(b);
+    prev = b.out;
+  }
+  Act dec_in = x5;
+  for (int l = 0; l < 4; ++l) {
+    const DecSpec& s = dspecs[l];
+    Dec d;
+    d.up = s.up; d.conv1 = s.conv1; d.bn1 = s.bn1; d.conv2 = s.conv2; d.bn2 = s.bn2;
+    d.cat = cats[l];
+    d.up_in = dec_in;
+    d.up_out = slice(cats[l], s.skipc, s.upout);
+    const int Hl = d.cat.H, Wl = d.cat.W;
+    d.y1 = act(A, N, Hl, Wl, s.outc);
+    d.h = act(A, N, Hl, Wl, s.outc);
+    d.y2 = act(A, N, Hl, Wl, s.outc);
+    d.out = act(A, N, Hl, Wl, s.outc);
+    p->decs.push_back(d);
+    dec_in = d.out;
+  }
+
+  // backward gradient tensors
+  for (int l = 3; l >= 0; --l) {
+    Dec& d = p->decs[l];
+    const int Hl = d.cat.H, Wl = d.cat.W, oc = d.out.C;
+    d.d_out = act(A, N, Hl, Wl, oc);
+    d.dy2 = act(A, N, Hl, Wl, oc);
+    d.dh = act(A, N, Hl, Wl, oc);
+    d.dy1 = act(A, N, Hl, Wl, oc);
+    d.dcat = act(A, N, Hl, Wl, d.cat.C);
+  }
+  for (int l = 0; l < 4; ++l) {
+    Dec& d = p->decs[l];
+    d.d_up_in = (l == 0) ? act(A, N, H / 32, W / 32, c3) : p->decs[l - 1].d_out;
+  }
+  for (auto& b : p->blocks) {
+    const int Hs = b.y1.H, Ws = b.y1.W, C = b.y1.C;
+    b.dy1 = act(A, N, Hs, Ws, C);
+    b.dh = act(A, N, Hs, Ws, C);
+    b.dy2 = act(A, N, Hs, Ws, C);
+    if (b.ds >= 0) b.dyds = act(A, N, Hs, Ws, C);
+    else b.dres = act(A, N, Hs, Ws, C);
+  }
+  // block output grads: last encoder block's d_out = decoder-4's d_up_in
+  const int nb = (int)p->blocks.size();
+  p->blocks[nb - 1].d_out = p->decs[0].d_up_in;
+  for (int i = nb - 2; i >= 0; --i) {
+    Block& b = p->blocks[i];
+    b.d_out = act(A, N, b.out.H, b.out.W, b.out.C);
+  }
+  p->d_p0 = act(A, N, H4, W4, c0);
+  for (int i = 0; i < nb; ++i) {
+    Block& b = p->blocks[i];
+    b.d_in = i == 0 ? p->d_p0 : p->blocks[i - 1].d_out;
+    b.skip_add = Act();
+    if (i > 0 && specs[i].stage != specs[i - 1].stage) {
+      // input x_{s+1} also fed cat_{s+1} slice 0: add that slice's gradient
+      const int s = specs[i].stage;            // 1..3
+      const int l = 3 - s;                     // x2 (s=1) -> cats[2], x3 -> cats[1], x4 -> cats[0]
+      b.skip_add = slice(p->decs[l].dcat, 0, specs[i].cin);
+    }
+  }
+  p->d_x1 = act(A, N, H2, W2, c0);
+  p->d_y0 = act(A, N, H2, W2, c0);
+  p->ws_bytes = A.top;
+
+  // unpack groups per bucket
+  p->bucket_convs.assign(4, {});
+  for (int i = 0; i < (int)p->convs.size(); ++i) {
+    const int64_t f = p->params[p->convs[i].w].flat;
+    for (int bk = 0; bk < 4; ++bk)
+      if (f >= p->buckets[bk].first && f < p->buckets[bk].second) p->bucket_convs[bk].push_back(i);
+  }
+
+  // algorithmic FLOPs: 2*MACs; training = 3x fwd - stem dgrad
+  double fw = 0, stem = 0;
+  for (auto& cv : p->convs) {
+    double macs;
+    if (cv.kind == L_STEM) { macs = (double)N * H2 * W2 * cv.Co * 49; stem = 2 * macs; }
+    else if (cv.kind == L_CONVT) {
+      // input pixels x Ci x Co x 4
+      int hin = 0;
+      for (auto& d : p->decs) if (d.up >= 0 && &p->convs[d.up] == &cv) hin = d.up_in.H * d.up_in.W;
+      macs = (double)N * hin * cv.Ci * cv.Co * 4;
+    } else {
+      macs = 0;
+    }
+    fw += 2 * macs;
+  }
+  for (auto& b : p->blocks) {
+    const double px = (double)N * b.y1.H * b.y1.W;
+    fw += 2 * px * p->convs[b.conv1].Ci * p->convs[b.conv1].Co * 9;
+    fw += 2 * px * p->convs[b.conv2].Ci * p->convs[b.conv2].Co * 9;
+    if (b.ds >= 0) fw += 2 * px * p->convs[b.ds].Ci * p->convs[b.ds].Co;
+  }
+  for (auto& d : p->decs) {
+    const double px = (double)N * d.y1.H * d.y1.W;
+    fw += 2 * px * p->convs[d.conv1].Ci * p->convs[d.conv1].Co * 9;
+    fw += 2 * px * p->convs[d.conv2].Ci * p->convs[d.conv2].Co * 9;
+  }
+  fw += 2.0 * N * H2 * W2 * (c0 / 2) * (c0 / 4) * 4;  // upconv0
+  fw += 2.0 * N * H * W * (c0 / 4);                    // conv_final
+  p->flops_fwd = fw;
+  p->flops_train = 3 * fw - stem;
+
+  return 0;  // bucket events are created lazily (plan creation needs no GPU)
+}
+
+static int ensure_events(unet_plan* p) {
+  if (p->nevents) return 0;
+  for (int i = 0; i < 4; ++i) CK(hipEventCreateWithFlags(&p->events[i], hipEventDisableTiming));
+  p->nevents = 4;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// execution helpers
+// ---------------------------------------------------------------------------
+namespace {
+
+struct Ctx {
+  unet_plan* p;
+  char* ws;
+  const float* const* prm;
+  float* const* buf;
+  hipStream_t st;
+  int training;
+  bf16_t* A(const Act& a) const { return reinterpret_cast<bf16_t*>(ws + a.off); }
+  template <class T> T* W(size_t off) const { return reinterpret_cast<T*>(ws + off); }
+};
+
+BnLaunch bn_launch(const Ctx& x, int bi, int64_t npix) {
+  const Bn& b = x.p->bns[bi];
+  BnLaunch l;
+  l.stats = x.W<double>(b.stats);
+  l.gamma = x.prm[b.gamma];
+  l.beta = x.prm[b.beta];
+  l.run_mean = x.buf[3 * b.idx + 0];
+  l.run_var = x.buf[3 * b.idx + 1];
+  l.save_mean = x.W<float>(b.save);
+  l.save_invstd = x.W<float>(b.save) + b.C;
+  l.count = (double)npix;
+  l.C = b.C;
+  l.eps = x.p->cfg.bn_eps;
+  l.momentum = x.p->cfg.bn_momentum;
+  l.training = x.training;
+  return l;
+}
+
+int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for_stats) {
+  const Conv& cv = x.p->convs[ci];
+  ConvFwdArgs a = {};
+  a.x = x.A(in); a.ldx = in.ld;
+  a.w = x.W<bf16_t>(cv.pk_fwd);
+  a.y = x.A(out); a.ldy = out.ld;
+  a.bias = cv.b >= 0 ? x.prm[cv.b] : nullptr;
+  a.stats = (bn_for_stats >= 0 && x.training) ? x.W<double>(x.p->bns[bn_for_stats].stats) : nullptr;
+  a.N = x.p->cfg.N; a.H = in.H; a.W = in.W; a.C = cv.Ci;
+  a.P = out.H; a.Q = out.W; a.Cout = cv.Co;
+  a.R = cv.R; a.S = cv.S; a.stride = cv.stride; a.pad = cv.pad;
+  CK(launch_conv_fwd(a, cv.kind == L_CONVT ? MODE_TRANS : MODE_FWD, x.st));
+  return 0;
+}
+
+// conv dgrad: dx = dgrad(dy) (+ addend)
+int conv_dgrad(const Ctx& x, int ci, const Act& dy, const Act& dx, const Act* add) {
+  const Conv& cv = x.p->convs[ci];
+  ConvFwdArgs a = {};
+  a.x = x.A(dy); a.ldx = dy.ld;
+  a.w = x.W<bf16_t>(cv.pk_dgrad);
+  a.y = x.A(dx); a.ldy = dx.ld;
+  if (add && add->ld) { a.add = x.A(*add); a.ldadd = add->ld; }
+  a.N = x.p->cfg.N;
+  a.H = dy.H; a.W = dy.W;
+  a.P = dx.H; a.Q = dx.W;
+  a.R = cv.R; a.S = cv.S; a.stride = cv.stride; a.pad = cv.pad;
+  if (cv.kind == L_CONVT) {  // ordinary k2s2 conv of dY: reduce over Co, produce Ci
+    a.C = cv.Co; a.Cout = cv.Ci;
+    CK(launch_conv_fwd(a, MODE_FWD, x.st));
+  } else {
+    a.C = cv.Co; a.Cout = cv.Ci;
+    CK(launch_conv_fwd(a, MODE_TRANS, x.st));
+  }
+  return 0;
+}
+
+int conv_wgrad(const Ctx& x, int ci, const Act& dy, const Act& in) {
+  const Conv& cv = x.p->convs[ci];
+  ConvWgradArgs a = {};
+  a.N = x.p->cfg.N;
+  a.dw = x.W<float>(cv.wacc);
+  a.R = cv.R; a.S = cv.S; a.stride = cv.stride; a.pad = cv.pad;
+  if (cv.kind == L_CONVT) {
+    // view as conv of dY (input, stride 2) producing X: "dy" := X, "x" := dY
+    a.dy = x.A(in); a.lddy = in.ld;
+    a.x = x.A(dy); a.ldx = dy.ld;
+    a.H = dy.H; a.W = dy.W; a.C = cv.Co;
+    a.P = in.H; a.Q = in.W; a.Cout = cv.Ci;
+  } else {
+    a.dy = x.A(dy); a.lddy = dy.ld;
+    a.x = x.A(in); a.ldx = in.ld;
+    a.H = in.H; a.W = in.W; a.C = cv.Ci;
+    a.P = dy.H; a.Q = dy.W; a.Cout = cv.Co;
+  }
+  CK(launch_conv_wgrad(a, 0, x.st));
+  return 0;
+}
+
+int bn_apply(const Ctx& x, int bi, const Act& y, const Act& out, int res_mode, const Act* res, int bi2,
+             bool relu) {
+  BnApplyArgs a = {};
+  const int64_t npix = (int64_t)x.p->cfg.N * y.H * y.W;
+  a.y = x.A(y); a.ldy = y.ld;
+  a.out = x.A(out); a.ldo = out.ld;
+  a.bn = bn_launch(x, bi, npix);
+  if (res_mode) { a.res = x.A(*res); a.ldr = res->ld; }
+  if (res_mode == 2) a.bn2 = bn_launch(x, bi2, npix);
+  a.npix = npix; a.C = y.C; a.res_mode = res_mode; a.relu = relu ? 1 : 0;
+  CK(launch_bn_apply(a, x.st));
+  return 0;
+}
+
+// BN(+ReLU) backward for out = relu(bn(y) [+ bn2(y2) | + res]).
+int bn_backward(const Ctx& x, int bi, const Act& dout, const Act& out, const Act& y, const Act& dy,
+                int bi2, const Act* y2, const Act* dy2, const Act* dres, float* grads) {
+  BnBwdArgs a = {};
+  const Bn& b = x.p->bns[bi];
+  const int64_t npix = (int64_t)x.p->cfg.N * y.H * y.W;
+  a.da = x.A(dout); a.ldda = dout.ld;
+  a.act = x.A(out); a.ldact = out.ld;
+  a.y = x.A(y); a.ldy = y.ld;
+  a.mean = x.W<float>(b.save); a.invstd = x.W<float>(b.save) + b.C; a.gamma = x.prm[b.gamma];
+  a.sums = x.W<double>(b.bsums);
+  a.dy = x.A(dy); a.lddy = dy.ld;
+  a.dgamma = grads + x.p->params[b.gamma].flat;
+  a.dbeta = grads + x.p->params[b.beta].flat;
+  if (bi2 >= 0) {
+    const Bn& b2 = x.p->bns[bi2];
+    a.y2 = x.A(*y2); a.ldy2 = y2->ld;
+    a.mean2 = x.W<float>(b2.save); a.invstd2 = x.W<float>(b2.save) + b2.C; a.gamma2 = x.prm[b2.gamma];
+    a.sums2 = x.W<double>(b2.bsums);
+    a.dy2 = x.A(*dy2); a.lddy2 = dy2->ld;
+    a.dgamma2 = grads + x.p->params[b2.gamma].flat;
+    a.dbeta2 = grads + x.p->params[b2.beta].flat;
+  }
+  if (dres) { a.dres = x.A(*dres); a.lddres = dres->ld; }
+  a.npix = npix; a.C = y.C; a.relu = 1;
+  CK(launch_bn_bwd_reduce(a, x.st));
+  CK(launch_bn_bwd_apply(a, x.st));
+  return 0;
+}
+
+int unpack_bucket(const Ctx& x, int bk, float* grads) {
+  UnpackTable t;
+  t.n = 0;
+  for (int ci : x.p->bucket_convs[bk]) {
+    const Conv& cv = x.p->convs[ci];
+    UnpackEntry& e = t.e[t.n++];
+    e.acc = x.W<float>(cv.wacc);
+    e.dst = grads + x.p->params[cv.w].flat;
+    e.R = cv.R; e.S = cv.S;
+    if (cv.kind == L_CONV) { e.kind = UP_CONV; e.Co = cv.Co; e.Ci = cv.Ci; }
+    else if (cv.kind == L_CONVT) { e.kind = UP_CONVT; e.Co = cv.Co; e.Ci = cv.Ci; }
+    else { e.kind = UP_STEM; e.Co = cv.Co; e.Ci = 1; e.R = 7; e.S = 7; }
+    if (t.n == kMaxPack) { CK(launch_unpack(t, x.st)); t.n = 0; }
+  }
+  CK(launch_unpack(t, x.st));
+  return 0;
+}
+
+}  // namespace
+
+#define RUN(expr)              \
+  do {                         \
+    int r_ = (expr);           \
+    if (r_) return r_;         \
+  } while (0)
+
+static int run_forward(unet_plan* p, const float* image, const float* const* prm, float* const* buf, char* ws,
+                       float* logits, int training, hipStream_t st) {
+  Ctx x{p, ws, prm, buf, st, training};
+  const int N = p->cfg.N;
+  CK(hipMemsetAsync(ws + p->zero_fwd_off, 0, p->zero_fwd_bytes, st));
+  // pack weights (fp32 torch layout -> bf16 kernel layouts)
+  {
+    PackTable t;
+    t.n = 0;
+    auto flush = [&]() -> int { CK(launch_pack(t, st)); t.n = 0; return 0; };
+    for (auto& cv : p->convs) {
+      if (cv.kind == L_STEM) {
+        t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_fwd), PK_STEM, cv.Co, 1, 7, 7};
+      } else if (cv.kind == L_CONV) {
+        t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_fwd), PK_CONV_FWD, cv.Co, cv.Ci, cv.R, cv.S};
+        if (t.n == kMaxPack) RUN(flush());
+        if (training) t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_dgrad), PK_CONV_DGRAD, cv.Co, cv.Ci, cv.R, cv.S};
+      } else {
+        t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_fwd), PK_CONVT_FWD, cv.Co, cv.Ci, cv.R, cv.S};
+        if (t.n == kMaxPack) RUN(flush());
+        if (training) t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_dgrad), PK_CONVT_DGRAD, cv.Co, cv.Ci, cv.R, cv.S};
+      }
+      if (t.n >= kMaxPack - 1) RUN(flush());
+    }
+    RUN(flush());
+  }
+  // stem: conv7x7/s2 -> bn1 -> relu into cat1[:, :c0]; maxpool
+  {
+    const Conv& cv = p->convs[p->stem_conv];
+    ConvFwdArgs a = {};
+    a.x = reinterpret_cast<const bf16_t*>(image); a.ldx = 1;
+    a.w = x.W<bf16_t>(cv.pk_fwd);
+    a.y = x.A(p->y0); a.ldy = p->y0.ld;
+    a.stats = training ? x.W<double>(p->bns[p->stem_bn].stats) : nullptr;
+    a.N = N; a.H = p->cfg.H; a.W = p->cfg.W; a.C = 1;
+    a.P = p->y0.H; a.Q = p->y0.W; a.Cout = cv.Co;
+    a.R = 7; a.S = 7; a.stride = 2; a.pad = 3;
+    CK(launch_conv_fwd(a, MODE_STEM, st));
+    RUN(bn_apply(x, p->stem_bn, p->y0, p->x1, 0, nullptr, -1, true));
+    MaxPoolArgs m = {};
+    m.x = x.A(p->x1); m.ldx = p->x1.ld; m.y = x.A(p->p0); m.ldy = p->p0.ld; m.idx = x.W<uint8_t>(p->pidx);
+    m.N = N; m.H = p->x1.H; m.W = p->x1.W; m.C = p->x1.C; m.P = p->p0.H; m.Q = p->p0.W;
+    CK(launch_maxpool_fwd(m, st));
+  }
+  for (auto& b : p->blocks) {
+    RUN(conv_forward(x, b.conv1, b.in, b.y1, b.bn1));
+    RUN(bn_apply(x, b.bn1, b.y1, b.h, 0, nullptr, -1, true));
+    RUN(conv_forward(x, b.conv2, b.h, b.y2, b.bn2));
+    if (b.ds >= 0) {
+      RUN(conv_forward(x, b.ds, b.in, b.yds, b.dsbn));
+      RUN(bn_apply(x, b.bn2, b.y2, b.out, 2, &b.yds, b.dsbn, true));
+    } else {
+      RUN(bn_apply(x, b.bn2, b.y2, b.out, 1, &b.in, -1, true));
+    }
+  }
+  for (auto& d : p->decs) {
+    RUN(conv_forward(x, d.up, d.up_in, d.up_out, -1));
+    RUN(conv_forward(x, d.conv1, d.cat, d.y1, d.bn1));
+    RUN(bn_apply(x, d.bn1, d.y1, d.h, 0, nullptr, -1, true));
+    RUN(conv_forward(x, d.conv2, d.h, d.y2, d.bn2));
+    RUN(bn_apply(x, d.bn2, d.y2, d.out, 0, nullptr, -1, true));
+  }
+  {
+    const Act& o = p->decs[3].out;
+    HeadArgs h = {};
+    h.x = x.A(o); h.ldx = o.ld;
+    h.w0 = prm[p->up0_w]; h.b0 = prm[p->up0_b]; h.wf = prm[p->fin_w]; h.bf = prm[p->fin_b];
+    h.logits = logits;
+    h.N = N; h.H = o.H; h.W = o.W; h.Cin = o.C; h.Co = (int)p->params[p->up0_b].numel;
+    CK(launch_head_fwd(h, st));
+  }
+  return 0;
+}
+
+static int run_backward(unet_plan* p, const float* image, const float* dlogits, const float* const* prm, char* ws,
+                        float* grads, hipStream_t st) {
+  Ctx x{p, ws, prm, nullptr, st, 1};
+  const int N = p->cfg.N;
+  RUN(ensure_events(p));
+  CK(hipMemsetAsync(ws + p->zero_bwd_off, 0, p->zero_bwd_bytes, st));
+  // head (upconv0 + conv_final)
+  {
+    const Act& o = p->decs[3].out;
+    HeadArgs h = {};
+    h.x = x.A(o); h.ldx = o.ld;
+    h.w0 = prm[p->up0_w]; h.b0 = prm[p->up0_b]; h.wf = prm[p->fin_w]; h.bf = prm[p->fin_b];
+    h.dl = dlogits;
+    h.dx = x.A(p->decs[3].d_out); h.lddx = p->decs[3].d_out.ld;
+    h.usum = x.W<double>(p->head_usum);
+    h.gw0 = grads + p->params[p->up0_w].flat; h.gb0 = grads + p->params[p->up0_b].flat;
+    h.gwf = grads + p->params[p->fin_w].flat; h.gbf = grads + p->params[p->fin_b].flat;
+    h.N = N; h.H = o.H; h.W = o.W; h.Cin = o.C; h.Co = (int)p->params[p->up0_b].numel;
+    CK(launch_head_bwd(h, st));
+    CK(launch_head_grads(h, st));
+  }
+  // decoder1 .. decoder4 (+ their up-convs)
+  for (int l = 3; l >= 0; --l) {
+    Dec& d = p->decs[l];
+    RUN(bn_backward(x, d.bn2, d.d_out, d.out, d.y2, d.dy2, -1, nullptr, nullptr, nullptr, grads));
+    RUN(conv_dgrad(x, d.conv2, d.dy2, d.dh, nullptr));
+    RUN(conv_wgrad(x, d.conv2, d.dy2, d.h));
+    RUN(bn_backward(x, d.bn1, d.dh, d.h, d.y1, d.dy1, -1, nullptr, nullptr, nullptr, grads));
+    RUN(conv_dgrad(x, d.conv1, d.dy1, d.dcat, nullptr));
+    RUN(conv_wgrad(x, d.conv1, d.dy1, d.cat));
+    // decoder conv biases feed a training-mode BN: their exact gradient is
+    // sum(dY) = 0 (BN removes the mean); write it explicitly.
+    CK(hipMemsetAsync(grads + p->params[p->convs[d.conv1].b].flat, 0, sizeof(float) * p->convs[d.conv1].Co, st));
+    CK(hipMemsetAsync(grads + p->params[p->convs[d.conv2].b].flat, 0, sizeof(float) * p->convs[d.conv2].Co, st));
+    // up-conv: dU = dcat[:, skip:]
+    const Conv& up = p->convs[d.up];
+    Act du = slice(d.dcat, d.cat.C - up.Co, up.Co);
+    RUN(conv_dgrad(x, d.up, du, d.d_up_in, nullptr));
+    RUN(conv_wgrad(x, d.up, du, d.up_in));
+    CK(launch_channel_sum(x.A(du), du.ld, (int64_t)N * du.H * du.W, up.Co, x.W<double>(up.bias_acc), st));
+    CK(launch_d2f(x.W<double>(up.bias_acc), grads + p->params[up.b].flat, up.Co, st));
+  }
+  RUN(unpack_bucket(x, 0, grads));
+  CK(hipEventRecord(p->events[0], st));
+  // encoder blocks, deepest first
+  const int nb = (int)p->blocks.size();
+  for (int i = nb - 1; i >= 0; --i) {
+    Block& b = p->blocks[i];
+    if (b.ds >= 0) {
+      RUN(bn_backward(x, b.bn2, b.d_out, b.out, b.y2, b.dy2, b.dsbn, &b.yds, &b.dyds, nullptr, grads));
+    } else {
+      RUN(bn_backward(x, b.bn2, b.d_out, b.out, b.y2, b.dy2, -1, nullptr, nullptr, &b.dres, grads));
+    }
+    RUN(conv_dgrad(x, b.conv2, b.dy2, b.dh, nullptr));
+    RUN(conv_wgrad(x, b.conv2, b.dy2, b.h));
+    RUN(bn_backward(x, b.bn1, b.dh, b.h, b.y1, b.dy1, -1, nullptr, nullptr, nullptr, grads));
+    if (b.ds >= 0) {
+      RUN(conv_dgrad(x, b.conv1, b.dy1, b.d_in, b.skip_add.ld ? &b.skip_add : nullptr));
+      RUN(conv_dgrad(x, b.ds, b.dyds, b.d_in, &b.d_in));
+      RUN(conv_wgrad(x, b.ds, b.dyds, b.in));
+    } else {
+      RUN(conv_dgrad(x, b.conv1, b.dy1, b.d_in, &b.dres));
+    }
+    RUN(conv_wgrad(x, b.conv1, b.dy1, b.in));
+    // bucket boundaries: enc4 done at i == 13, enc3 at i == 7
+    if (i == 13) { RUN(unpack_bucket(x, 1, grads)); CK(hipEventRecord(p->events[1], st)); }
+    if (i == 7) { RUN(unpack_bucket(x, 2, grads)); CK(hipEventRecord(p->events[2], st)); }
+  }
+  // maxpool + stem
+  {
+    MaxPoolArgs m = {};
+    m.dy = x.A(p->d_p0); m.lddy = p->d_p0.ld; m.idx = x.W<uint8_t>(p->pidx);
+    const Act skip = slice(p->decs[3].dcat, 0, p->x1.C);
+    m.add = x.A(skip); m.ldadd = skip.ld;
+    m.dx = x.A(p->d_x1); m.lddx = p->d_x1.ld;
+    m.N = N; m.H = p->x1.H; m.W = p->x1.W; m.C = p->x1.C; m.P = p->p0.H; m.Q = p->p0.W;
+    CK(launch_maxpool_bwd(m, st));
+    RUN(bn_backward(x, p->stem_bn, p->d_x1, p->x1, p->y0, p->d_y0, -1, nullptr, nullptr, nullptr, grads));
+    const Conv& cv = p->convs[p->stem_conv];
+    ConvWgradArgs a = {};
+    a.dy = x.A(p->d_y0); a.lddy = p->d_y0.ld;
+    a.dw = x.W<float>(cv.wacc);
+    a.N = N; a.H = p->cfg.H; a.W = p->cfg.W; a.C = 1;
+    a.P = p->y0.H; a.Q = p->y0.W; a.Cout = cv.Co;
+    a.R = 7; a.S = 7; a.stride = 2; a.pad = 3;
+    a.x = reinterpret_cast<const bf16_t*>(image);
+    CK(launch_conv_wgrad(a, 1, st));
+  }
+  RUN(unpack_bucket(x, 3, grads));
+  CK(hipEventRecord(p->events[3], st));
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+#define API_GUARD(body)                                    \
+  try {                                                    \
+    body                                                   \
+  } catch (const std::exception& e) {                      \
+    set_err(std::string("exception: ") + e.what());        \
+    return 1;                                              \
+  } catch (...) {                                          \
+    set_err("unknown exception");                          \
+    return 1;                                              \
+  }
+
+extern "C" {
+
+const char* unet_last_error(void) { return g_err.c_str(); }
+const char* unet_version(void) { return "unet_hip 0.1 gfx950"; }
+
+int unet_plan_create(const unet_config* cfg, unet_plan** out) {
+  API_GUARD({
+    if (!cfg || !out) { set_err("null argument"); return 1; }
+    unet_plan* p = new unet_plan();
+    p->cfg = *cfg;
+    const int r = build_plan(p);
+    if (r) { delete p; return r; }
+    *out = p;
+    return 0;
+  })
+}
+
+void unet_plan_destroy(unet_plan* p) {
+  if (!p) return;
+  for (int i = 0; i < p->nevents; ++i) (void)hipEventDestroy(p->events[i]);
+  delete p;
+}
+
+int64_t unet_plan_workspace_bytes(const unet_plan* p) { return p ? (int64_t)p->ws_bytes : -1; }
+int unet_plan_num_params(const unet_plan* p) { return p ? (int)p->params.size() : -1; }
+int unet_plan_param_name(const unet_plan* p, int i, char* buf, int buflen) {
+  if (!p || i < 0 || i >= (int)p->params.size() || !buf || buflen <= 0) { set_err("bad index"); return 1; }
+  std::snprintf(buf, (size_t)buflen, "%s", p->params[i].name.c_str());
+  return 0;
+}
+int unet_plan_param_shape(const unet_plan* p, int i, int64_t shape[4]) {
+  if (!p || i < 0 || i >= (int)p->params.size()) { set_err("bad index"); return -1; }
+  const auto& s = p->params[i].shape;
+  for (size_t k = 0; k < s.size() && k < 4; ++k) shape[k] = s[k];
+  return (int)s.size();
+}
+int64_t unet_plan_param_offset(const unet_plan* p, int i) {
+  if (!p || i < 0 || i >= (int)p->params.size()) return -1;
+  return p->params[i].flat;
+}
+int64_t unet_plan_grad_numel(const unet_plan* p) { return p ? p->grad_numel : -1; }
+int unet_plan_num_bn(const unet_plan* p) { return p ? (int)p->bns.size() : -1; }
+int unet_plan_num_buckets(const unet_plan* p) { return p ? (int)p->buckets.size() : -1; }
+int unet_plan_bucket_range(const unet_plan* p, int b, int64_t* begin, int64_t* end) {
+  if (!p || b < 0 || b >= (int)p->buckets.size()) { set_err("bad bucket"); return 1; }
+  *begin = p->buckets[b].first;
+  *end = p->buckets[b].second;
+  return 0;
+}
+double unet_plan_flops(const unet_plan* p, int training) {
+  return p ? (training ? p->flops_train : p->flops_fwd) : -1.0;
+}
+
+int unet_forward(unet_plan* p, const float* image, const float* const* params, float* const* buffers,
+                 void* workspace, float* logits, int training, hipStream_t stream) {
+  API_GUARD({
+    if (!p || !image || !params || !buffers || !workspace || !logits) { set_err("null argument"); return 1; }
+    return run_forward(p, image, params, buffers, reinterpret_cast<char*>(workspace), logits, training, stream);
+  })
+}
+
+int unet_backward(unet_plan* p, const float* image, const float* dlogits, const float* const* params,
+                  void* workspace, float* grads, hipStream_t stream) {
+  API_GUARD({
+    if (!p || !image || !dlogits || !params || !workspace || !grads) { set_err("null argument"); return 1; }
+    return run_backward(p, image, dlogits, params, reinterpret_cast<char*>(workspace), grads, stream);
+  })
+}
+
+int unet_bucket_wait(unet_plan* p, int bucket, hipStream_t waiter) {
+  if (!p || bucket < 0 || bucket >= p->nevents) { set_err("bad bucket"); return 1; }
+  CK(hipStreamWaitEvent(waiter, p->events[bucket], 0));
+  return 0;
+}
+
+int unet_loss_forward(const float* logits, const float* target, int64_t n, int kind, float alpha, float smooth,
+                      double* sums8, float* loss_out, hipStream_t stream) {
+  CK(hipMemsetAsync(sums8, 0, 8 * sizeof(double), stream));
+  CK(launch_loss_sums(logits, target, n, sums8, 0, stream));
+  CK(launch_loss_value(sums8, n, kind, alpha, smooth, loss_out, stream));
+  return 0;
+}
+
+int unet_loss_backward(const float* logits, const float* target, int64_t n, int kind, float alpha, float smooth,
+                       const double* sums8, const float* grad_scale, float* dlogits, hipStream_t stream) {
+  CK(launch_loss_grad(logits, target, n, sums8, kind, alpha, smooth, grad_scale, dlogits, stream));
+  return 0;
+}
+
+int unet_mask_metrics(const float* values, const float* target, int64_t n, int values_are_prob, double* sums8,
+                      hipStream_t stream) {
+  CK(hipMemsetAsync(sums8, 0, 8 * sizeof(double), stream));
+  CK(launch_loss_sums(values, target, n, sums8, values_are_prob, stream));
+  return 0;
+}
+
+int unet_conv_fwd(const void* x, int ldx, const void* w, void* y, int ldy, const float* bias, const void* addend,
+                  int ldadd, double* stats, int N, int H, int W, int C, int P, int Q, int Cout, int R, int S,
+                  int stride, int pad, int mode, hipStream_t stream) {
+  ConvFwdArgs a = {};
+  a.x = (const bf16_t*)x; a.ldx = ldx; a.w = (const bf16_t*)w; a.y = (bf16_t*)y; a.ldy = ldy;
+  a.bias = bias; a.add = (const bf16_t*)addend; a.ldadd = ldadd; a.stats = stats;
+  a.N = N; a.H = H; a.W = W; a.C = C; a.P = P; a.Q = Q; a.Cout = Cout;
+  a.R = R; a.S = S; a.stride = stride; a.pad = pad;
+  if (mode < 0 || mode > 2) { set_err("bad mode"); return 1; }
+  CK(launch_conv_fwd(a, mode, stream));
+  return 0;
+}
+
+int unet_conv_wgrad(const void* dy, int lddy, const void* x, int ldx, float* dw_acc, int N, int H, int W, int C,
+                    int P, int Q, int Cout, int R, int S, int stride, int pad, int stem, hipStream_t stream) {
+  ConvWgradArgs a = {};
+  a.dy = (const bf16_t*)dy; a.lddy = lddy; a.x = (const bf16_t*)x; a.ldx = ldx; a.dw = dw_acc;
+  a.N = N; a.H = H; a.W = W; a.C = C; a.P = P; a.Q = Q; a.Cout = Cout;
+  a.R = R; a.S = S; a.stride = stride; a.pad = pad;
+  CK(launch_conv_wgrad(a, stem, stream));
+  return 0;
+}
+
+int unet_pack_weight(const float* src, void* dst, int kind, int Co, int Ci, int R, int S, hipStream_t stream) {
+  PackTable t;
+  t.n = 1;
+  t.e[0] = PackEntry{src, (bf16_t*)dst, kind, Co, Ci, R, S};
+  CK(launch_pack(t, stream));
+  return 0;
+}
+
+int unet_unpack_grad(const float* acc, float* dst, int kind, int Co, int Ci, int R, int S, hipStream_t stream) {
+  UnpackTable t;
+  t.n = 1;
+  t.e[0] = UnpackEntry{acc, dst, kind, Co, Ci, R, S};
+  CK(launch_unpack(t, stream));
+  return 0;
+}
+
+int unet_maxpool_fwd(const void* x, int ldx, void* y, uint8_t* idx, int N, int H, int W, int C,
+                     hipStream_t stream) {
+  MaxPoolArgs m = {};
+  m.x = (const bf16_t*)x; m.ldx = ldx; m.y = (bf16_t*)y; m.ldy = C; m.idx = idx;
+  m.N = N; m.H = H; m.W = W; m.C = C; m.P = (H + 1) / 2; m.Q = (W + 1) / 2;
+  CK(launch_maxpool_fwd(m, stream));
+  return 0;
+}
+
+int unet_maxpool_bwd(const void* dy, const uint8_t* idx, const void* addend, int ldadd, void* dx, int N, int H,
+                     int W, int C, hipStream_t stream) {
+  MaxPoolArgs m = {};
+  m.dy = (const bf16_t*)dy; m.lddy = C; m.idx = (uint8_t*)idx; m.add = (const bf16_t*)addend; m.ldadd = ldadd;
+  m.dx = (bf16_t*)dx; m.lddx = C;
+  m.N = N; m.H = H; m.W = W; m.C = C; m.P = (H + 1) / 2; m.Q = (W + 1) / 2;
+  CK(launch_maxpool_bwd(m, stream));
+  return 0;
+}
+
+}  // extern "C"

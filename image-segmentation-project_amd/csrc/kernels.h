@@ -1,0 +1,127 @@
+// Kernel argument blocks and launchers (internal to libunet_hip.so).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace unet {
+
+typedef unsigned short bf16_t;
+
+enum { MODE_FWD = 0, MODE_TRANS = 1, MODE_STEM = 2 };
+enum { ALOAD_NHWC = 0, ALOAD_STEM = 1 };
+enum { XLOAD_NHWC = 0, XLOAD_STEM = 1 };
+
+struct ConvFwdArgs {
+  const bf16_t* x; int ldx;      // input NHWC bf16, channel stride ldx (stem: fp32 [N,H,W])
+  const bf16_t* w;               // packed weights [Cout][R*S*C] (stem: [64][64])
+  bf16_t* y; int ldy;            // output NHWC bf16
+  const float* bias;             // [Cout] or null
+  const bf16_t* add; int ldadd;  // optional addend (same pixel grid as y)
+  double* stats;                 // optional BN sums [2][Cout] (fp64 atomics)
+  int N, H, W, C;                // input geometry (C = GEMM reduction channels)
+  int P, Q, Cout;                // output geometry
+  int R, S, stride, pad;
+  int mblocks, nblocks, Pc, Qc;  // filled by the launcher
+};
+
+struct ConvWgradArgs {
+  const bf16_t* dy; int lddy;    // gradient wrt conv output [N,P,Q,Cout]
+  const bf16_t* x; int ldx;      // conv input [N,H,W,C] (stem: fp32 image)
+  float* dw;                     // fp32 accumulator [Cout][R*S*C] (stem: [64][64])
+  int N, H, W, C, P, Q, Cout, R, S, stride, pad;
+  int px_per_split, co_blocks, c_blocks;  // filled by the launcher
+};
+
+hipError_t launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st);
+hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st);
+
+// ---- elementwise / reduction kernels (elementwise.hip) ----
+struct BnLaunch {
+  const double* stats; const float* gamma; const float* beta;
+  float* run_mean; float* run_var; float* save_mean; float* save_invstd;
+  double count; int C; float eps, momentum; int training;
+};
+
+// A = act( bn(Y) + residual ), residual: 0 none, 1 identity tensor R, 2 bn2(R)
+struct BnApplyArgs {
+  const bf16_t* y; int ldy;
+  bf16_t* out; int ldo;
+  const bf16_t* res; int ldr;
+  BnLaunch bn, bn2;
+  int64_t npix; int C; int res_mode; int relu;
+};
+hipError_t launch_bn_apply(const BnApplyArgs& a, hipStream_t st);
+
+// backward: dZ = dA * (A > 0); sums over pixels of dZ and dZ*xhat (and for bn2)
+struct BnBwdArgs {
+  const bf16_t* da; int ldda;
+  const bf16_t* act; int ldact;      // forward output (relu mask source)
+  const bf16_t* y; int ldy;          // raw conv output of bn
+  const bf16_t* y2; int ldy2;        // raw conv output of bn2 (downsample) or null
+  const float* mean; const float* invstd; const float* gamma;
+  const float* mean2; const float* invstd2; const float* gamma2;
+  double* sums;                      // [2][C]: sum dZ, sum dZ*xhat
+  double* sums2;                     // [2][C] for bn2
+  bf16_t* dy; int lddy;              // apply: dY out
+  bf16_t* dy2; int lddy2;            // apply: dY2 out (bn2)
+  bf16_t* dres; int lddres;          // apply: dZ out (identity residual) or null
+  float* dgamma; float* dbeta;       // apply: param grads (block 0)
+  float* dgamma2; float* dbeta2;
+  int64_t npix; int C; int relu;
+};
+hipError_t launch_bn_bwd_reduce(const BnBwdArgs& a, hipStream_t st);
+hipError_t launch_bn_bwd_apply(const BnBwdArgs& a, hipStream_t st);
+
+struct MaxPoolArgs {
+  const bf16_t* x; int ldx; bf16_t* y; int ldy; uint8_t* idx;
+  const bf16_t* dy; int lddy; const bf16_t* add; int ldadd; bf16_t* dx; int lddx;
+  int N, H, W, C, P, Q;
+};
+hipError_t launch_maxpool_fwd(const MaxPoolArgs& a, hipStream_t st);
+hipError_t launch_maxpool_bwd(const MaxPoolArgs& a, hipStream_t st);
+
+// fused ConvTranspose2d(k2,s2, Cin->16) + Conv1x1(16->1): logits[2i+a,2j+b] =
+// c0 + sum_c X[i,j,c] V[c][a][b],  V[c][ab] = sum_o Wf[o] W0[c][o][ab].
+struct HeadArgs {
+  const bf16_t* x; int ldx;          // decoder1 output [N,H,W,Cin]
+  const float* w0; const float* b0;  // upconv0 weight [Cin][Co][2][2], bias [Co]
+  const float* wf; const float* bf;  // conv_final weight [1][Co][1][1], bias [1]
+  float* logits;                     // [N,2H,2W]
+  const float* dl;                   // backward: dL/dlogits
+  bf16_t* dx; int lddx;              // backward: dL/dX
+  double* usum;                      // backward: [Cin*4 + 1] sums U[c][ab], S
+  float* gw0; float* gb0; float* gwf; float* gbf;  // param grads
+  int N, H, W, Cin, Co;
+};
+hipError_t launch_head_fwd(const HeadArgs& a, hipStream_t st);
+hipError_t launch_head_bwd(const HeadArgs& a, hipStream_t st);
+hipError_t launch_head_grads(const HeadArgs& a, hipStream_t st);
+
+// per-channel sum over pixels (ConvTranspose bias grads): out[c] = sum_px x[px][c]
+hipError_t launch_channel_sum(const bf16_t* x, int ldx, int64_t npix, int C, double* acc,
+                              hipStream_t st);
+hipError_t launch_d2f(const double* src, float* dst, int n, hipStream_t st);
+
+// weight (un)packing between torch fp32 layouts and kernel bf16 layouts
+enum { PK_CONV_FWD = 0, PK_CONV_DGRAD = 1, PK_CONVT_FWD = 2, PK_CONVT_DGRAD = 3, PK_STEM = 4 };
+struct PackEntry { const float* src; bf16_t* dst; int kind, Co, Ci, R, S; };
+enum { UP_CONV = 0, UP_CONVT = 1, UP_STEM = 2 };
+struct UnpackEntry { const float* acc; float* dst; int kind, Co, Ci, R, S; };
+constexpr int kMaxPack = 48;
+struct PackTable { int n; PackEntry e[kMaxPack]; };
+struct UnpackTable { int n; UnpackEntry e[kMaxPack]; };
+hipError_t launch_pack(const PackTable& t, hipStream_t st);
+hipError_t launch_unpack(const UnpackTable& t, hipStream_t st);
+
+// loss + metrics
+enum { LOSS_BCE = 0, LOSS_DICE = 1, LOSS_COMBO = 2 };
+// sums[0..8): sum bce, sum sig*y, sum sig, sum y, tp, fp, fn, tn
+hipError_t launch_loss_sums(const float* logits, const float* target, int64_t n, double* sums,
+                            int from_prob, hipStream_t st);
+hipError_t launch_loss_value(const double* sums, int64_t n, int kind, float alpha, float smooth,
+                             float* out, hipStream_t st);
+hipError_t launch_loss_grad(const float* logits, const float* target, int64_t n, const double* sums,
+                            int kind, float alpha, float smooth, const float* gscale, float* dl,
+                            hipStream_t st);
+
+}  // namespace unet

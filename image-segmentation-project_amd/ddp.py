@@ -1,0 +1,110 @@
+"""Data-parallel training over RCCL (torch.distributed 'nccl' backend = RCCL on
+ROCm), one process per MI355X.
+
+The reference has no distributed code; its insertion
+point is between ``loss.backward()`` and ``optimizer.step()`` (train.py:48-49).
+Here the reduction runs *inside* the native backward: ``unet_backward`` records
+one hipEvent per gradient bucket as soon as that bucket's gradients are final
+(decoder+head first, then enc4, enc3, enc2+enc1+stem), and each bucket's
+mean all-reduce is issued on a side stream that waits only for its own event, so
+RCCL traffic over xGMI overlaps the rest of the backward pass.  When
+``loss.backward()`` returns, the compute stream has been ordered after every
+collective, so the caller's ``optimizer.step()`` sees averaged gradients.
+
+BatchNorm statistics stay rank-local (standard DDP); ``sync_buffers`` broadcasts
+rank 0's running statistics (call it before evaluation / checkpointing).
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+
+
+class GradBucketReducer:
+    """Mean all-reduce of contiguous slices of one flat gradient buffer.
+
+    ``wait_bucket(b, stream)`` must order ``stream`` after the producer of bucket
+    ``b`` (the native backward's hipEvent); on CPU/gloo it can be a no-op.
+    """
+
+    def __init__(self, ranges: Sequence[Tuple[int, int]], group=None):
+        self.ranges = list(ranges)
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self._stream = None
+
+    def _avg_op(self):
+        if dist.get_backend(self.group) == "nccl":
+            return dist.ReduceOp.AVG, False
+        return dist.ReduceOp.SUM, True  # gloo: no AVG
+
+    def reduce(self, flat: torch.Tensor, wait_bucket: Optional[Callable[[int, object], None]] = None):
+        if self.world == 1:
+            return
+        op, divide = self._avg_op()
+        works: List = []
+        if flat.is_cuda:
+            if self._stream is None or self._stream.device != flat.device:
+                self._stream = torch.cuda.Stream(device=flat.device)
+            comm = self._stream
+            flat.record_stream(comm)
+            with torch.cuda.stream(comm):
+                for b, (lo, hi) in enumerate(self.ranges):
+                    if wait_bucket is not None:
+                        wait_bucket(b, comm)
+                    works.append(dist.all_reduce(flat[lo:hi], op=op, group=self.group, async_op=True))
+            for w in works:
+                w.wait()  # orders the current (compute) stream after the collective
+        else:
+            for b, (lo, hi) in enumerate(self.ranges):
+                if wait_bucket is not None:
+                    wait_bucket(b, None)
+                works.append(dist.all_reduce(flat[lo:hi], op=op, group=self.group, async_op=True))
+            for w in works:
+                w.wait()
+        if divide:
+            flat.div_(self.world)
+
+
+class _NativeDDP:
+    def __init__(self, group):
+        self.group = group
+        self._reducers = {}
+
+    def reduce(self, plan, grads: torch.Tensor):
+        red = self._reducers.get(id(plan))
+        if red is None:
+            red = GradBucketReducer(plan.buckets, self.group)
+            self._reducers = {id(plan): red}
+
+        def wait(b, stream):
+            _lib.check(plan.lib.unet_bucket_wait(plan.handle, b, stream.cuda_stream), "unet_bucket_wait")
+
+        red.reduce(grads, wait)
+
+
+def broadcast_state(model: torch.nn.Module, group=None, src: int = 0):
+    """Make every rank start from rank ``src``'s parameters and buffers."""
+    with torch.no_grad():
+        for t in list(model.parameters()) + list(model.buffers()):
+            dist.broadcast(t.data, src=src, group=group)
+
+
+def sync_buffers(model: torch.nn.Module, group=None, src: int = 0):
+    with torch.no_grad():
+        for b in model.buffers():
+            dist.broadcast(b.data, src=src, group=group)
+
+
+def enable_data_parallel(model, group=None, broadcast: bool = True):
+    """Turn ``model`` (a UNetWithBackbone on this rank's GPU) into a DDP replica."""
+    if not dist.is_initialized():
+        raise RuntimeError("torch.distributed is not initialised (init_process_group('nccl'))")
+    if broadcast:
+        broadcast_state(model, group)
+    model._ddp = _NativeDDP(group)
+    return model

@@ -1,0 +1,171 @@
+"""Training loop on MI355X — the API of /root/reference/train.py:17-364.
+
+``train_epoch`` / ``evaluate`` keep the reference's per-batch semantics
+(forward, criterion, ``zero_grad`` after the forward, backward, ``step``; train
+metrics from the pre-step logits in train-mode BN; batch-size-weighted means of
+per-batch metrics, train.py:38-68,89-112).  What changes is where the work
+runs: the model/criterion are the HIP path, the per-batch mask counts are one
+fused kernel on the logits, and the five ``.item()`` syncs per batch become one
+device->host copy per epoch.
+
+``train_model`` keeps the epoch loop control of train.py:115-244 (ReduceLROnPlateau
+on val IoU, best-state deepcopy, EarlyStopping, returned dict) but takes
+in-memory tensors instead of image paths: the cv2/albumentations data pipeline
+is outside the hot path.
+"""
+from __future__ import annotations
+
+import copy
+import time
+from collections import defaultdict
+from typing import Dict, Optional
+
+import torch
+
+from .utils import EarlyStopping, mask_counts, metrics_from_counts
+
+
+def _batch_record(logits, masks, loss, n):
+    counts = mask_counts(logits.detach(), masks, from_logits=True)[4:8]
+    return counts, loss.detach().reshape(1).float(), n
+
+
+def _finish(records, with_loss_key: bool) -> Dict:
+    if not records:
+        return defaultdict(float)
+    counts = torch.stack([r[0] for r in records]).cpu().tolist()
+    losses = torch.cat([r[1] for r in records]).cpu().tolist()
+    out = defaultdict(float)
+    total = 0
+    loss_sum = 0.0
+    for (c, loss_v, (_, _, b)) in zip(counts, losses, records):
+        m = metrics_from_counts(*c)
+        for k, v in m.items():
+            out[k] += v * b
+        loss_sum += loss_v * b  # == loss.item() (fp32 value as Python float)
+        total += b
+    for k in list(out):
+        out[k] /= total
+    if with_loss_key:
+        out["loss"] = loss_sum / total
+    return out
+
+
+def train_epoch(model: torch.nn.Module, loader, optimizer: torch.optim.Optimizer, criterion: torch.nn.Module,
+                device: torch.device) -> Dict:
+    """train.py:17-68."""
+    model.train()
+    records = []
+    for images, masks in loader:
+        images = images.to(device, non_blocking=True)
+        masks = masks.to(device, non_blocking=True)
+        outputs = model(images)
+        loss = criterion(outputs, masks)
+        optimizer.zero_grad()
+        loss.backward()
+        optimizer.step()
+        with torch.no_grad():
+            records.append(_batch_record(outputs, masks, loss, images.size(0)))
+    return _finish(records, with_loss_key=True)
+
+
+def evaluate(model: torch.nn.Module, loader, device: torch.device, criterion: torch.nn.Module) -> Dict:
+    """train.py:71-112 (eval-mode BN, no grad)."""
+    model.eval()
+    records = []
+    with torch.no_grad():
+        for images, masks in loader:
+            images = images.to(device, non_blocking=True)
+            masks = masks.to(device, non_blocking=True)
+            outputs = model(images)
+            loss = criterion(outputs, masks)
+            records.append(_batch_record(outputs, masks, loss, images.size(0)))
+    return _finish(records, with_loss_key=True)
+
+
+class TensorLoader:
+    """Minimal in-memory replacement for ``prepare_data`` (dataset.py:121-138)."""
+
+    def __init__(self, images, masks, batch_size, shuffle=False, seed=0):
+        self.images = torch.as_tensor(images)
+        self.masks = torch.as_tensor(masks)
+        self.batch_size = batch_size
+        self.shuffle = shuffle
+        self.gen = torch.Generator().manual_seed(seed)
+
+    def __len__(self):
+        return (len(self.images) + self.batch_size - 1) // self.batch_size
+
+    def __iter__(self):
+        n = len(self.images)
+        order = torch.randperm(n, generator=self.gen) if self.shuffle else torch.arange(n)
+        for i in range(0, n, self.batch_size):
+            idx = order[i:i + self.batch_size]
+            yield self.images[idx], self.masks[idx]
+
+
+def train_model(model, train_images, train_masks, val_images, val_masks, criterion, optimizer,
+                scheduler: Optional[object], num_epochs: int, device, config: Dict,
+                augmentations_per_image: int = 0, save_plots: bool = True) -> Dict:
+    """train.py:115-244 epoch loop over in-memory tensors [N,1,H,W]."""
+    if augmentations_per_image:
+        raise NotImplementedError("CellAugmenter (dataset.py:140-210) is outside the MI355X hot path")
+    if isinstance(train_images, (list, tuple)) and train_images and isinstance(train_images[0], str):
+        raise NotImplementedError("image paths need the cv2 pipeline (dataset.py:17-66); pass tensors")
+    train_loader = TensorLoader(train_images, train_masks, config["batch_size"], shuffle=True)
+    val_loader = TensorLoader(val_images, val_masks, config["batch_size"], shuffle=False)
+    train_hist, val_hist, lr_hist = [], [], []
+    best_iou, best_state, best_epoch = 0.0, None, 0
+    stopper = EarlyStopping(patience=config.get("early_stopping_patience", 7),
+                            min_delta=config.get("early_stopping_min_delta", 0.001))
+    verbose = config.get("verbose", True)
+    start = time.time()
+    train_metrics = val_metrics = None
+    for epoch in range(num_epochs):
+        train_metrics = train_epoch(model, train_loader, optimizer, criterion, device)
+        train_hist.append(train_metrics)
+        val_metrics = evaluate(model, val_loader, device, criterion)
+        val_hist.append(val_metrics)
+        if scheduler is not None:
+            if isinstance(scheduler, torch.optim.lr_scheduler.ReduceLROnPlateau):
+                scheduler.step(val_metrics["iou"])
+            else:
+                scheduler.step()
+        lr = optimizer.param_groups[0]["lr"]
+        lr_hist.append(lr)
+        if verbose:
+            print(f"Epoch {epoch + 1:3d}/{num_epochs} - Train Loss: {train_metrics['loss']:.4f}, "
+                  f"Train IoU: {train_metrics['iou']:.4f}, Val Loss: {val_metrics['loss']:.4f}, "
+                  f"Val IoU: {val_metrics['iou']:.4f}, LR: {lr:.6f}")
+        if val_metrics["iou"] > best_iou:
+            best_iou = val_metrics["iou"]
+            best_state = copy.deepcopy(model.state_dict())
+            best_epoch = epoch
+        if stopper.step(val_metrics["iou"]):
+            if verbose:
+                print(f"Early stopping triggered at epoch {epoch + 1}")
+            break
+    elapsed = time.time() - start
+    if best_state is not None:
+        model.load_state_dict(best_state)
+    return {"train_metrics": train_hist, "val_metrics": val_hist, "lr_history": lr_hist, "best_iou": best_iou,
+            "best_epoch": best_epoch, "best_model_state": best_state, "training_time": elapsed,
+            "final_train_metrics": train_metrics, "final_val_metrics": val_metrics}
+
+
+def quick_train(model, train_images, train_masks, val_images, val_masks, config: Dict, device=None,
+                augmentations_per_image: int = 0) -> Dict:
+    """train.py:301-364: Adam (coupled L2) + ReduceLROnPlateau(max, 0.5, thr 0.01, min 1e-6)."""
+    from .losses import get_loss_function
+    from .utils import get_device
+    device = device or get_device()
+    model = model.to(device)
+    criterion = get_loss_function(config)
+    optimizer = torch.optim.Adam(model.parameters(), lr=config.get("learning_rate", 1e-3),
+                                 weight_decay=config.get("weight_decay", 1e-5))
+    scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optimizer, mode="max", factor=0.5,
+                                                           patience=config.get("scheduler_patience", 3),
+                                                           threshold=0.01, min_lr=1e-6)
+    return train_model(model, train_images, train_masks, val_images, val_masks, criterion, optimizer, scheduler,
+                       config.get("num_epochs", 50), device, config, augmentations_per_image,
+                       config.get("save_plots", True))

@@ -1,0 +1,108 @@
+/* unet_hip.h — C ABI of libunet_hip.so, the MI355X (gfx950) U-Net training path.
+ *
+ * Drop-in boundary for the reference's hot path (SwagMag1213/image-segmentation-
+ * project, /root/reference).  The reference is pure Python over PyTorch, so its
+ * "FFI" is the Python API; each entry point below replaces the compute under one
+ * reference call (file:line in /root/reference):
+ *
+ *   unet_forward         UNetWithBackbone.forward (advanced_models.py:264-357),
+ *                        resnet34 encoder (:72-100), use_attention=False
+ *   unet_backward        loss.backward() through that graph (train.py:48)
+ *   unet_bucket_wait     DDP gradient reduction insertion point between
+ *                        loss.backward() and optimizer.step() (train.py:48-49)
+ *   unet_loss_forward    BCELoss / DiceLoss / ComboLoss forward (losses.py:13-37,161-171)
+ *   unet_loss_backward   their gradient wrt the logits
+ *   unet_mask_metrics    calculate_metrics tp/fp/fn/tn counts (utils.py:120-151)
+ *   unet_conv_* / unet_maxpool_* / unet_bn_*   single ops of the graph above
+ *                        (torchvision BasicBlock, advanced_models.py:197-205) for tests
+ *
+ * Conventions: every pointer is a DEVICE pointer owned by the caller (PyTorch's
+ * caching allocator); the library never allocates or frees on the hot path.
+ * Activations are bf16 NHWC; parameters / grads fp32 in torch layouts.  All work
+ * is enqueued asynchronously on the given hipStream_t.  Every function returns
+ * 0 on success or a non-zero hipError_t-style code; unet_last_error() gives a
+ * thread-local message.  No C++ exception crosses the ABI.
+ */
+#ifndef UNET_HIP_H
+#define UNET_HIP_H
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct unet_plan unet_plan;
+
+typedef struct unet_config {
+  int N, H, W;       /* batch and input size (H, W multiples of 32)            */
+  int width;         /* channel multiplier: 1 = resnet34 U-Net (64..512)       */
+  int n_classes;     /* must be 1 (binary segmentation, advanced_models.py:160) */
+  float bn_eps;      /* 1e-5  (torch.nn.BatchNorm2d default)                   */
+  float bn_momentum; /* 0.1                                                    */
+} unet_config;
+
+const char* unet_last_error(void);
+const char* unet_version(void);
+
+/* ---- plan: layer graph, parameter table, workspace layout ---- */
+int unet_plan_create(const unet_config* cfg, unet_plan** out);
+void unet_plan_destroy(unet_plan* p);
+int64_t unet_plan_workspace_bytes(const unet_plan* p);
+int unet_plan_num_params(const unet_plan* p);
+int unet_plan_param_name(const unet_plan* p, int i, char* buf, int buflen);
+int unet_plan_param_shape(const unet_plan* p, int i, int64_t shape[4]); /* returns ndim */
+int64_t unet_plan_param_offset(const unet_plan* p, int i);             /* in flat grads */
+int64_t unet_plan_grad_numel(const unet_plan* p);
+int unet_plan_num_bn(const unet_plan* p);
+int unet_plan_num_buckets(const unet_plan* p);
+int unet_plan_bucket_range(const unet_plan* p, int b, int64_t* begin, int64_t* end);
+double unet_plan_flops(const unet_plan* p, int training); /* algorithmic FLOPs per step */
+
+/* params[i]: fp32 tensors in unet_plan_param_name order (== reference
+ * state_dict parameter order); buffers[3*k+0/1]: running_mean/var of BN k in
+ * named_buffers order (num_batches_tracked slots are ignored). */
+int unet_forward(unet_plan* p, const float* image, const float* const* params, float* const* buffers,
+                 void* workspace, float* logits, int training, hipStream_t stream);
+/* grads: flat fp32 [unet_plan_grad_numel], param i at unet_plan_param_offset(i). */
+int unet_backward(unet_plan* p, const float* image, const float* dlogits, const float* const* params,
+                  void* workspace, float* grads, hipStream_t stream);
+/* make `waiter` wait until bucket b of the last unet_backward is final */
+int unet_bucket_wait(unet_plan* p, int bucket, hipStream_t waiter);
+
+/* ---- loss + metrics (kind: 0 bce, 1 dice, 2 combo) ---- */
+int unet_loss_forward(const float* logits, const float* target, int64_t n, int kind, float alpha,
+                      float smooth, double* sums8, float* loss_out, hipStream_t stream);
+int unet_loss_backward(const float* logits, const float* target, int64_t n, int kind, float alpha,
+                       float smooth, const double* sums8, const float* grad_scale, float* dlogits,
+                       hipStream_t stream);
+/* sums8[4..8) = tp, fp, fn, tn.  values_are_prob=0: logits (mask = sigmoid>0.5
+ * evaluated bit-exactly as logit >= 0x33C00001); 1: probabilities (p > 0.5). */
+int unet_mask_metrics(const float* values, const float* target, int64_t n, int values_are_prob,
+                      double* sums8, hipStream_t stream);
+
+/* ---- single ops (tests / custom graphs) ---- */
+/* mode 0: conv  y = conv(x, w) [stride, pad]           (w packed [Cout][R][S][C])
+ * mode 1: transposed gather (conv dgrad / ConvTranspose2d forward)
+ * mode 2: 7x7 stem on an fp32 single-channel image     (w packed [64][64]) */
+int unet_conv_fwd(const void* x, int ldx, const void* w, void* y, int ldy, const float* bias,
+                  const void* addend, int ldadd, double* stats, int N, int H, int W, int C, int P,
+                  int Q, int Cout, int R, int S, int stride, int pad, int mode, hipStream_t stream);
+int unet_conv_wgrad(const void* dy, int lddy, const void* x, int ldx, float* dw_acc, int N, int H,
+                    int W, int C, int P, int Q, int Cout, int R, int S, int stride, int pad, int stem,
+                    hipStream_t stream);
+/* kind: 0 conv fwd, 1 conv dgrad, 2 convT fwd, 3 convT dgrad, 4 stem */
+int unet_pack_weight(const float* src, void* dst, int kind, int Co, int Ci, int R, int S,
+                     hipStream_t stream);
+/* kind: 0 conv [Co][R][S][Ci] -> [Co][Ci][R][S], 1 convT, 2 stem */
+int unet_unpack_grad(const float* acc, float* dst, int kind, int Co, int Ci, int R, int S,
+                     hipStream_t stream);
+int unet_maxpool_fwd(const void* x, int ldx, void* y, uint8_t* idx, int N, int H, int W, int C,
+                     hipStream_t stream);
+int unet_maxpool_bwd(const void* dy, const uint8_t* idx, const void* addend, int ldadd, void* dx,
+                     int N, int H, int W, int C, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UNET_HIP_H */

@@ -1,0 +1,137 @@
+"""CPU checks of the drop-in boundary: the C-ABI library loads and exports every
+symbol include/unet_hip.h declares, the native plan reproduces the reference
+parameter table, and the product path refuses to fall back to the CPU."""
+import copy
+import ctypes
+import importlib
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    src = open(os.path.join(REPO, "include", "unet_hip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(unet_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol(pkg):
+    lib_mod = importlib.import_module("image-segmentation-project_amd._lib")
+    lib = lib_mod.load()
+    syms = _declared_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(lib, s), s
+        assert s in lib_mod.SIGNATURES, f"{s} has no ctypes signature"
+    assert b"gfx950" in lib.unet_version()
+
+
+def test_plan_matches_reference_parameter_table(pkg):
+    am = importlib.import_module("image-segmentation-project_amd.advanced_models")
+    plan = am._Plan(4, 64, 64, 1, 1, torch.device("cpu"))
+    ref = oracle.ReferenceUNet()
+    names = [k for k, _ in ref.named_parameters()]
+    assert plan.param_names == names
+    assert plan.param_shapes == [tuple(p.shape) for _, p in ref.named_parameters()]
+    offs = np.cumsum([0] + [p.numel() for p in ref.parameters()])[:-1]
+    assert plan.param_offsets == list(offs)
+    assert plan.grad_numel == 24339457
+    # buckets tile the flat gradient buffer exactly, in backward order
+    b = plan.buckets
+    assert b[0][1] == plan.grad_numel and b[-1][0] == 0
+    assert all(b[i][0] == b[i + 1][1] for i in range(len(b) - 1))
+
+
+def test_algorithmic_flops_match_survey(pkg):
+    am = importlib.import_module("image-segmentation-project_amd.advanced_models")
+    plan = am._Plan(16, 512, 512, 1, 1, torch.device("cpu"))
+    assert abs(plan.flops_fwd / 16 / 1e9 - 54.509) < 1e-3
+    assert abs(plan.flops_train / 16 / 1e9 - 163.1165) < 1e-3  # 3 x fwd - stem dgrad
+    hi = am._Plan(4, 1024, 1024, 1, 1, torch.device("cpu"))
+    assert abs(hi.flops_train / 4 / 1e9 - 652.5) < 0.1
+
+
+def test_plan_rejects_bad_shapes(pkg):
+    am = importlib.import_module("image-segmentation-project_amd.advanced_models")
+    with pytest.raises(RuntimeError, match="multiples of 32"):
+        am._Plan(2, 100, 100, 1, 1, torch.device("cpu"))
+
+
+def test_module_state_dict_equals_reference_layout(pkg):
+    m = pkg.UNetWithBackbone(n_classes=1, backbone="resnet34", pretrained=False, use_attention=False)
+    ref = oracle.ReferenceUNet()
+    assert [(k, tuple(v.shape)) for k, v in m.state_dict().items()] == \
+        [(k, tuple(v.shape)) for k, v in ref.state_dict().items()]
+    sd = oracle.closed_form_state_dict(ref)
+    m.load_state_dict(sd)
+    m2 = copy.deepcopy(m)
+    for (k, a), (_, b) in zip(m.state_dict().items(), m2.state_dict().items()):
+        assert torch.equal(a, b), k
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-5)
+    assert len(opt.param_groups[0]["params"]) == 152
+
+
+def test_unsupported_configs_raise(pkg):
+    with pytest.raises(NotImplementedError):
+        pkg.UNetWithBackbone(backbone="resnet50", pretrained=False, use_attention=False)
+    with pytest.raises(NotImplementedError):
+        pkg.UNetWithBackbone(pretrained=False, use_attention=True)
+    with pytest.warns(RuntimeWarning):
+        pkg.UNetWithBackbone(pretrained=True, use_attention=False)
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure mode")
+def test_no_cpu_fallback(pkg):
+    m = pkg.UNetWithBackbone(pretrained=False, use_attention=False)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        m(torch.zeros(1, 1, 64, 64))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        pkg.BCELoss()(torch.zeros(4), torch.zeros(4))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        pkg.calculate_metrics(torch.zeros(4), torch.zeros(4))
+
+
+def test_loss_registry(pkg, capsys):
+    assert isinstance(pkg.get_loss_function({}), pkg.ComboLoss)
+    assert isinstance(pkg.get_loss_function({"loss_fn": "bce"}), pkg.BCELoss)
+    d = pkg.get_loss_function({"loss_fn": "dice", "smooth": 2.0})
+    assert isinstance(d, pkg.DiceLoss) and d.smooth == 2.0
+    c = pkg.get_loss_function({"loss_fn": "nope", "loss_alpha": 0.3})
+    assert isinstance(c, pkg.ComboLoss) and c.alpha == 0.3
+    assert "Unknown loss function 'nope'" in capsys.readouterr().out
+    with pytest.raises(NotImplementedError):
+        pkg.get_loss_function({"loss_fn": "focal"})
+
+
+def test_early_stopping_matches_reference_semantics(pkg):
+    es = pkg.EarlyStopping(patience=2, min_delta=0.01)
+    seq = [0.5, 0.505, 0.509, 0.6, 0.6]
+    out = [es.step(v) for v in seq]
+    assert out == [False, False, True, True, True]  # early_stop latches (utils.py:182-190)
+
+
+def test_metrics_formula_matches_reference(pkg, golden):
+    utils = importlib.import_module("image-segmentation-project_amd.utils")
+    g = golden("mask_metrics.npz")
+    keys = list(g["metric_keys"])
+    cases = {"empty_both": (0, 0, 0, 64), "all_fg": (64, 0, 0, 0), "pred_only": (0, 64, 0, 0),
+             "half": (16, 16, 0, 32)}
+    for name, c in cases.items():
+        m = utils.metrics_from_counts(*map(float, c))
+        assert [m[k] for k in keys] == list(g["edge/" + name]), name
+
+
+def test_synthetic_cells(pkg):
+    x, m = pkg.synthetic_cells(2, 128, 128, seed=1234)
+    assert x.shape == (2, 1, 128, 128) and x.dtype == np.float32
+    assert x.min() >= 0 and x.max() <= 1
+    assert set(np.unique(m)) <= {0.0, 1.0}
+    x2, _ = pkg.synthetic_cells(2, 128, 128, seed=1234)
+    assert np.array_equal(x, x2)

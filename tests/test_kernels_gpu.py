@@ -1,0 +1,238 @@
+"""Single-op parity of the gfx950 kernels against torch fp32 on the same
+bf16-rounded operands (CPU reference).  Tolerance: outputs are stored in bf16
+(relative rounding 2^-8) after fp32 accumulation, so |err| <= 1e-2 * max|ref|
++ 1e-2 * |ref| elementwise; fp32 weight gradients: 2e-3 * max|ref|."""
+import importlib
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+PK_CONV_FWD, PK_CONV_DGRAD, PK_CONVT_FWD, PK_CONVT_DGRAD, PK_STEM = range(5)
+
+
+@pytest.fixture(scope="module")
+def L(pkg):
+    return importlib.import_module("image-segmentation-project_amd._lib").load()
+
+
+def S():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(t):
+    return t.permute(0, 3, 1, 2)
+
+
+def bf(t):
+    return t.to(torch.bfloat16)
+
+
+def close(got, ref, rel=1e-2):
+    got, ref = got.float().cpu(), ref.float().cpu()
+    tol = rel * ref.abs().max().item() + rel * ref.abs()
+    err = (got - ref).abs()
+    bad = (err > tol).sum().item()
+    assert bad == 0, f"{bad} / {ref.numel()} elements off; max err {err.max().item():.4g} (ref max {ref.abs().max().item():.4g})"
+
+
+def pack(L, w, kind, Co, Ci, R, S_):
+    n = Co * 64 if kind == PK_STEM else w.numel()
+    dst = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+    assert L.unet_pack_weight(w.data_ptr(), dst.data_ptr(), kind, Co, Ci, R, S_, S()) == 0
+    return dst
+
+
+def conv_fwd(L, x, wp, N, H, W, C, P, Q, Co, R, stride, pad, mode, bias=None, add=None, stats=None, ldy=None, y=None):
+    ldy = ldy or Co
+    if y is None:
+        y = torch.empty(N, P, Q, ldy, dtype=torch.bfloat16, device="cuda")
+    rc = L.unet_conv_fwd(x.data_ptr(), x.shape[-1] if x.dim() == 4 else 1, wp.data_ptr(), y.data_ptr(), ldy,
+                         0 if bias is None else bias.data_ptr(), 0 if add is None else add.data_ptr(),
+                         0 if add is None else add.shape[-1], 0 if stats is None else stats.data_ptr(),
+                         N, H, W, C, P, Q, Co, R, R, stride, pad, mode, S())
+    assert rc == 0, L.unet_last_error()
+    return y
+
+
+CASES_FWD = [  # N, C, H, Co, R, stride, pad
+    (2, 64, 16, 64, 3, 1, 1),
+    (2, 96, 16, 32, 3, 1, 1),
+    (2, 32, 16, 32, 3, 1, 1),
+    (1, 128, 32, 128, 3, 1, 1),
+    (2, 128, 128, 128, 3, 1, 1),   # M = 32768 -> 128x128 tile
+    (2, 64, 32, 128, 3, 2, 1),
+    (2, 64, 32, 128, 1, 2, 0),
+    (2, 512, 8, 512, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", CASES_FWD)
+def test_conv_fwd_bias_stats(L, case, cuda):
+    N, C, H, Co, R, st, pad = case
+    g = torch.Generator().manual_seed(1)
+    x = bf(torch.randn(N, C, H, H, generator=g))
+    w = torch.randn(Co, C, R, R, generator=g) / (C * R * R) ** 0.5
+    b = torch.randn(Co, generator=g)
+    wb = bf(w).float()
+    ref = F.conv2d(x.float(), wb, b, stride=st, padding=pad)
+    P = ref.shape[2]
+    wg = w.cuda()
+    wp = pack(L, wg, PK_CONV_FWD, Co, C, R, R)
+    stats = torch.zeros(2 * Co, dtype=torch.float64, device="cuda")
+    y = conv_fwd(L, nhwc(x).cuda(), wp, N, H, H, C, P, P, Co, R, st, pad, 0, bias=b.cuda(), stats=stats)
+    torch.cuda.synchronize()
+    close(nchw(y), ref)
+    s = stats.cpu()
+    torch.testing.assert_close(s[:Co], ref.double().sum((0, 2, 3)), rtol=1e-3, atol=1e-2 * ref.abs().max().item() * 10)
+    torch.testing.assert_close(s[Co:], ref.double().pow(2).sum((0, 2, 3)), rtol=1e-3, atol=1.0)
+
+
+CASES_DGRAD = [  # N, Ci, H, Co, R, stride, pad  (forward geometry)
+    (2, 64, 16, 64, 3, 1, 1),
+    (2, 96, 16, 32, 3, 1, 1),
+    (2, 64, 32, 128, 3, 2, 1),
+    (2, 64, 32, 128, 1, 2, 0),
+    (1, 256, 16, 512, 3, 2, 1),
+]
+
+
+@pytest.mark.parametrize("case", CASES_DGRAD)
+def test_conv_dgrad_with_addend(L, case, cuda):
+    N, Ci, H, Co, R, st, pad = case
+    g = torch.Generator().manual_seed(2)
+    w = torch.randn(Co, Ci, R, R, generator=g) / (Ci * R * R) ** 0.5
+    P = (H + 2 * pad - R) // st + 1
+    dy = bf(torch.randn(N, Co, P, P, generator=g))
+    add = bf(torch.randn(N, Ci, H, H, generator=g))
+    ref = torch.nn.grad.conv2d_input((N, Ci, H, H), bf(w).float(), dy.float(), stride=st, padding=pad) + add.float()
+    wp = pack(L, w.cuda(), PK_CONV_DGRAD, Co, Ci, R, R)
+    dx = conv_fwd(L, nhwc(dy).cuda(), wp, N, P, P, Co, H, H, Ci, R, st, pad, 1, add=nhwc(add).cuda())
+    torch.cuda.synchronize()
+    close(nchw(dx), ref)
+
+
+@pytest.mark.parametrize("Ci,Co,H", [(512, 256, 8), (64, 32, 16), (128, 64, 16)])
+def test_convT_fwd_and_dgrad(L, Ci, Co, H, cuda):
+    N = 2
+    g = torch.Generator().manual_seed(3)
+    x = bf(torch.randn(N, Ci, H, H, generator=g))
+    w = torch.randn(Ci, Co, 2, 2, generator=g) / Ci ** 0.5
+    b = torch.randn(Co, generator=g)
+    wb = bf(w).float()
+    ref = F.conv_transpose2d(x.float(), wb, b, stride=2)
+    wp = pack(L, w.cuda(), PK_CONVT_FWD, Co, Ci, 2, 2)
+    # write into a concat slice: ld = Co + 16, channel offset 16
+    ld = Co + 16
+    ybuf = torch.zeros(N, 2 * H, 2 * H, ld, dtype=torch.bfloat16, device="cuda")
+    ysl = ybuf[..., 16:]
+    xg, bg = nhwc(x).cuda(), b.cuda()  # keep alive across the async launch
+    rc = L.unet_conv_fwd(xg.data_ptr(), Ci, wp.data_ptr(), ysl.data_ptr(), ld, bg.data_ptr(), 0, 0, 0,
+                         N, H, H, Ci, 2 * H, 2 * H, Co, 2, 2, 2, 0, 1, S())
+    assert rc == 0, L.unet_last_error()
+    torch.cuda.synchronize()
+    close(nchw(ysl), ref)
+    assert ybuf[..., :16].abs().sum().item() == 0  # skip half untouched
+    # dgrad: ordinary k2s2 conv of dY
+    dy = bf(torch.randn(N, Co, 2 * H, 2 * H, generator=g))
+    xr = x.float().requires_grad_(True)
+    F.conv_transpose2d(xr, wb, None, stride=2).backward(dy.float())
+    wpd = pack(L, w.cuda(), PK_CONVT_DGRAD, Co, Ci, 2, 2)
+    dx = conv_fwd(L, nhwc(dy).cuda(), wpd, N, 2 * H, 2 * H, Co, H, H, Ci, 2, 2, 0, 0)
+    torch.cuda.synchronize()
+    close(nchw(dx), xr.grad)
+
+
+def wgrad(L, dy, x, N, H, W, C, P, Q, Co, R, st, pad, stem=0):
+    n = Co * 64 if stem else Co * R * R * C
+    acc = torch.zeros(n, dtype=torch.float32, device="cuda")
+    rc = L.unet_conv_wgrad(dy.data_ptr(), dy.shape[-1], x.data_ptr(), x.shape[-1] if x.dim() == 4 else 1,
+                           acc.data_ptr(), N, H, W, C, P, Q, Co, R, R, st, pad, stem, S())
+    assert rc == 0, L.unet_last_error()
+    return acc
+
+
+@pytest.mark.parametrize("case", CASES_DGRAD + [(2, 128, 32, 128, 3, 1, 1), (4, 32, 32, 32, 3, 1, 1)])
+def test_conv_wgrad(L, case, cuda):
+    N, Ci, H, Co, R, st, pad = case
+    g = torch.Generator().manual_seed(4)
+    x = bf(torch.randn(N, Ci, H, H, generator=g))
+    P = (H + 2 * pad - R) // st + 1
+    dy = bf(torch.randn(N, Co, P, P, generator=g))
+    ref = torch.nn.grad.conv2d_weight(x.float(), (Co, Ci, R, R), dy.float(), stride=st, padding=pad)
+    acc = wgrad(L, nhwc(dy).cuda(), nhwc(x).cuda(), N, H, H, Ci, P, P, Co, R, st, pad)
+    out = torch.empty(Co, Ci, R, R, device="cuda")
+    assert L.unet_unpack_grad(acc.data_ptr(), out.data_ptr(), 0, Co, Ci, R, R, S()) == 0
+    torch.cuda.synchronize()
+    close(out, ref, rel=2e-3)
+
+
+def test_convT_wgrad(L, cuda):
+    N, Ci, Co, H = 2, 128, 64, 16
+    g = torch.Generator().manual_seed(5)
+    x = bf(torch.randn(N, Ci, H, H, generator=g))
+    dy = bf(torch.randn(N, Co, 2 * H, 2 * H, generator=g))
+    w = torch.zeros(Ci, Co, 2, 2, requires_grad=True)
+    F.conv_transpose2d(x.float(), w, None, stride=2).backward(dy.float())
+    # convT wgrad = conv wgrad with dy := X (Cout = Ci), x := dY (C = Co), k2 s2
+    acc = wgrad(L, nhwc(x).cuda(), nhwc(dy).cuda(), N, 2 * H, 2 * H, Co, H, H, Ci, 2, 2, 0)
+    out = torch.empty(Ci, Co, 2, 2, device="cuda")
+    assert L.unet_unpack_grad(acc.data_ptr(), out.data_ptr(), 1, Co, Ci, 2, 2, S()) == 0
+    torch.cuda.synchronize()
+    close(out, w.grad, rel=2e-3)
+
+
+def test_stem_fwd_and_wgrad(L, cuda):
+    N, H, Co = 2, 64, 64
+    g = torch.Generator().manual_seed(6)
+    img = torch.rand(N, 1, H, H, generator=g)
+    w = torch.randn(Co, 1, 7, 7, generator=g) / 7.0
+    ref = F.conv2d(bf(img).float(), bf(w).float(), stride=2, padding=3)
+    wp = pack(L, w.cuda(), PK_STEM, Co, 1, 7, 7)
+    x = img.cuda().contiguous()
+    y = torch.empty(N, H // 2, H // 2, Co, dtype=torch.bfloat16, device="cuda")
+    rc = L.unet_conv_fwd(x.data_ptr(), 1, wp.data_ptr(), y.data_ptr(), Co, 0, 0, 0, 0,
+                         N, H, H, 1, H // 2, H // 2, Co, 7, 7, 2, 3, 2, S())
+    assert rc == 0, L.unet_last_error()
+    torch.cuda.synchronize()
+    close(nchw(y), ref)
+    dy = bf(torch.randn(N, Co, H // 2, H // 2, generator=g))
+    wref = torch.nn.grad.conv2d_weight(bf(img).float(), (Co, 1, 7, 7), dy.float(), stride=2, padding=3)
+    acc = wgrad(L, nhwc(dy).cuda(), x, N, H, H, 1, H // 2, H // 2, Co, 7, 2, 3, stem=1)
+    out = torch.empty(Co, 1, 7, 7, device="cuda")
+    assert L.unet_unpack_grad(acc.data_ptr(), out.data_ptr(), 2, Co, 1, 7, 7, S()) == 0
+    torch.cuda.synchronize()
+    close(out, wref, rel=2e-3)
+
+
+def test_maxpool_fwd_bwd(L, cuda):
+    N, C, H = 2, 64, 32
+    g = torch.Generator().manual_seed(7)
+    x = bf(torch.randn(N, C, H, H, generator=g)).relu()  # ties at 0, like post-ReLU
+    # a slice of a wider (concat) buffer as input
+    buf = torch.zeros(N, H, H, C + 32, dtype=torch.bfloat16, device="cuda")
+    buf[..., :C] = nhwc(x).cuda()
+    xs = buf[..., :C]
+    P = H // 2
+    y = torch.empty(N, P, P, C, dtype=torch.bfloat16, device="cuda")
+    idx = torch.empty(N, P, P, C, dtype=torch.uint8, device="cuda")
+    assert L.unet_maxpool_fwd(xs.data_ptr(), C + 32, y.data_ptr(), idx.data_ptr(), N, H, H, C, S()) == 0
+    xr = x.float().requires_grad_(True)
+    ref, _ = F.max_pool2d(xr, 3, 2, 1, return_indices=True)
+    torch.cuda.synchronize()
+    assert torch.equal(nchw(y).float().cpu(), ref.detach())
+    dy = bf(torch.randn(N, C, P, P, generator=g))
+    ref.backward(dy.float())
+    add = bf(torch.randn(N, C, H, H, generator=g))
+    dx = torch.empty(N, H, H, C, dtype=torch.bfloat16, device="cuda")
+    addn, dyg = nhwc(add).cuda(), nhwc(dy).cuda()
+    assert L.unet_maxpool_bwd(dyg.data_ptr(), idx.data_ptr(), addn.data_ptr(), C, dx.data_ptr(),
+                              N, H, H, C, S()) == 0
+    torch.cuda.synchronize()
+    close(nchw(dx), xr.grad + add.float())
