@@ -41,6 +41,8 @@ SIGNATURES = {
     "unet_plan_num_buckets": (c_int, [c_void_p]),
     "unet_plan_bucket_range": (c_int, [c_void_p, c_int, ctypes.POINTER(c_int64), ctypes.POINTER(c_int64)]),
     "unet_plan_flops": (c_double, [c_void_p, c_int]),
+    "unet_plan_num_tensors": (c_int, [c_void_p]),
+    "unet_plan_tensor_info": (c_int, [c_void_p, c_int, ctypes.c_char_p, c_int, ctypes.POINTER(c_int64)]),
     "unet_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "unet_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "unet_bucket_wait": (c_int, [c_void_p, c_int, c_void_p]),
@@ -54,6 +56,10 @@ SIGNATURES = {
     "unet_conv_wgrad": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p] + [c_int] * 12 + [c_void_p]),
     "unet_pack_weight": (c_int, [c_void_p, c_void_p] + [c_int] * 5 + [c_void_p]),
     "unet_unpack_grad": (c_int, [c_void_p, c_void_p] + [c_int] * 5 + [c_void_p]),
+    "unet_bn_forward": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_void_p]),
+    "unet_bn_backward": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
     "unet_maxpool_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p] + [c_int] * 4 + [c_void_p]),
     "unet_maxpool_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 4 + [c_void_p]),
 }

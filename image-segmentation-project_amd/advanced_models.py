@@ -80,6 +80,21 @@ class _Plan:
         self.flops_fwd = lib.unet_plan_flops(handle, 0)
         self.generation = 0
 
+    def tensor_views(self):
+        """name -> NCHW float32 copy of a bf16 NHWC workspace tensor (tests / debugging)."""
+        lib, h = self.lib, self.handle
+        info = (ctypes.c_int64 * 5)()
+        buf = ctypes.create_string_buffer(128)
+        out = {}
+        n = self.shape[0]
+        ws = self.workspace.view(torch.bfloat16)
+        for i in range(lib.unet_plan_num_tensors(h)):
+            _lib.check(lib.unet_plan_tensor_info(h, i, buf, 128, info), "tensor_info")
+            off, ld, c, hh, ww = (int(v) for v in info)
+            t = ws.as_strided((n, hh, ww, c), (hh * ww * ld, ww * ld, ld, 1), off // 2)
+            out[buf.value.decode()] = t.permute(0, 3, 1, 2).float()
+        return out
+
     def __del__(self):
         try:
             if self.handle:

@@ -256,22 +256,19 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(MaxPoolArgs a) {
     int bi[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; bi[k] = -1; }
-#pragma unroll
-    for (int kh = 0; kh < 3; ++kh) {
+    for (int t = 0; t < 9; ++t) {
+      const int kh = t / 3, kw = t - kh * 3;
       const int ih = 2 * p - 1 + kh;
-      if (ih < 0 || ih >= a.H) continue;
-#pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
-        const int iw = 2 * q - 1 + kw;
-        if (iw < 0 || iw >= a.W) continue;
+      const int iw = 2 * q - 1 + kw;
+      const bool ok = ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+      if (ok) {
         float v[8];
         unpack8(*reinterpret_cast<const uint4*>(a.x + ((int64_t)(n * a.H + ih) * a.W + iw) * a.ldx + c8), v);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          if (bi[k] < 0 || v[k] > best[k] || (v[k] != v[k] && best[k] == best[k])) {
-            best[k] = v[k];
-            bi[k] = kh * 3 + kw;
-          }
+          const bool take = bi[k] < 0 || v[k] > best[k] || (v[k] != v[k] && best[k] == best[k]);
+          best[k] = take ? v[k] : best[k];
+          bi[k] = take ? t : bi[k];
         }
       }
     }

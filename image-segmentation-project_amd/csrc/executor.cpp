@@ -97,6 +97,7 @@ struct unet_plan {
   hipEvent_t events[8] = {};
   int nevents = 0;
   double flops_fwd = 0, flops_train = 0;
+  std::vector<std::pair<std::string, Act>> named;  // debug / test introspection
 };
 
 namespace {
@@ -372,6 +373,33 @@ static int build_plan(unet_plan* p) {
   p->d_x1 = act(A, N, H2, W2, c0);
   p->d_y0 = act(A, N, H2, W2, c0);
   p->ws_bytes = A.top;
+
+  // named views for tests: forward activations and their gradients
+  auto& nm = p->named;
+  nm.push_back({"y0", p->y0}); nm.push_back({"x1", p->x1}); nm.push_back({"p0", p->p0});
+  nm.push_back({"d.x1", p->d_x1}); nm.push_back({"d.y0", p->d_y0}); nm.push_back({"d.p0", p->d_p0});
+  {
+    int bi = 0;
+    for (int s = 0; s < 4; ++s)
+      for (int k = 0; k < nblk[s]; ++k, ++bi) {
+        const Block& b = p->blocks[bi];
+        const std::string pre = "enc" + std::to_string(s + 1) + "." + std::to_string(k) + ".";
+        nm.push_back({pre + "y1", b.y1}); nm.push_back({pre + "h", b.h}); nm.push_back({pre + "y2", b.y2});
+        if (b.ds >= 0) { nm.push_back({pre + "yds", b.yds}); nm.push_back({pre + "d.yds", b.dyds}); }
+        nm.push_back({pre + "out", b.out});
+        nm.push_back({pre + "d.out", b.d_out}); nm.push_back({pre + "d.y2", b.dy2});
+        nm.push_back({pre + "d.h", b.dh}); nm.push_back({pre + "d.y1", b.dy1});
+      }
+  }
+  for (int l = 0; l < 4; ++l) {
+    const Dec& d = p->decs[l];
+    const std::string pre = "dec" + std::to_string(4 - l) + ".";
+    nm.push_back({pre + "up", d.up_out}); nm.push_back({pre + "cat", d.cat});
+    nm.push_back({pre + "y1", d.y1}); nm.push_back({pre + "h", d.h}); nm.push_back({pre + "y2", d.y2});
+    nm.push_back({pre + "out", d.out});
+    nm.push_back({pre + "d.out", d.d_out}); nm.push_back({pre + "d.y2", d.dy2}); nm.push_back({pre + "d.h", d.dh});
+    nm.push_back({pre + "d.y1", d.dy1}); nm.push_back({pre + "d.cat", d.dcat});
+  }
 
   // unpack groups per bucket
   p->bucket_convs.assign(4, {});
@@ -819,6 +847,16 @@ double unet_plan_flops(const unet_plan* p, int training) {
   return p ? (training ? p->flops_train : p->flops_fwd) : -1.0;
 }
 
+int unet_plan_num_tensors(const unet_plan* p) { return p ? (int)p->named.size() : -1; }
+int unet_plan_tensor_info(const unet_plan* p, int i, char* name, int namelen, int64_t info[5]) {
+  if (!p || i < 0 || i >= (int)p->named.size() || !name || namelen <= 0) { set_err("bad tensor index"); return 1; }
+  const auto& t = p->named[i];
+  std::snprintf(name, (size_t)namelen, "%s", t.first.c_str());
+  info[0] = (int64_t)t.second.off; info[1] = t.second.ld; info[2] = t.second.C;
+  info[3] = t.second.H; info[4] = t.second.W;
+  return 0;
+}
+
 int unet_forward(unet_plan* p, const float* image, const float* const* params, float* const* buffers,
                  void* workspace, float* logits, int training, hipStream_t stream) {
   API_GUARD({
@@ -898,6 +936,34 @@ int unet_unpack_grad(const float* acc, float* dst, int kind, int Co, int Ci, int
   t.n = 1;
   t.e[0] = UnpackEntry{acc, dst, kind, Co, Ci, R, S};
   CK(launch_unpack(t, stream));
+  return 0;
+}
+
+int unet_bn_forward(const void* y, int ldy, void* out, int ldo, const void* res, int ldr, int res_mode,
+                    const double* stats, const float* gamma, const float* beta, float* run_mean, float* run_var,
+                    float* save, int64_t npix, int C, int relu, int training, hipStream_t stream) {
+  if (res_mode < 0 || res_mode > 1) { set_err("res_mode must be 0 or 1"); return 1; }
+  BnApplyArgs a = {};
+  a.y = (const bf16_t*)y; a.ldy = ldy; a.out = (bf16_t*)out; a.ldo = ldo;
+  a.res = (const bf16_t*)res; a.ldr = ldr; a.res_mode = res_mode; a.relu = relu;
+  a.bn.stats = stats; a.bn.gamma = gamma; a.bn.beta = beta; a.bn.run_mean = run_mean; a.bn.run_var = run_var;
+  a.bn.save_mean = save; a.bn.save_invstd = save + C; a.bn.count = (double)npix; a.bn.C = C;
+  a.bn.eps = 1e-5f; a.bn.momentum = 0.1f; a.bn.training = training;
+  a.npix = npix; a.C = C;
+  CK(launch_bn_apply(a, stream));
+  return 0;
+}
+
+int unet_bn_backward(const void* dout, int ldd, const void* out, int ldo, const void* y, int ldy, const float* save,
+                     const float* gamma, double* sums, void* dy, int lddy, void* dres, float* dgamma, float* dbeta,
+                     int64_t npix, int C, hipStream_t stream) {
+  BnBwdArgs a = {};
+  a.da = (const bf16_t*)dout; a.ldda = ldd; a.act = (const bf16_t*)out; a.ldact = ldo;
+  a.y = (const bf16_t*)y; a.ldy = ldy; a.mean = save; a.invstd = save + C; a.gamma = gamma;
+  a.sums = sums; a.dy = (bf16_t*)dy; a.lddy = lddy; a.dres = (bf16_t*)dres; a.lddres = C;
+  a.dgamma = dgamma; a.dbeta = dbeta; a.npix = npix; a.C = C; a.relu = 1;
+  CK(launch_bn_bwd_reduce(a, stream));
+  CK(launch_bn_bwd_apply(a, stream));
   return 0;
 }
 

@@ -58,6 +58,9 @@ int unet_plan_num_bn(const unet_plan* p);
 int unet_plan_num_buckets(const unet_plan* p);
 int unet_plan_bucket_range(const unet_plan* p, int b, int64_t* begin, int64_t* end);
 double unet_plan_flops(const unet_plan* p, int training); /* algorithmic FLOPs per step */
+/* named workspace views (tests): info = {byte offset, ld, C, H, W} of a bf16 NHWC tensor */
+int unet_plan_num_tensors(const unet_plan* p);
+int unet_plan_tensor_info(const unet_plan* p, int i, char* name, int namelen, int64_t info[5]);
 
 /* params[i]: fp32 tensors in unet_plan_param_name order (== reference
  * state_dict parameter order); buffers[3*k+0/1]: running_mean/var of BN k in
@@ -97,6 +100,18 @@ int unet_pack_weight(const float* src, void* dst, int kind, int Co, int Ci, int 
 /* kind: 0 conv [Co][R][S][Ci] -> [Co][Ci][R][S], 1 convT, 2 stem */
 int unet_unpack_grad(const float* acc, float* dst, int kind, int Co, int Ci, int R, int S,
                      hipStream_t stream);
+/* BatchNorm2d (+identity residual)(+ReLU) forward from fp64 sums stats[2C]
+ * (sum, sumsq over npix pixels; training) or running stats (eval); save[2C] =
+ * batch mean | invstd.  res_mode: 0 none, 1 out = act(bn(y) + res). */
+int unet_bn_forward(const void* y, int ldy, void* out, int ldo, const void* res, int ldr, int res_mode,
+                    const double* stats, const float* gamma, const float* beta, float* run_mean,
+                    float* run_var, float* save, int64_t npix, int C, int relu, int training,
+                    hipStream_t stream);
+/* backward of out = relu(bn(y)[+res]): dY, optional dres (= dZ), dgamma/dbeta;
+ * sums[2C] must be zero on entry. */
+int unet_bn_backward(const void* dout, int ldd, const void* out, int ldo, const void* y, int ldy,
+                     const float* save, const float* gamma, double* sums, void* dy, int lddy, void* dres,
+                     float* dgamma, float* dbeta, int64_t npix, int C, hipStream_t stream);
 int unet_maxpool_fwd(const void* x, int ldx, void* y, uint8_t* idx, int N, int H, int W, int C,
                      hipStream_t stream);
 int unet_maxpool_bwd(const void* dy, const uint8_t* idx, const void* addend, int ldadd, void* dx,
