@@ -58,6 +58,9 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", dest="graph", action="store_true", default=None,
+                    help="replay the step as one HIP graph (default for --gpus 1)")
+    ap.add_argument("--no-graph", dest="graph", action="store_false")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -74,20 +77,23 @@ def main():
     model = pkg.UNetWithBackbone(n_classes=1, backbone="resnet34", pretrained=False, use_attention=False).to(dev)
     if world > 1:
         ddp.enable_data_parallel(model)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-5)
+    use_graph = args.graph if args.graph is not None else world == 1
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-5, capturable=use_graph)
     crit = pkg.get_loss_function({"loss_fn": "bce"})
     xs, ms = pkg.synthetic_cells(args.batch, args.size, args.size, seed=1234 + rank)
     x = torch.from_numpy(xs).to(dev)
     y = torch.from_numpy(ms).to(dev)
     model.train()
 
-    def step():
+    def eager_step():
         out = model(x)
         loss = crit(out, y)
         opt.zero_grad()
         loss.backward()
         opt.step()
         return out, loss
+
+    step = pkg.GraphedTrainStep(model, crit, opt, x, y) if use_graph else eager_step
 
     for _ in range(args.warmup):
         step()
@@ -112,7 +118,20 @@ def main():
     imgs = args.batch * args.steps * world
     flops_step = model.step_flops((args.batch, 1, args.size, args.size), training=True)
     ms_step = dt / args.steps * 1e3
-    achieved_tflops = flops_step / (dt / args.steps) / 1e12
+    step_tflops = flops_step / (dt / args.steps) / 1e12
+    # dominant kernel family (implicit-GEMM conv fwd/dgrad/wgrad): per-launch HIP
+    # events around every launch of one eager step right after the timed region
+    plan = next(iter(model._plans.values()))
+    torch.cuda.synchronize()
+    plan.profile(True)
+    eager_step()
+    torch.cuda.synchronize()
+    recs = plan.profile_report()
+    plan.profile(False)
+    conv = [r for r in recs if r[2] > 0]
+    conv_ms = sum(r[1] for r in conv)
+    achieved_tflops = sum(r[2] for r in conv) / 1e9 / conv_ms if conv_ms > 0 else 0.0
+    kernel_ms_total = sum(r[1] for r in recs)
     line = {
         "metric": "images/sec + mIoU, 512x512 U-Net bf16 at 1/2/4/8 MI355X",
         "value": round(imgs / dt, 3),
@@ -132,7 +151,12 @@ def main():
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "achieved": round(achieved_tflops, 2), "peak": MFMA_BF16_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved_tflops / MFMA_BF16_PEAK_TFLOPS, 4),
-                     "traffic": None, "scope": "whole step (algorithmic 163.1 GFLOP/img / step time)"},
+                     "traffic": None,
+                     "kernel": "implicit-GEMM conv (fwd+dgrad+wgrad launches, algorithmic FLOPs / event time)",
+                     "conv_ms_per_step": round(conv_ms, 3), "kernel_ms_per_step": round(kernel_ms_total, 3),
+                     "step_tflops": round(step_tflops, 2),
+                     "step_frac": round(step_tflops / MFMA_BF16_PEAK_TFLOPS, 4)},
+        "graph": bool(use_graph),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.batch, args.size, args.cpu_steps, args.cpu_threads)

@@ -11,7 +11,8 @@ from .advanced_models import UNetWithBackbone  # noqa: F401
 from .losses import BCELoss, ComboLoss, DiceLoss, get_loss_function  # noqa: F401
 from .utils import (EarlyStopping, calculate_metrics, calculate_metrics_from_logits,  # noqa: F401
                     get_device)
-from .train import evaluate, quick_train, train_epoch, train_model, TensorLoader  # noqa: F401
+from .train import (evaluate, quick_train, train_epoch, train_model, TensorLoader,  # noqa: F401
+                    GraphedTrainStep)
 from .synthetic import random_batch, synthetic_cells  # noqa: F401
 from . import ddp  # noqa: F401
 from ._lib import LIB_PATH  # noqa: F401

@@ -46,6 +46,9 @@ SIGNATURES = {
     "unet_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "unet_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "unet_bucket_wait": (c_int, [c_void_p, c_int, c_void_p]),
+    "unet_plan_use_bucket_events": (c_int, [c_void_p, c_int]),
+    "unet_profile_enable": (c_int, [c_void_p, c_int]),
+    "unet_profile_report": (c_int, [c_void_p, ctypes.c_char_p, c_int64]),
     "unet_loss_forward": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_float, c_float, c_void_p, c_void_p,
                                   c_void_p]),
     "unet_loss_backward": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_float, c_float, c_void_p, c_void_p,

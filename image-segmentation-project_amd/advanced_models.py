@@ -80,6 +80,22 @@ class _Plan:
         self.flops_fwd = lib.unet_plan_flops(handle, 0)
         self.generation = 0
 
+    def profile(self, on: bool):
+        _lib.check(self.lib.unet_profile_enable(self.handle, 1 if on else 0), "unet_profile_enable")
+
+    def profile_report(self):
+        """[(name, ms, flops)] for every launch recorded since profile(True)."""
+        n = self.lib.unet_profile_report(self.handle, None, 0)
+        if n < 0:
+            _lib.check(1, "unet_profile_report")
+        buf = ctypes.create_string_buffer(n + 16)
+        self.lib.unet_profile_report(self.handle, buf, n + 16)
+        out = []
+        for line in buf.value.decode().splitlines():
+            name, ms, fl = line.split("\t")
+            out.append((name, float(ms), float(fl)))
+        return out
+
     def tensor_views(self):
         """name -> NCHW float32 copy of a bf16 NHWC workspace tensor (tests / debugging)."""
         lib, h = self.lib, self.handle

@@ -61,8 +61,14 @@ __device__ __forceinline__ void bn_scale_shift(const unet::BnLaunch& p, int c, f
                                                float& var_out) {
   float mean, var;
   if (p.training) {
-    const double m = p.stats[c] / p.count;
-    double v = p.stats[p.C + c] / p.count - m * m;
+    double s = 0.0, q = 0.0;
+#pragma unroll
+    for (int r = 0; r < unet::kStatRep; ++r) {
+      s += p.stats[(size_t)r * 2 * p.C + c];
+      q += p.stats[(size_t)r * 2 * p.C + p.C + c];
+    }
+    const double m = s / p.count;
+    double v = q / p.count - m * m;
     if (v < 0.0) v = 0.0;
     mean = (float)m;
     var = (float)v;

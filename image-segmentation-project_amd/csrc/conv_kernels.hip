@@ -20,6 +20,9 @@
 // [pixel][channel] LDS tiles and fed to the MFMA with ds_read_b64_tr_b16
 // (hardware transpose, cdna_hip_programming.md T10); split-K over pixels with
 // fp32 atomics into a [Cout][R*S*C] accumulator.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -44,6 +47,10 @@ struct TapIter {
   // MODE_FWD: all R*S taps.  MODE_TRANS: taps r = r0 + st*j valid for class py.
   int r0, s0, nr, ns, st;
 };
+
+template <int MODE, int BN, int WM, int WN, int FM, int FN>
+__device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x4 (&acc)[FN][FM], char* smem, int m0,
+                                              int n0, int Mtot, int py, int px_);
 
 template <int MODE, int ALOAD, int BM, int BN, int BK, int WM, int WN>
 __global__ void __launch_bounds__(256)
@@ -229,8 +236,17 @@ conv_fwd_kernel(ConvFwdArgs a) {
     if (kt + 1 < KT) store_tiles(buf ^ 1);
     __syncthreads();
   }
+  conv_epilogue<MODE, BN, WM, WN, FM, FN>(a, acc, smem, m0, n0, Mtot, py, px_);
+}
 
-  // ---- epilogue: bias, addend, bf16 store, BN partial sums ----
+// ---- epilogue: bias, addend, bf16 NHWC store, BN partial sums (fp64 atomics) ----
+template <int MODE, int BN, int WM, int WN, int FM, int FN>
+__device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x4 (&acc)[FN][FM], char* smem, int m0,
+                                              int n0, int Mtot, int py, int px_) {
+  constexpr int WTM = FM * 16, WTN = FN * 16;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int st = a.stride, Pc = a.Pc, Qc = a.Qc;
   float csum[FN][4], csq[FN][4];
 #pragma unroll
   for (int i = 0; i < FN; ++i)
@@ -307,11 +323,192 @@ conv_fwd_kernel(ConvFwdArgs a) {
         float s = 0.f, q = 0.f;
 #pragma unroll
         for (int w = 0; w < WM; ++w) { s += red[(w * BN + cl) * 2]; q += red[(w * BN + cl) * 2 + 1]; }
-        atomicAdd(a.stats + co, (double)s);
-        atomicAdd(a.stats + a.Cout + co, (double)q);
+        double* rep = a.stats + (size_t)(blockIdx.x % kStatRep) * 2 * a.Cout;
+        atomicAdd(rep + co, (double)s);
+        atomicAdd(rep + a.Cout + co, (double)q);
       }
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// LDS-DMA pipelined implicit GEMM (the production fwd / dgrad kernel).
+//
+// Both operand tiles are filled by buffer_load_dwordx4 ... lds (no VGPR
+// staging): lane l of a wave instruction writes 16 B at base + 16*l, i.e. one
+// instruction fills 1 KiB = 1024/(2*BK) consecutive tile rows.  The XOR
+// swizzle of frag_off is applied on the SOURCE side (lane -> logical chunk)
+// so the LDS image is exactly the one the fragment reads expect
+// (cdna_hip_programming.md §5.4 rule 21).  Conv padding / tile tails use a
+// buffer offset beyond num_records, which the hardware range check turns into
+// zeros in LDS.  NS stages are kept in flight with a counted vmcnt and raw
+// s_barrier (never __syncthreads inside the loop: its vmcnt(0) would drain
+// the pipeline).
+// ---------------------------------------------------------------------------
+constexpr unsigned kOOB = 0x80000000u;
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, char* lds_wave_base, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, 0,
+                                           0, 0);
+}
+
+template <int BK>
+__device__ __forceinline__ int swz_chunk(int row, int p) {  // physical slot p -> logical chunk (involution)
+  if constexpr (BK == 64) return p ^ ((row >> 1) & 7);
+  else return p ^ ((0x78 >> (((row >> 2) & 3) << 1)) & 3);
+}
+
+template <int MODE, int BM, int BN, int BK, int NS, int WM, int WN>
+__global__ void __launch_bounds__(256)
+conv_glds_kernel(ConvFwdArgs a) {
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  static_assert(WM * WN == 4 && FM >= 1 && FN >= 1, "tiling");
+  constexpr int CPR = BK / 8;          // 16-B chunks per row
+  constexpr int ROWB = BK * 2;
+  constexpr int RPI = 1024 / ROWB;     // rows per wave instruction
+  constexpr int A_INS = BM / RPI / 4;  // per wave per stage
+  constexpr int B_INS = (BN / RPI + 3) / 4;
+  static_assert(BM % (RPI * 4) == 0, "A rows per wave");
+  constexpr int LPS = A_INS + B_INS;   // vm ops per wave per stage
+  constexpr int A_BYTES = BM * ROWB;
+  constexpr int B_BYTES = ((BN + RPI * 4 - 1) / (RPI * 4)) * RPI * 4 * ROWB;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % WM, wn = wave / WM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int nblk = bid % a.nblocks, mblk = bid / a.nblocks;
+  const int cls = blockIdx.z, st = a.stride;
+  const int py = (MODE == MODE_TRANS) ? cls / st : 0;
+  const int px_ = (MODE == MODE_TRANS) ? cls % st : 0;
+  const int Pc = a.Pc, Qc = a.Qc;
+  const int Mtot = a.N * Pc * Qc;
+  const int m0 = mblk * BM, n0 = nblk * BN;
+  TapIter ti;
+  if constexpr (MODE == MODE_TRANS) {
+    ti.st = st;
+    ti.r0 = (py + a.pad) % st;
+    ti.s0 = (px_ + a.pad) % st;
+    ti.nr = (a.R - ti.r0 + st - 1) / st;
+    ti.ns = (a.S - ti.s0 + st - 1) / st;
+  } else {
+    ti.st = 1; ti.r0 = 0; ti.s0 = 0; ti.nr = a.R; ti.ns = a.S;
+  }
+  const int cchunks = a.C / BK;
+  const int KT = ti.nr * ti.ns * cchunks;
+  const int Ktot = a.R * a.S * a.C;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (unsigned)((size_t)a.Cout * Ktot * 2));
+
+  // lane geometry inside one wave instruction
+  const int lrow = lane / CPR, lslot = lane % CPR;
+  int an[A_INS], aa[A_INS], ab[A_INS], ach[A_INS];
+#pragma unroll
+  for (int j = 0; j < A_INS; ++j) {
+    const int row = (wave * A_INS + j) * RPI + lrow;
+    ach[j] = swz_chunk<BK>(row, lslot);
+    const int m = m0 + row;
+    if (m < Mtot) {
+      const int n = m / (Pc * Qc);
+      const int rem = m - n * (Pc * Qc);
+      an[j] = n;
+      aa[j] = rem / Qc;
+      ab[j] = rem - aa[j] * Qc;
+    } else {
+      an[j] = -1; aa[j] = 0; ab[j] = 0;
+    }
+  }
+  int bch[B_INS];
+  unsigned bbase[B_INS];
+#pragma unroll
+  for (int j = 0; j < B_INS; ++j) {
+    const int row = (wave * B_INS + j) * RPI + lrow;
+    bch[j] = swz_chunk<BK>(row, lslot);
+    bbase[j] = (row < BN && n0 + row < a.Cout) ? (unsigned)((n0 + row) * Ktot) * 2u : kOOB;
+  }
+
+  auto issue = [&](int kt, int buf) {
+    const int cc = kt % cchunks;
+    const int tap = kt / cchunks;
+    const int jr = tap / ti.ns, js = tap - jr * ti.ns;
+    const int r = ti.r0 + ti.st * jr, s = ti.s0 + ti.st * js;
+    const int c0 = cc * BK;
+    char* As = smem + buf * STAGE;
+    char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int j = 0; j < A_INS; ++j) {
+      int ih, iw;
+      if constexpr (MODE == MODE_FWD) {
+        ih = aa[j] * st - a.pad + r;
+        iw = ab[j] * st - a.pad + s;
+      } else {
+        ih = aa[j] + (py + a.pad - r) / st;
+        iw = ab[j] + (px_ + a.pad - s) / st;
+      }
+      unsigned off = kOOB;
+      if (an[j] >= 0 && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+        off = (unsigned)(((an[j] * a.H + ih) * a.W + iw) * a.ldx + c0 + ach[j] * 8) * 2u;
+      glds16(xr, As + (wave * A_INS + j) * 1024, off);
+    }
+    const int kb = (r * a.S + s) * a.C + c0;
+#pragma unroll
+    for (int j = 0; j < B_INS; ++j) {
+      const unsigned off = bbase[j] == kOOB ? kOOB : bbase[j] + (unsigned)(kb + bch[j] * 8) * 2u;
+      glds16(wr, Bs + (wave * B_INS + j) * 1024, off);
+    }
+  };
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < KT) issue(s, s);
+
+  for (int kt = 0; kt < KT; ++kt) {
+    const int ahead = KT - 1 - kt;  // stages issued after kt (capped at NS-2)
+    if (ahead >= NS - 2) wait_vmcnt<(NS - 2) * LPS>();
+    else if (NS > 3 && ahead == 1) wait_vmcnt<LPS>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (kt + NS - 1 < KT) issue(kt + NS - 1, (kt + NS - 1) % NS);
+    const char* As = smem + (kt % NS) * STAGE;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int ch = kk * 4 + (lane >> 4);
+      bf16x8 wf[FN], xf[FM];
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+        wf[i] = *reinterpret_cast<const bf16x8*>(Bs + frag_off<BK>(wn * WTN + i * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+        xf[j] = *reinterpret_cast<const bf16x8*>(As + frag_off<BK>(wm * WTM + j * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+  conv_epilogue<MODE, BN, WM, WN, FM, FN>(a, acc, smem, m0, n0, Mtot, py, px_);
 }
 
 // ---------------------------------------------------------------------------
@@ -515,6 +712,131 @@ conv_wgrad_kernel(ConvWgradArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// 3x3 stride-1 weight gradient with an LDS input halo (all 9 taps per block).
+//
+// Block = 64 output channels x 32 input channels x 9 taps (72 fp32 acc / lane)
+// and a split-K range of TH x TW pixel tiles.  Per tile one LDS-DMA stage
+// holds dY [TH*TW px][64 co] and the input halo [(TH+2)(TW+2) px][32 ci];
+// every tap reads the halo at a row offset, so the input is fetched once per
+// tile instead of 9 times.  Operands are pixel-major, fed to the MFMA through
+// ds_read_b64_tr_b16.
+// ---------------------------------------------------------------------------
+template <int TW, int NS>
+__global__ void __launch_bounds__(256)
+wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
+  constexpr int TH = 128 / TW;
+  constexpr int HW2 = TW + 2;
+  constexpr int HROWS = (TH + 2) * HW2;
+  constexpr int A_BYTES = 128 * 128;    // dY: 128 px x 64 co (128-B rows)
+  constexpr int B_BYTES = 16 * 1024;    // halo: up to 256 rows x 32 ci (64-B rows)
+  static_assert(HROWS <= 256, "halo rows");
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int LPS = 8;                // 4 dY + 4 halo glds per wave per stage
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  typedef TrTile<64, 64, 128> TA;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 1, wn = wave >> 1;  // wave tile 32 co x 16 ci
+  const int cob = blockIdx.x % a.co_blocks;
+  const int cib = blockIdx.x / a.co_blocks;
+  const int co0 = cob * 64, c0 = cib * 32;
+  const int t0 = blockIdx.z * tiles_per_split;
+  const int t1 = min(tiles_total, t0 + tiles_per_split);
+  const int KT = t1 - t0;
+  if (KT <= 0) return;
+  const int tq = a.Q / TW, tp = a.P / TH;
+  const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, (unsigned)((size_t)a.N * a.P * a.Q * a.lddy * 2));
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
+
+  // per-lane constant parts of the loads
+  const int arow = lane >> 3, aslot = lane & 7;  // dY: 8 rows of 128 B per instruction
+  const int hrow = lane >> 2, hslot = lane & 3;  // halo: 16 rows of 64 B per instruction
+
+  auto issue = [&](int kt, int buf) {
+    const int t = t0 + kt;
+    const int n = t / (tp * tq);
+    const int rem = t - n * (tp * tq);
+    const int oh0 = (rem / tq) * TH, ow0 = (rem % tq) * TW;
+    char* As = smem + buf * STAGE;
+    char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = (wave * 4 + j) * 8 + arow;  // pixel in tile
+      const int f = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+      const int lchunk = ((((aslot >> 1) ^ f)) << 1) | (aslot & 1);
+      const int oh = oh0 + row / TW, ow = ow0 + row % TW;
+      const unsigned off = (unsigned)((((n * a.P + oh) * a.Q + ow) * a.lddy) + co0 + lchunk * 8) * 2u;
+      glds16(dyr, As + (wave * 4 + j) * 1024, off);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = (wave * 4 + j) * 16 + hrow;  // halo row
+      const int lchunk = ((((hslot >> 1) ^ ((row >> 3) & 1))) << 1) | (hslot & 1);
+      const int ih = oh0 - 1 + row / HW2, iw = ow0 - 1 + row % HW2;
+      unsigned off = kOOB;
+      if (row < HROWS && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+        off = (unsigned)((((n * a.H + ih) * a.W + iw) * a.ldx) + c0 + lchunk * 8) * 2u;
+      glds16(xr, Bs + (wave * 4 + j) * 1024, off);
+    }
+  };
+
+  f32x4 acc[9][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < KT) issue(s, s);
+  const int g = lane >> 4, li = lane & 15, trq = li >> 2, trp = li & 3;
+  for (int kt = 0; kt < KT; ++kt) {
+    const int ahead = KT - 1 - kt;
+    if (ahead >= NS - 2) wait_vmcnt<(NS - 2) * LPS>();
+    else if (NS > 3 && ahead == 1) wait_vmcnt<LPS>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (kt + NS - 1 < KT) issue(kt + NS - 1, (kt + NS - 1) % NS);
+    const char* As = smem + (kt % NS) * STAGE;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int p_lo = kk * 32 + 8 * g + trq;  // this lane's pixel (first tr read)
+      bf16x8 af[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int col = wm * 32 + i * 16 + 4 * trp;
+        af[i] = tr_read8(As + TA::off(p_lo, col), As + TA::off(p_lo + 4, col));
+      }
+      const int ty = p_lo / TW, tx = p_lo % TW;  // p_lo and p_lo+4 share the tile row
+      const int col = wn * 16 + 4 * trp;
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const int hr = (ty + r) * HW2 + tx + s;
+          const bf16x8 bfr = tr_read8(Bs + tr_off<32>(hr, col), Bs + tr_off<32>(hr + 4, col));
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+            acc[r * 3 + s][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[r * 3 + s][i], 0, 0, 0);
+        }
+    }
+  }
+  wait_vmcnt<0>();
+  // epilogue: fp32 atomics into dw[co][tap][ci]
+  const int Krow = 9 * a.C;
+  const int c = c0 + wn * 16 + li;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = co0 + wm * 32 + i * 16 + 4 * g + e;
+        if (co < a.Cout) atomicAdd(a.dw + (size_t)co * Krow + t * a.C + c, acc[t][i][e]);
+      }
+}
+
+// ---------------------------------------------------------------------------
 // host-side launch selection
 // ---------------------------------------------------------------------------
 template <int MODE, int ALOAD, int BM, int BN, int BK, int WM, int WN>
@@ -532,7 +854,59 @@ static hipError_t launch_fwd_cfg(const ConvFwdArgs& a0, int classes, hipStream_t
   return hipGetLastError();
 }
 
+template <int MODE, int BM, int BN, int BK, int NS, int WM, int WN>
+static hipError_t launch_glds_cfg(const ConvFwdArgs& a0, int classes, hipStream_t st) {
+  ConvFwdArgs a = a0;
+  a.nblocks = (a.Cout + BN - 1) / BN;
+  const int M = a.N * a.Pc * a.Qc;
+  a.mblocks = (M + BM - 1) / BM;
+  constexpr int ROWB = BK * 2, RPI = 1024 / ROWB;
+  constexpr size_t B_ROWS = ((BN + RPI * 4 - 1) / (RPI * 4)) * RPI * 4;
+  size_t lds = (size_t)NS * (BM + B_ROWS) * ROWB;
+  const size_t red = (size_t)WM * BN * 2 * sizeof(float);
+  if (red > lds) lds = red;
+  dim3 grid(a.mblocks * a.nblocks, 1, classes);
+  hipLaunchKernelGGL((conv_glds_kernel<MODE, BM, BN, BK, NS, WM, WN>), grid, dim3(256), lds, st, a);
+  return hipGetLastError();
+}
+
+template <int MODE>
+static hipError_t launch_glds(const ConvFwdArgs& a, int classes, hipStream_t st) {
+  const bool bk64 = (a.C % 64) == 0;
+  const long long M = (long long)a.N * a.Pc * a.Qc * classes;
+  if (a.Cout <= 32) {
+    return bk64 ? launch_glds_cfg<MODE, 128, 32, 64, 3, 4, 1>(a, classes, st)
+                : launch_glds_cfg<MODE, 128, 32, 32, 3, 4, 1>(a, classes, st);
+  }
+  if (a.Cout <= 64 || (M / 128) * (a.Cout / 128) < 512) {
+    return bk64 ? launch_glds_cfg<MODE, 128, 64, 64, 3, 2, 2>(a, classes, st)
+                : launch_glds_cfg<MODE, 128, 64, 32, 3, 2, 2>(a, classes, st);
+  }
+  return bk64 ? launch_glds_cfg<MODE, 128, 128, 64, 3, 2, 2>(a, classes, st)
+              : launch_glds_cfg<MODE, 128, 128, 32, 3, 2, 2>(a, classes, st);
+}
+
+static bool g_use_glds = std::getenv("UNET_CONV_V1") == nullptr;  // A/B switch for measurements
+void set_conv_impl(int glds) { g_use_glds = glds != 0; }
+
 hipError_t launch_conv_fwd(const ConvFwdArgs& a0, int mode, hipStream_t st) {
+  if (g_use_glds && mode != MODE_STEM && a0.C % 32 == 0) {
+    ConvFwdArgs a = a0;
+    if ((size_t)a.N * a.H * a.W * a.ldx * 2 >= 0x80000000ull) return hipErrorInvalidValue;
+    if (mode == MODE_TRANS) {
+      if (a.P % a.stride || a.Q % a.stride) return hipErrorInvalidValue;
+      a.Pc = a.P / a.stride;
+      a.Qc = a.Q / a.stride;
+      return launch_glds<MODE_TRANS>(a, a.stride * a.stride, st);
+    }
+    a.Pc = a.P;
+    a.Qc = a.Q;
+    return launch_glds<MODE_FWD>(a, 1, st);
+  }
+  return launch_conv_fwd_v1(a0, mode, st);
+}
+
+hipError_t launch_conv_fwd_v1(const ConvFwdArgs& a0, int mode, hipStream_t st) {
   ConvFwdArgs a = a0;
   int classes = 1;
   if (mode == MODE_TRANS) {
@@ -590,8 +964,33 @@ static hipError_t launch_wgrad_cfg(const ConvWgradArgs& a0, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <int TW>
+static hipError_t launch_wgrad_halo(const ConvWgradArgs& a0, hipStream_t st) {
+  ConvWgradArgs a = a0;
+  constexpr int TH = 128 / TW;
+  a.co_blocks = (a.Cout + 63) / 64;
+  a.c_blocks = a.C / 32;
+  const int tiles = a.N * (a.P / TH) * (a.Q / TW);
+  const int blocks_xy = a.co_blocks * a.c_blocks;
+  int splits = (2048 + blocks_xy - 1) / blocks_xy;
+  // keep >= 8 tiles (1024 px) per block: ~1 KB of fp32 atomics per 1.2 MFLOP
+  splits = std::max(1, std::min(splits, tiles / 8));
+  const int per = (tiles + splits - 1) / splits;
+  splits = (tiles + per - 1) / per;
+  constexpr int NS = 3;
+  const size_t lds = (size_t)NS * (128 * 128 + 16 * 1024);
+  hipLaunchKernelGGL((wgrad3x3_halo_kernel<TW, NS>), dim3(blocks_xy, 1, splits), dim3(256), lds, st, a, tiles, per);
+  return hipGetLastError();
+}
+
 hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st) {
   if (stem) return launch_wgrad_cfg<XLOAD_STEM, 64, 64, 64, 2, 2>(a, st);
+  if (g_use_glds && a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.C % 32 == 0 && a.P == a.H &&
+      a.Q == a.W && (size_t)a.N * a.H * a.W * a.ldx * 2 < 0x80000000ull &&
+      (size_t)a.N * a.P * a.Q * a.lddy * 2 < 0x80000000ull) {
+    if (a.Q % 32 == 0 && a.P % 4 == 0) return launch_wgrad_halo<32>(a, st);
+    if (a.Q % 16 == 0 && a.P % 8 == 0) return launch_wgrad_halo<16>(a, st);
+  }
   if (a.C % 32 || a.Cout % 32) return hipErrorInvalidValue;
   const bool co64 = a.Cout % 64 == 0, c64 = a.C % 64 == 0;
   if (a.Cout >= 128 && a.C >= 128)

@@ -40,34 +40,43 @@ __device__ void bn_finalize_block0(const BnLaunch& p, int tid, int nthreads) {
   }
 }
 
+// Thread layout for all per-channel elementwise kernels: chunk = tid % CC
+// (8 channels = one 16-B access), row = tid / CC; a thread keeps its chunk for
+// the whole grid-stride pixel loop, so per-channel coefficients live in
+// registers (no LDS, no bank conflicts) and loads are unrolled 2 pixels deep.
 __global__ void __launch_bounds__(256) bn_apply_kernel(BnApplyArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* sc1 = sm;
-  float* sh1 = sm + a.C;
-  float* sc2 = sm + 2 * a.C;
-  float* sh2 = sm + 3 * a.C;
+  const int CC = a.C >> 3;
+  const int rows = blockDim.x / CC;
+  const int chunk = threadIdx.x % CC, row = threadIdx.x / CC;
+  const int c8 = chunk << 3;
+  // per-channel affine coefficients: computed once per channel into LDS, then
+  // each thread keeps its 8 in registers
+  extern __shared__ __attribute__((aligned(16))) float coef[];  // [4][C]
   for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
     float m, inv, var;
-    bn_scale_shift(a.bn, c, sc1[c], sh1[c], m, inv, var);
-    if (a.res_mode == 2) bn_scale_shift(a.bn2, c, sc2[c], sh2[c], m, inv, var);
+    bn_scale_shift(a.bn, c, coef[c], coef[a.C + c], m, inv, var);
+    if (a.res_mode == 2) bn_scale_shift(a.bn2, c, coef[2 * a.C + c], coef[3 * a.C + c], m, inv, var);
   }
   __syncthreads();
-  const int CC = a.C >> 3;
-  const int64_t total = a.npix * CC;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t pix = e / CC;
-    const int c8 = (int)(e - pix * CC) << 3;
+  float sc1[8], sh1[8], sc2[8], sh2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sc1[k] = coef[c8 + k];
+    sh1[k] = coef[a.C + c8 + k];
+    sc2[k] = a.res_mode == 2 ? coef[2 * a.C + c8 + k] : 0.f;
+    sh2[k] = a.res_mode == 2 ? coef[3 * a.C + c8 + k] : 0.f;
+  }
+  auto one = [&](int64_t pix) {
     float v[8];
     unpack8(*reinterpret_cast<const uint4*>(a.y + pix * a.ldy + c8), v);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = v[k] * sc1[c8 + k] + sh1[c8 + k];
+    for (int k = 0; k < 8; ++k) v[k] = v[k] * sc1[k] + sh1[k];
     if (a.res_mode) {
       float r[8];
       unpack8(*reinterpret_cast<const uint4*>(a.res + pix * a.ldr + c8), r);
       if (a.res_mode == 2) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) r[k] = r[k] * sc2[c8 + k] + sh2[c8 + k];
+        for (int k = 0; k < 8; ++k) r[k] = r[k] * sc2[k] + sh2[k];
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] += r[k];
@@ -77,6 +86,15 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(BnApplyArgs a) {
       for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
     }
     *reinterpret_cast<uint4*>(a.out + pix * a.ldo + c8) = pack8(v);
+  };
+  if (row < rows) {
+    const int64_t stride = (int64_t)gridDim.x * rows;
+    int64_t pix = (int64_t)blockIdx.x * rows + row;
+    for (; pix + stride < a.npix; pix += 2 * stride) {
+      one(pix);
+      one(pix + stride);
+    }
+    if (pix < a.npix) one(pix);
   }
   if (blockIdx.x == 0) {
     __syncthreads();
@@ -85,11 +103,16 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(BnApplyArgs a) {
   }
 }
 
+static inline dim3 chunk_block(int C) {
+  const int CC = C / 8;
+  return dim3((256 / CC) * CC);
+}
+
 hipError_t launch_bn_apply(const BnApplyArgs& a, hipStream_t st) {
-  if (a.C % 8) return hipErrorInvalidValue;
-  const int64_t total = a.npix * (a.C / 8);
-  const int g = grid_for(total, 256 * 4);
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(g), dim3(256), 4 * a.C * sizeof(float), st, a);
+  if (a.C % 8 || a.C / 8 > 256) return hipErrorInvalidValue;
+  const int rows = 256 / (a.C / 8);
+  const int g = grid_for(a.npix, rows * 4, 4096);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(g), chunk_block(a.C), 4 * a.C * sizeof(float), st, a);
   return hipGetLastError();
 }
 
@@ -122,19 +145,26 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a) {
     mu[k] = a.mean[c8 + k]; is[k] = a.invstd[c8 + k];
     mu2[k] = two ? a.mean2[c8 + k] : 0.f; is2[k] = two ? a.invstd2[c8 + k] : 0.f;
   }
-  if (row < rows) {
-    for (int64_t pix = (int64_t)blockIdx.x * rows + row; pix < a.npix; pix += (int64_t)gridDim.x * rows) {
-      float dz[8], y[8];
-      load_dz(a, pix, c8, dz);
-      unpack8(*reinterpret_cast<const uint4*>(a.y + pix * a.ldy + c8), y);
+  auto one = [&](int64_t pix) {
+    float dz[8], y[8];
+    load_dz(a, pix, c8, dz);
+    unpack8(*reinterpret_cast<const uint4*>(a.y + pix * a.ldy + c8), y);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) { s1[k] += dz[k]; s2[k] += dz[k] * (y[k] - mu[k]) * is[k]; }
-      if (two) {
-        unpack8(*reinterpret_cast<const uint4*>(a.y2 + pix * a.ldy2 + c8), y);
+    for (int k = 0; k < 8; ++k) { s1[k] += dz[k]; s2[k] += dz[k] * (y[k] - mu[k]) * is[k]; }
+    if (two) {
+      unpack8(*reinterpret_cast<const uint4*>(a.y2 + pix * a.ldy2 + c8), y);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) t2[k] += dz[k] * (y[k] - mu2[k]) * is2[k];
-      }
+      for (int k = 0; k < 8; ++k) t2[k] += dz[k] * (y[k] - mu2[k]) * is2[k];
     }
+  };
+  if (row < rows) {
+    const int64_t stride = (int64_t)gridDim.x * rows;
+    int64_t pix = (int64_t)blockIdx.x * rows + row;
+    for (; pix + stride < a.npix; pix += 2 * stride) {
+      one(pix);
+      one(pix + stride);
+    }
+    if (pix < a.npix) one(pix);
   }
   // fold rows through LDS: red[row][C]
   extern __shared__ __attribute__((aligned(16))) float red[];
@@ -149,7 +179,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a) {
     for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
       float acc = 0.f;
       for (int r = 0; r < rows; ++r) acc += red[r * a.C + c];
-      double* dst = q == 0 ? a.sums : (q == 1 ? a.sums + a.C : a.sums2 + a.C);
+      const size_t rep = (size_t)(blockIdx.x % kStatRep) * 2 * a.C;
+      double* dst = q == 0 ? a.sums + rep : (q == 1 ? a.sums + rep + a.C : a.sums2 + rep + a.C);
       atomicAdd(dst + c, (double)acc);
     }
     __syncthreads();
@@ -160,80 +191,95 @@ hipError_t launch_bn_bwd_reduce(const BnBwdArgs& a, hipStream_t st) {
   if (a.C % 8 || a.C / 8 > 256) return hipErrorInvalidValue;
   const int CC = a.C / 8;
   const int rows = 256 / CC;
-  const int threads = rows * CC;
-  const int g = grid_for(a.npix, rows * 8, 1024);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(g), dim3(threads), (size_t)rows * a.C * sizeof(float), st, a);
+  // <= 512 blocks: every block adds into the same C addresses (fp64 atomics)
+  const int g = grid_for(a.npix, rows * 16, 512);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(g), chunk_block(a.C), (size_t)rows * a.C * sizeof(float), st, a);
   return hipGetLastError();
 }
 
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, double inv_n) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  // per channel: k1 = gamma*invstd, m1 = mean(dZ), m2 = mean(dZ*xhat), mu, invstd (x2 for bn2)
-  float* k1 = sm;
-  float* m1 = sm + a.C;
-  float* m2 = sm + 2 * a.C;
-  float* mu = sm + 3 * a.C;
-  float* is = sm + 4 * a.C;
-  float* k1b = sm + 5 * a.C;
-  float* m2b = sm + 6 * a.C;
-  float* mub = sm + 7 * a.C;
-  float* isb = sm + 8 * a.C;
+  const int CC = a.C >> 3;
+  const int rows = blockDim.x / CC;
+  const int chunk = threadIdx.x % CC, row = threadIdx.x / CC;
+  const int c8 = chunk << 3;
   const bool two = a.y2 != nullptr;
+  // per channel: k1 = gamma*invstd, m1 = mean(dZ), m2 = mean(dZ*xhat) (x2 for bn2),
+  // computed once per channel into LDS, then 8 per thread into registers
+  extern __shared__ __attribute__((aligned(16))) float coef[];  // [9][C]
   for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
-    k1[c] = a.gamma[c] * a.invstd[c];
-    m1[c] = (float)(a.sums[c] * inv_n);
-    m2[c] = (float)(a.sums[a.C + c] * inv_n);
-    mu[c] = a.mean[c];
-    is[c] = a.invstd[c];
+    double s1 = 0.0, s2 = 0.0, t2 = 0.0;
+    for (int r = 0; r < kStatRep; ++r) {
+      const size_t rep = (size_t)r * 2 * a.C;
+      s1 += a.sums[rep + c];
+      s2 += a.sums[rep + a.C + c];
+      if (two) t2 += a.sums2[rep + a.C + c];
+    }
+    coef[c] = a.gamma[c] * a.invstd[c];
+    coef[a.C + c] = (float)(s1 * inv_n);
+    coef[2 * a.C + c] = (float)(s2 * inv_n);
+    coef[3 * a.C + c] = a.mean[c];
+    coef[4 * a.C + c] = a.invstd[c];
     if (two) {
-      k1b[c] = a.gamma2[c] * a.invstd2[c];
-      m2b[c] = (float)(a.sums2[a.C + c] * inv_n);
-      mub[c] = a.mean2[c];
-      isb[c] = a.invstd2[c];
+      coef[5 * a.C + c] = a.gamma2[c] * a.invstd2[c];
+      coef[6 * a.C + c] = (float)(t2 * inv_n);
+      coef[7 * a.C + c] = a.mean2[c];
+      coef[8 * a.C + c] = a.invstd2[c];
     }
     if (blockIdx.x == 0) {
-      a.dgamma[c] = (float)a.sums[a.C + c];
-      a.dbeta[c] = (float)a.sums[c];
+      a.dgamma[c] = (float)s2;
+      a.dbeta[c] = (float)s1;
       if (two) {
-        a.dgamma2[c] = (float)a.sums2[a.C + c];
-        a.dbeta2[c] = (float)a.sums[c];  // same dZ feeds both BNs
+        a.dgamma2[c] = (float)t2;
+        a.dbeta2[c] = (float)s1;  // same dZ feeds both BNs
       }
     }
   }
   __syncthreads();
-  const int CC = a.C >> 3;
-  const int64_t total = a.npix * CC;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t pix = e / CC;
-    const int c8 = (int)(e - pix * CC) << 3;
+  float k1[8], m1[8], m2[8], mu[8], is[8], k1b[8], m2b[8], mub[8], isb[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = c8 + k;
+    k1[k] = coef[c];
+    m1[k] = coef[a.C + c];
+    m2[k] = coef[2 * a.C + c];
+    mu[k] = coef[3 * a.C + c];
+    is[k] = coef[4 * a.C + c];
+    k1b[k] = two ? coef[5 * a.C + c] : 0.f;
+    m2b[k] = two ? coef[6 * a.C + c] : 0.f;
+    mub[k] = two ? coef[7 * a.C + c] : 0.f;
+    isb[k] = two ? coef[8 * a.C + c] : 0.f;
+  }
+  auto one = [&](int64_t pix) {
     float dz[8], y[8], o[8];
     load_dz(a, pix, c8, dz);
     unpack8(*reinterpret_cast<const uint4*>(a.y + pix * a.ldy + c8), y);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int c = c8 + k;
-      o[k] = k1[c] * (dz[k] - m1[c] - (y[k] - mu[c]) * is[c] * m2[c]);
-    }
+    for (int k = 0; k < 8; ++k) o[k] = k1[k] * (dz[k] - m1[k] - (y[k] - mu[k]) * is[k] * m2[k]);
     *reinterpret_cast<uint4*>(a.dy + pix * a.lddy + c8) = pack8(o);
     if (two) {
       unpack8(*reinterpret_cast<const uint4*>(a.y2 + pix * a.ldy2 + c8), y);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int c = c8 + k;
-        o[k] = k1b[c] * (dz[k] - m1[c] - (y[k] - mub[c]) * isb[c] * m2b[c]);
-      }
+      for (int k = 0; k < 8; ++k) o[k] = k1b[k] * (dz[k] - m1[k] - (y[k] - mub[k]) * isb[k] * m2b[k]);
       *reinterpret_cast<uint4*>(a.dy2 + pix * a.lddy2 + c8) = pack8(o);
     }
     if (a.dres) *reinterpret_cast<uint4*>(a.dres + pix * a.lddres + c8) = pack8(dz);
+  };
+  if (row < rows) {
+    const int64_t stride = (int64_t)gridDim.x * rows;
+    int64_t pix = (int64_t)blockIdx.x * rows + row;
+    for (; pix + stride < a.npix; pix += 2 * stride) {
+      one(pix);
+      one(pix + stride);
+    }
+    if (pix < a.npix) one(pix);
   }
 }
 
 hipError_t launch_bn_bwd_apply(const BnBwdArgs& a, hipStream_t st) {
-  if (a.C % 8) return hipErrorInvalidValue;
-  const int64_t total = a.npix * (a.C / 8);
-  const int g = grid_for(total, 256 * 4);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(g), dim3(256), 9 * a.C * sizeof(float), st, a,
+  if (a.C % 8 || a.C / 8 > 256) return hipErrorInvalidValue;
+  const int rows = 256 / (a.C / 8);
+  const int g = grid_for(a.npix, rows * 4, 4096);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(g), chunk_block(a.C), 9 * a.C * sizeof(float), st, a,
                      1.0 / (double)a.npix);
   return hipGetLastError();
 }
@@ -538,44 +584,44 @@ hipError_t launch_d2f(const double* src, float* dst, int n, hipStream_t st) {
 __global__ void __launch_bounds__(256) pack_kernel(PackTable t) {
   const PackEntry e = t.e[blockIdx.y];
   const int Co = e.Co, Ci = e.Ci, R = e.R, S = e.S;
-  int64_t total;
-  if (e.kind == PK_STEM) total = (int64_t)Co * 64;
-  else total = (int64_t)Co * Ci * R * S;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
+  int total;
+  if (e.kind == PK_STEM) total = (int)Co * 64;
+  else total = (int)Co * Ci * R * S;
+  for (int i = (int)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int)gridDim.x * blockDim.x) {
     float v = 0.f;
     switch (e.kind) {
       case PK_CONV_FWD: {  // dst[co][r][s][ci] <- W[co][ci][r][s]
-        const int ci = (int)(i % Ci); int64_t q = i / Ci;
+        const int ci = (int)(i % Ci); int q = i / Ci;
         const int s = (int)(q % S); q /= S;
         const int r = (int)(q % R); const int co = (int)(q / R);
-        v = e.src[(((int64_t)co * Ci + ci) * R + r) * S + s];
+        v = e.src[(((int)co * Ci + ci) * R + r) * S + s];
         break;
       }
       case PK_CONV_DGRAD: {  // dst[ci][r][s][co] <- W[co][ci][r][s]
-        const int co = (int)(i % Co); int64_t q = i / Co;
+        const int co = (int)(i % Co); int q = i / Co;
         const int s = (int)(q % S); q /= S;
         const int r = (int)(q % R); const int ci = (int)(q / R);
-        v = e.src[(((int64_t)co * Ci + ci) * R + r) * S + s];
+        v = e.src[(((int)co * Ci + ci) * R + r) * S + s];
         break;
       }
       case PK_CONVT_FWD: {  // dst[co][a][b][ci] <- W[ci][co][a][b]
-        const int ci = (int)(i % Ci); int64_t q = i / Ci;
+        const int ci = (int)(i % Ci); int q = i / Ci;
         const int b = (int)(q % S); q /= S;
         const int aa = (int)(q % R); const int co = (int)(q / R);
-        v = e.src[(((int64_t)ci * Co + co) * R + aa) * S + b];
+        v = e.src[(((int)ci * Co + co) * R + aa) * S + b];
         break;
       }
       case PK_CONVT_DGRAD: {  // dst[ci][a][b][co] <- W[ci][co][a][b]
-        const int co = (int)(i % Co); int64_t q = i / Co;
+        const int co = (int)(i % Co); int q = i / Co;
         const int b = (int)(q % S); q /= S;
         const int aa = (int)(q % R); const int ci = (int)(q / R);
-        v = e.src[(((int64_t)ci * Co + co) * R + aa) * S + b];
+        v = e.src[(((int)ci * Co + co) * R + aa) * S + b];
         break;
       }
       default: {  // PK_STEM: dst[co][k], k < 49 -> W[co][0][k/7][k%7]
         const int k = (int)(i % 64), co = (int)(i / 64);
-        v = k < 49 ? e.src[(int64_t)co * 49 + k] : 0.f;
+        v = k < 49 ? e.src[(int)co * 49 + k] : 0.f;
       }
     }
     e.dst[i] = f2bf(v);
@@ -584,30 +630,30 @@ __global__ void __launch_bounds__(256) pack_kernel(PackTable t) {
 
 hipError_t launch_pack(const PackTable& t, hipStream_t st) {
   if (t.n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(pack_kernel, dim3(128, t.n), dim3(256), 0, st, t);
+  hipLaunchKernelGGL(pack_kernel, dim3(512, t.n), dim3(256), 0, st, t);
   return hipGetLastError();
 }
 
 __global__ void __launch_bounds__(256) unpack_kernel(UnpackTable t) {
   const UnpackEntry e = t.e[blockIdx.y];
   const int Co = e.Co, Ci = e.Ci, R = e.R, S = e.S;
-  const int64_t total = (int64_t)Co * Ci * R * S;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
+  const int total = (int)Co * Ci * R * S;
+  for (int i = (int)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int)gridDim.x * blockDim.x) {
     float v;
     if (e.kind == UP_CONV) {  // dst[co][ci][r][s] <- acc[co][r][s][ci]
-      const int s = (int)(i % S); int64_t q = i / S;
+      const int s = (int)(i % S); int q = i / S;
       const int r = (int)(q % R); q /= R;
       const int ci = (int)(q % Ci); const int co = (int)(q / Ci);
-      v = e.acc[(((int64_t)co * R + r) * S + s) * Ci + ci];
+      v = e.acc[(((int)co * R + r) * S + s) * Ci + ci];
     } else if (e.kind == UP_CONVT) {  // dst W[ci][co][a][b] <- acc[ci][a][b][co]  (Ci = in ch)
-      const int b = (int)(i % S); int64_t q = i / S;
+      const int b = (int)(i % S); int q = i / S;
       const int aa = (int)(q % R); q /= R;
       const int co = (int)(q % Co); const int ci = (int)(q / Co);
-      v = e.acc[(((int64_t)ci * R + aa) * S + b) * Co + co];
+      v = e.acc[(((int)ci * R + aa) * S + b) * Co + co];
     } else {  // UP_STEM: dst[co][0][r][s] <- acc[co][r*7+s] (row length 64)
       const int k = (int)(i % 49), co = (int)(i / 49);
-      v = e.acc[(int64_t)co * 64 + k];
+      v = e.acc[(int)co * 64 + k];
     }
     e.dst[i] = v;
   }
@@ -615,7 +661,7 @@ __global__ void __launch_bounds__(256) unpack_kernel(UnpackTable t) {
 
 hipError_t launch_unpack(const UnpackTable& t, hipStream_t st) {
   if (t.n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(unpack_kernel, dim3(64, t.n), dim3(256), 0, st, t);
+  hipLaunchKernelGGL(unpack_kernel, dim3(512, t.n), dim3(256), 0, st, t);
   return hipGetLastError();
 }
 

@@ -96,9 +96,42 @@ struct unet_plan {
   std::vector<std::vector<int>> bucket_convs;        // convs to unpack per bucket
   hipEvent_t events[8] = {};
   int nevents = 0;
+  bool want_events = false;  // DDP overlap: record one hipEvent per gradient bucket
   double flops_fwd = 0, flops_train = 0;
   std::vector<std::pair<std::string, Act>> named;  // debug / test introspection
+  // per-launch HIP-event profiler (unet_profile_*): one record per kernel
+  struct ProfRec { std::string name; double flops; int e0, e1; };
+  bool prof = false;
+  std::vector<hipEvent_t> evpool;
+  int evused = 0;
+  std::vector<ProfRec> recs;
 };
+
+namespace {
+int prof_event(unet_plan* p, hipStream_t st) {
+  if (p->evused == (int)p->evpool.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return -1;
+    p->evpool.push_back(e);
+  }
+  const int i = p->evused++;
+  if (hipEventRecord(p->evpool[i], st) != hipSuccess) return -1;
+  return i;
+}
+// RAII: brackets one launch with two events when profiling is on
+struct ProfScope {
+  unet_plan* p; hipStream_t st; std::string name; double flops; int e0 = -1;
+  ProfScope(unet_plan* p_, hipStream_t s, std::string n, double f) : p(p_), st(s), name(std::move(n)), flops(f) {
+    if (p->prof) e0 = prof_event(p, st);
+  }
+  ~ProfScope() {
+    if (p->prof && e0 >= 0) {
+      const int e1 = prof_event(p, st);
+      if (e1 >= 0) p->recs.push_back({name, flops, e0, e1});
+    }
+  }
+};
+}  // namespace
 
 namespace {
 
@@ -251,11 +284,11 @@ static int build_plan(unet_plan* p) {
   Alloc A;
   // zeroed at forward start: BN fwd sums
   p->zero_fwd_off = A.take(0);
-  for (auto& b : p->bns) b.stats = A.take((size_t)2 * b.C * sizeof(double));
+  for (auto& b : p->bns) b.stats = A.take((size_t)kStatRep * 2 * b.C * sizeof(double));
   p->zero_fwd_bytes = A.top - p->zero_fwd_off;
   // zeroed at backward start: BN bwd sums, convT bias sums, head sums, wgrad accumulators
   p->zero_bwd_off = A.take(0);
-  for (auto& b : p->bns) b.bsums = A.take((size_t)2 * b.C * sizeof(double));
+  for (auto& b : p->bns) b.bsums = A.take((size_t)kStatRep * 2 * b.C * sizeof(double));
   for (auto& cv : p->convs)
     if (cv.kind == L_CONVT) cv.bias_acc = A.take((size_t)cv.Co * sizeof(double));
   p->head_usum = A.take((size_t)(c0 / 2 * 4 + 1) * sizeof(double));
@@ -484,8 +517,16 @@ BnLaunch bn_launch(const Ctx& x, int bi, int64_t npix) {
   return l;
 }
 
+double conv_flops(const unet_plan* p, const Conv& cv, const Act& fwd_out) {
+  const double N = p->cfg.N;
+  if (cv.kind == L_CONVT) return 2.0 * N * (fwd_out.H / 2) * (fwd_out.W / 2) * cv.Ci * cv.Co * 4;
+  return 2.0 * N * fwd_out.H * fwd_out.W * cv.Co * cv.Ci * cv.R * cv.S;
+}
+const std::string& pname(const Ctx& x, int param) { return x.p->params[param].name; }
+
 int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for_stats) {
   const Conv& cv = x.p->convs[ci];
+  ProfScope ps(x.p, x.st, "fwd " + pname(x, cv.w), conv_flops(x.p, cv, out));
   ConvFwdArgs a = {};
   a.x = x.A(in); a.ldx = in.ld;
   a.w = x.W<bf16_t>(cv.pk_fwd);
@@ -502,6 +543,7 @@ int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for
 // conv dgrad: dx = dgrad(dy) (+ addend)
 int conv_dgrad(const Ctx& x, int ci, const Act& dy, const Act& dx, const Act* add) {
   const Conv& cv = x.p->convs[ci];
+  ProfScope ps(x.p, x.st, "dgrad " + pname(x, cv.w), conv_flops(x.p, cv, cv.kind == L_CONVT ? dy : dy));
   ConvFwdArgs a = {};
   a.x = x.A(dy); a.ldx = dy.ld;
   a.w = x.W<bf16_t>(cv.pk_dgrad);
@@ -523,6 +565,7 @@ int conv_dgrad(const Ctx& x, int ci, const Act& dy, const Act& dx, const Act* ad
 
 int conv_wgrad(const Ctx& x, int ci, const Act& dy, const Act& in) {
   const Conv& cv = x.p->convs[ci];
+  ProfScope ps(x.p, x.st, "wgrad " + pname(x, cv.w), conv_flops(x.p, cv, dy));
   ConvWgradArgs a = {};
   a.N = x.p->cfg.N;
   a.dw = x.W<float>(cv.wacc);
@@ -547,6 +590,7 @@ int bn_apply(const Ctx& x, int bi, const Act& y, const Act& out, int res_mode, c
              bool relu) {
   BnApplyArgs a = {};
   const int64_t npix = (int64_t)x.p->cfg.N * y.H * y.W;
+  ProfScope ps(x.p, x.st, "bn_fwd " + pname(x, x.p->bns[bi].gamma), 0);
   a.y = x.A(y); a.ldy = y.ld;
   a.out = x.A(out); a.ldo = out.ld;
   a.bn = bn_launch(x, bi, npix);
@@ -563,6 +607,7 @@ int bn_backward(const Ctx& x, int bi, const Act& dout, const Act& out, const Act
   BnBwdArgs a = {};
   const Bn& b = x.p->bns[bi];
   const int64_t npix = (int64_t)x.p->cfg.N * y.H * y.W;
+  ProfScope ps(x.p, x.st, "bn_bwd " + pname(x, b.gamma), 0);
   a.da = x.A(dout); a.ldda = dout.ld;
   a.act = x.A(out); a.ldact = out.ld;
   a.y = x.A(y); a.ldy = y.ld;
@@ -588,6 +633,7 @@ int bn_backward(const Ctx& x, int bi, const Act& dout, const Act& out, const Act
 }
 
 int unpack_bucket(const Ctx& x, int bk, float* grads) {
+  ProfScope ps(x.p, x.st, "unpack", 0);
   UnpackTable t;
   t.n = 0;
   for (int ci : x.p->bucket_convs[bk]) {
@@ -622,7 +668,12 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
   {
     PackTable t;
     t.n = 0;
-    auto flush = [&]() -> int { CK(launch_pack(t, st)); t.n = 0; return 0; };
+    auto flush = [&]() -> int {
+      ProfScope ps(p, st, "pack", 0);
+      CK(launch_pack(t, st));
+      t.n = 0;
+      return 0;
+    };
     for (auto& cv : p->convs) {
       if (cv.kind == L_STEM) {
         t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_fwd), PK_STEM, cv.Co, 1, 7, 7};
@@ -650,12 +701,18 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
     a.N = N; a.H = p->cfg.H; a.W = p->cfg.W; a.C = 1;
     a.P = p->y0.H; a.Q = p->y0.W; a.Cout = cv.Co;
     a.R = 7; a.S = 7; a.stride = 2; a.pad = 3;
-    CK(launch_conv_fwd(a, MODE_STEM, st));
+    {
+      ProfScope ps(p, st, "fwd input_conv.weight", 2.0 * N * p->y0.H * p->y0.W * cv.Co * 49);
+      CK(launch_conv_fwd(a, MODE_STEM, st));
+    }
     RUN(bn_apply(x, p->stem_bn, p->y0, p->x1, 0, nullptr, -1, true));
     MaxPoolArgs m = {};
     m.x = x.A(p->x1); m.ldx = p->x1.ld; m.y = x.A(p->p0); m.ldy = p->p0.ld; m.idx = x.W<uint8_t>(p->pidx);
     m.N = N; m.H = p->x1.H; m.W = p->x1.W; m.C = p->x1.C; m.P = p->p0.H; m.Q = p->p0.W;
-    CK(launch_maxpool_fwd(m, st));
+    {
+      ProfScope ps(p, st, "maxpool_fwd", 0);
+      CK(launch_maxpool_fwd(m, st));
+    }
   }
   for (auto& b : p->blocks) {
     RUN(conv_forward(x, b.conv1, b.in, b.y1, b.bn1));
@@ -682,6 +739,7 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
     h.w0 = prm[p->up0_w]; h.b0 = prm[p->up0_b]; h.wf = prm[p->fin_w]; h.bf = prm[p->fin_b];
     h.logits = logits;
     h.N = N; h.H = o.H; h.W = o.W; h.Cin = o.C; h.Co = (int)p->params[p->up0_b].numel;
+    ProfScope ps(p, st, "head_fwd", 0);
     CK(launch_head_fwd(h, st));
   }
   return 0;
@@ -691,7 +749,7 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
                         float* grads, hipStream_t st) {
   Ctx x{p, ws, prm, nullptr, st, 1};
   const int N = p->cfg.N;
-  RUN(ensure_events(p));
+  if (p->want_events) RUN(ensure_events(p));
   CK(hipMemsetAsync(ws + p->zero_bwd_off, 0, p->zero_bwd_bytes, st));
   // head (upconv0 + conv_final)
   {
@@ -705,6 +763,7 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     h.gw0 = grads + p->params[p->up0_w].flat; h.gb0 = grads + p->params[p->up0_b].flat;
     h.gwf = grads + p->params[p->fin_w].flat; h.gbf = grads + p->params[p->fin_b].flat;
     h.N = N; h.H = o.H; h.W = o.W; h.Cin = o.C; h.Co = (int)p->params[p->up0_b].numel;
+    ProfScope ps(p, st, "head_bwd", 0);
     CK(launch_head_bwd(h, st));
     CK(launch_head_grads(h, st));
   }
@@ -726,11 +785,12 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     Act du = slice(d.dcat, d.cat.C - up.Co, up.Co);
     RUN(conv_dgrad(x, d.up, du, d.d_up_in, nullptr));
     RUN(conv_wgrad(x, d.up, du, d.up_in));
+    ProfScope ps(p, st, "bias_sum", 0);
     CK(launch_channel_sum(x.A(du), du.ld, (int64_t)N * du.H * du.W, up.Co, x.W<double>(up.bias_acc), st));
     CK(launch_d2f(x.W<double>(up.bias_acc), grads + p->params[up.b].flat, up.Co, st));
   }
   RUN(unpack_bucket(x, 0, grads));
-  CK(hipEventRecord(p->events[0], st));
+  if (p->nevents) CK(hipEventRecord(p->events[0], st));
   // encoder blocks, deepest first
   const int nb = (int)p->blocks.size();
   for (int i = nb - 1; i >= 0; --i) {
@@ -752,8 +812,8 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     }
     RUN(conv_wgrad(x, b.conv1, b.dy1, b.in));
     // bucket boundaries: enc4 done at i == 13, enc3 at i == 7
-    if (i == 13) { RUN(unpack_bucket(x, 1, grads)); CK(hipEventRecord(p->events[1], st)); }
-    if (i == 7) { RUN(unpack_bucket(x, 2, grads)); CK(hipEventRecord(p->events[2], st)); }
+    if (i == 13) { RUN(unpack_bucket(x, 1, grads)); if (p->nevents) CK(hipEventRecord(p->events[1], st)); }
+    if (i == 7) { RUN(unpack_bucket(x, 2, grads)); if (p->nevents) CK(hipEventRecord(p->events[2], st)); }
   }
   // maxpool + stem
   {
@@ -763,7 +823,10 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     m.add = x.A(skip); m.ldadd = skip.ld;
     m.dx = x.A(p->d_x1); m.lddx = p->d_x1.ld;
     m.N = N; m.H = p->x1.H; m.W = p->x1.W; m.C = p->x1.C; m.P = p->p0.H; m.Q = p->p0.W;
-    CK(launch_maxpool_bwd(m, st));
+    {
+      ProfScope ps(p, st, "maxpool_bwd", 0);
+      CK(launch_maxpool_bwd(m, st));
+    }
     RUN(bn_backward(x, p->stem_bn, p->d_x1, p->x1, p->y0, p->d_y0, -1, nullptr, nullptr, nullptr, grads));
     const Conv& cv = p->convs[p->stem_conv];
     ConvWgradArgs a = {};
@@ -773,10 +836,11 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     a.P = p->y0.H; a.Q = p->y0.W; a.Cout = cv.Co;
     a.R = 7; a.S = 7; a.stride = 2; a.pad = 3;
     a.x = reinterpret_cast<const bf16_t*>(image);
+    ProfScope ps(p, st, "wgrad input_conv.weight", 2.0 * N * p->y0.H * p->y0.W * cv.Co * 49);
     CK(launch_conv_wgrad(a, 1, st));
   }
   RUN(unpack_bucket(x, 3, grads));
-  CK(hipEventRecord(p->events[3], st));
+  if (p->nevents) CK(hipEventRecord(p->events[3], st));
   return 0;
 }
 
@@ -871,6 +935,37 @@ int unet_backward(unet_plan* p, const float* image, const float* dlogits, const 
     if (!p || !image || !dlogits || !params || !workspace || !grads) { set_err("null argument"); return 1; }
     return run_backward(p, image, dlogits, params, reinterpret_cast<char*>(workspace), grads, stream);
   })
+}
+
+int unet_plan_use_bucket_events(unet_plan* p, int on) {
+  if (!p) { set_err("null plan"); return 1; }
+  p->want_events = on != 0;
+  return 0;
+}
+
+int unet_profile_enable(unet_plan* p, int on) {
+  if (!p) { set_err("null plan"); return 1; }
+  p->prof = on != 0;
+  p->recs.clear();
+  p->evused = 0;
+  return 0;
+}
+
+int unet_profile_report(unet_plan* p, char* buf, int64_t buflen) {
+  if (!p) { set_err("null plan"); return -1; }
+  std::string out;
+  if (!p->recs.empty()) {
+    if (hipEventSynchronize(p->evpool[p->recs.back().e1]) != hipSuccess) { set_err("event sync failed"); return -1; }
+  }
+  char line[256];
+  for (const auto& r : p->recs) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, p->evpool[r.e0], p->evpool[r.e1]) != hipSuccess) ms = -1.f;
+    std::snprintf(line, sizeof(line), "%s\t%.6f\t%.6e\n", r.name.c_str(), ms, r.flops);
+    out += line;
+  }
+  if (buf && buflen > 0) std::snprintf(buf, (size_t)buflen, "%s", out.c_str());
+  return (int)out.size() + 1;
 }
 
 int unet_bucket_wait(unet_plan* p, int bucket, hipStream_t waiter) {

@@ -8,6 +8,12 @@ namespace unet {
 typedef unsigned short bf16_t;
 
 enum { MODE_FWD = 0, MODE_TRANS = 1, MODE_STEM = 2 };
+
+// Per-channel fp64 reductions (BN sums) are spread over kStatRep replicas of
+// [2][C] (replica = blockIdx.x % kStatRep) so thousands of blocks do not all
+// hit the same addresses (MI355X_MICROARCH.md, float atomics "contention");
+// readers sum the replicas.  Layout everywhere: [kStatRep][2][C].
+constexpr int kStatRep = 16;
 enum { ALOAD_NHWC = 0, ALOAD_STEM = 1 };
 enum { XLOAD_NHWC = 0, XLOAD_STEM = 1 };
 
@@ -33,6 +39,8 @@ struct ConvWgradArgs {
 };
 
 hipError_t launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st);
+hipError_t launch_conv_fwd_v1(const ConvFwdArgs& a, int mode, hipStream_t st);  // register-staged
+void set_conv_impl(int glds);  // 1: LDS-DMA pipelined kernels (default), 0: register-staged v1
 hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st);
 
 // ---- elementwise / reduction kernels (elementwise.hip) ----

@@ -80,6 +80,10 @@ class _NativeDDP:
         if red is None:
             red = GradBucketReducer(plan.buckets, self.group)
             self._reducers = {id(plan): red}
+            # events are recorded from the NEXT backward on; order this one fully
+            _lib.check(plan.lib.unet_plan_use_bucket_events(plan.handle, 1), "use_bucket_events")
+            red.reduce(grads, None)
+            return
 
         def wait(b, stream):
             _lib.check(plan.lib.unet_bucket_wait(plan.handle, b, stream.cuda_stream), "unet_bucket_wait")

@@ -70,8 +70,14 @@ int unet_forward(unet_plan* p, const float* image, const float* const* params, f
 /* grads: flat fp32 [unet_plan_grad_numel], param i at unet_plan_param_offset(i). */
 int unet_backward(unet_plan* p, const float* image, const float* dlogits, const float* const* params,
                   void* workspace, float* grads, hipStream_t stream);
+/* record one hipEvent per gradient bucket in every unet_backward (DDP overlap) */
+int unet_plan_use_bucket_events(unet_plan* p, int on);
 /* make `waiter` wait until bucket b of the last unet_backward is final */
 int unet_bucket_wait(unet_plan* p, int bucket, hipStream_t waiter);
+/* per-launch hipEvent profiler: enable (clears records), then report lines
+ * "name\tms\tflops\n" for every launch since; returns bytes needed (incl. NUL). */
+int unet_profile_enable(unet_plan* p, int on);
+int unet_profile_report(unet_plan* p, char* buf, int64_t buflen);
 
 /* ---- loss + metrics (kind: 0 bce, 1 dice, 2 combo) ---- */
 int unet_loss_forward(const float* logits, const float* target, int64_t n, int kind, float alpha,
@@ -100,15 +106,17 @@ int unet_pack_weight(const float* src, void* dst, int kind, int Co, int Ci, int 
 /* kind: 0 conv [Co][R][S][Ci] -> [Co][Ci][R][S], 1 convT, 2 stem */
 int unet_unpack_grad(const float* acc, float* dst, int kind, int Co, int Ci, int R, int S,
                      hipStream_t stream);
-/* BatchNorm2d (+identity residual)(+ReLU) forward from fp64 sums stats[2C]
- * (sum, sumsq over npix pixels; training) or running stats (eval); save[2C] =
- * batch mean | invstd.  res_mode: 0 none, 1 out = act(bn(y) + res). */
+/* BatchNorm2d (+identity residual)(+ReLU) forward from fp64 sums
+ * stats[16][2][C] (16 atomic-spreading replicas of (sum, sumsq) over npix
+ * pixels, summed by the kernel; training) or running stats (eval); save[2C] =
+ * batch mean | invstd.  res_mode: 0 none, 1 out = act(bn(y) + res).
+ * unet_conv_fwd's `stats` output has the same [16][2][Cout] layout. */
 int unet_bn_forward(const void* y, int ldy, void* out, int ldo, const void* res, int ldr, int res_mode,
                     const double* stats, const float* gamma, const float* beta, float* run_mean,
                     float* run_var, float* save, int64_t npix, int C, int relu, int training,
                     hipStream_t stream);
 /* backward of out = relu(bn(y)[+res]): dY, optional dres (= dZ), dgamma/dbeta;
- * sums[2C] must be zero on entry. */
+ * sums[16][2][C] must be zero on entry. */
 int unet_bn_backward(const void* dout, int ldd, const void* out, int ldo, const void* y, int ldy,
                      const float* save, const float* gamma, double* sums, void* dy, int lddy, void* dres,
                      float* dgamma, float* dbeta, int64_t npix, int C, hipStream_t stream);

@@ -1,0 +1,60 @@
+"""Per-launch timing of one U-Net training step (HIP events inside the native
+executor).  usage: python scripts/layer_profile.py [--batch 16] [--size 512]"""
+import argparse
+import importlib
+import sys
+from collections import defaultdict
+
+import torch
+
+sys.path.insert(0, ".")
+pkg = importlib.import_module("image-segmentation-project_amd")
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--batch", type=int, default=16)
+ap.add_argument("--size", type=int, default=512)
+ap.add_argument("--top", type=int, default=40)
+args = ap.parse_args()
+
+torch.manual_seed(0)
+m = pkg.UNetWithBackbone(pretrained=False, use_attention=False).cuda().train()
+xs, ms = pkg.synthetic_cells(args.batch, args.size, args.size, seed=1234)
+x, y = torch.from_numpy(xs).cuda(), torch.from_numpy(ms).cuda()
+opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-5)
+crit = pkg.BCELoss()
+
+
+def step():
+    out = m(x)
+    loss = crit(out, y)
+    opt.zero_grad()
+    loss.backward()
+    opt.step()
+
+
+for _ in range(3):
+    step()
+torch.cuda.synchronize()
+plan = next(iter(m._plans.values()))
+plan.profile(True)
+step()
+torch.cuda.synchronize()
+recs = plan.profile_report()
+plan.profile(False)
+tot = sum(r[1] for r in recs)
+fl = sum(r[2] for r in recs)
+print(f"launches {len(recs)}  sum of kernel ms {tot:.3f}  conv TFLOP/s over conv launches "
+      f"{sum(r[2] for r in recs if r[2] > 0) / 1e9 / sum(r[1] for r in recs if r[2] > 0):.1f}")
+by_kind = defaultdict(lambda: [0.0, 0.0, 0])
+for name, ms_, f in recs:
+    k = name.split(" ")[0]
+    by_kind[k][0] += ms_
+    by_kind[k][1] += f
+    by_kind[k][2] += 1
+for k, (t, f, n) in sorted(by_kind.items(), key=lambda kv: -kv[1][0]):
+    tf = f / 1e9 / t if t > 0 and f > 0 else 0
+    print(f"{k:12s} n={n:3d} {t:8.3f} ms  {100 * t / tot:5.1f}%  {tf:7.1f} TFLOP/s")
+print("--- top launches")
+for name, ms_, f in sorted(recs, key=lambda r: -r[1])[: args.top]:
+    tf = f / 1e9 / ms_ if ms_ > 0 and f > 0 else 0
+    print(f"{name:40s} {ms_ * 1e3:9.1f} us  {tf:7.1f} TFLOP/s")

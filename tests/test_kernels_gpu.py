@@ -11,6 +11,7 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 PK_CONV_FWD, PK_CONV_DGRAD, PK_CONVT_FWD, PK_CONVT_DGRAD, PK_STEM = range(5)
+REP = 16  # kStatRep: BN sums are [16][2][C] replicas
 
 
 @pytest.fixture(scope="module")
@@ -85,11 +86,11 @@ def test_conv_fwd_bias_stats(L, case, cuda):
     P = ref.shape[2]
     wg = w.cuda()
     wp = pack(L, wg, PK_CONV_FWD, Co, C, R, R)
-    stats = torch.zeros(2 * Co, dtype=torch.float64, device="cuda")
+    stats = torch.zeros(REP * 2 * Co, dtype=torch.float64, device="cuda")
     y = conv_fwd(L, nhwc(x).cuda(), wp, N, H, H, C, P, P, Co, R, st, pad, 0, bias=b.cuda(), stats=stats)
     torch.cuda.synchronize()
     close(nchw(y), ref)
-    s = stats.cpu()
+    s = stats.cpu().view(REP, 2 * Co).sum(0)
     torch.testing.assert_close(s[:Co], ref.double().sum((0, 2, 3)), rtol=1e-3, atol=1e-2 * ref.abs().max().item() * 10)
     torch.testing.assert_close(s[Co:], ref.double().pow(2).sum((0, 2, 3)), rtol=1e-3, atol=1.0)
 
@@ -231,7 +232,8 @@ def test_bn_forward_backward(L, C, res, cuda):
     dout = bf(torch.randn(N, C, H, H, generator=g))
     ref.backward(dout.float())
     yg = nhwc(y).cuda()
-    stats = torch.cat([yg.double().sum((0, 1, 2)), yg.double().pow(2).sum((0, 1, 2))]).contiguous()
+    stats = torch.zeros(REP, 2 * C, dtype=torch.float64, device="cuda")
+    stats[3] = torch.cat([yg.double().sum((0, 1, 2)), yg.double().pow(2).sum((0, 1, 2))])
     out = torch.empty_like(yg)
     rgc = nhwc(r).cuda() if res else None
     gc, bc, rmc, rvc = gamma.cuda(), beta.cuda(), rm0.clone().cuda(), rv0.clone().cuda()
@@ -245,7 +247,7 @@ def test_bn_forward_backward(L, C, res, cuda):
     close(nchw(out), ref.detach())
     torch.testing.assert_close(rmc.cpu(), rm, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(rvc.cpu(), rv, rtol=1e-5, atol=1e-6)
-    sums = torch.zeros(2 * C, dtype=torch.float64, device="cuda")
+    sums = torch.zeros(REP * 2 * C, dtype=torch.float64, device="cuda")
     dy = torch.empty_like(yg)
     dres = torch.empty_like(yg)
     dgb = torch.zeros(2 * C, device="cuda")
