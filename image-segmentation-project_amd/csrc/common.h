@@ -53,6 +53,36 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
 
+// Last-arriver election across the blocks of one launch
+// (cdna_hip_programming.md §6 Guideline 16, counter form): every wave drains
+// its own atomics/stores, one lane releases at agent scope and takes a ticket;
+// the block that draws total-1 acquires and may read everybody's results.
+// `flag` must be a word of the DYNAMIC LDS region (no second __shared__ object
+// beside an LDS-DMA staging array: §5 trap 4(a)).
+// The published data are device-scope fp64 atomic adds, which execute at the
+// memory side ("8-B agent atomics both sides", MI355X_MICROARCH.md Valid
+// forms): the waves that issued them only drain their own vmcnt — no L2
+// write-back release fence per block.
+__device__ __forceinline__ bool last_block_arrive(unsigned* ticket, unsigned total, int* flag,
+                                                  bool issued_atomics) {
+  if (issued_atomics) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = prev == total - 1 ? 1 : 0;
+  }
+  __syncthreads();
+  const bool last = *flag != 0;
+  if (last) {
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+  }
+  return last;
+}
+
 // BatchNorm per-channel statistics are fp64 sums (sum, sumsq) so that
 // var = E[y^2]-mean^2 does not cancel: stats[0..C) = sum, stats[C..2C) = sumsq.
 // Per-channel affine form of BN: y_hat*gamma+beta == y*scale + shift.
@@ -82,4 +112,26 @@ __device__ __forceinline__ void bn_scale_shift(const unet::BnLaunch& p, int c, f
   mean_out = mean;
   invstd_out = inv;
   var_out = var;
+}
+
+// Training-mode finalisation of one BN layer (run by ONE block): scale/shift
+// for the consumers, batch mean/invstd for the backward, running stats with
+// momentum and the unbiased variance (torch.nn.BatchNorm2d semantics).
+__device__ __forceinline__ void bn_finalize(const unet::BnLaunch& p) {
+  for (int c = threadIdx.x; c < p.C; c += blockDim.x) {
+    float sc, sh, m, inv, var;
+    bn_scale_shift(p, c, sc, sh, m, inv, var);
+    if (p.ss) {
+      p.ss[c] = sc;
+      p.ss[p.C + c] = sh;
+    }
+    if (p.training) {
+      p.save_mean[c] = m;
+      p.save_invstd[c] = inv;
+      const double n = p.count;
+      const float unb = (float)((double)var * (n / (n > 1.0 ? n - 1.0 : 1.0)));
+      p.run_mean[c] = (1.f - p.momentum) * p.run_mean[c] + p.momentum * m;
+      p.run_var[c] = (1.f - p.momentum) * p.run_var[c] + p.momentum * unb;
+    }
+  }
 }

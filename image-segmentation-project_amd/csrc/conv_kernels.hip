@@ -328,6 +328,11 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x4 (&acc)
         atomicAdd(rep + a.Cout + co, (double)q);
       }
     }
+    if (a.bn.ticket) {
+      const unsigned total = gridDim.x * gridDim.y * gridDim.z;
+      int* flag = reinterpret_cast<int*>(smem + WM * BN * 2 * sizeof(float));
+      if (last_block_arrive(a.bn.ticket, total, flag, tid < BN)) bn_finalize(a.bn);
+    }
   }
 }
 
@@ -870,20 +875,60 @@ static hipError_t launch_glds_cfg(const ConvFwdArgs& a0, int classes, hipStream_
   return hipGetLastError();
 }
 
+static int env_int(const char* name) {
+  const char* v = std::getenv(name);
+  return v ? std::atoi(v) : 0;
+}
+static int g_cfg_override = env_int("UNET_CONV_CFG");  // tuning runs only
+void set_conv_config(int cfg) { g_cfg_override = cfg; }
+
+// Explicit tile configurations (tuning / override).  Returns hipErrorNotSupported
+// when the configuration does not apply to the shape.
+template <int MODE>
+static hipError_t launch_glds_fixed(const ConvFwdArgs& a, int classes, int cfg, hipStream_t st) {
+  const bool bk64 = (a.C % 64) == 0;
+  switch (cfg) {
+    case 1: return bk64 ? launch_glds_cfg<MODE, 128, 64, 64, 3, 2, 2>(a, classes, st) : hipErrorNotSupported;
+    case 2: return bk64 ? launch_glds_cfg<MODE, 128, 64, 64, 2, 2, 2>(a, classes, st) : hipErrorNotSupported;
+    case 3: return launch_glds_cfg<MODE, 128, 64, 32, 3, 2, 2>(a, classes, st);
+    case 4: return bk64 ? launch_glds_cfg<MODE, 128, 128, 64, 2, 2, 2>(a, classes, st) : hipErrorNotSupported;
+    case 5: return launch_glds_cfg<MODE, 128, 128, 32, 3, 2, 2>(a, classes, st);
+    case 6: return bk64 ? launch_glds_cfg<MODE, 128, 128, 64, 3, 2, 2>(a, classes, st) : hipErrorNotSupported;
+    case 7: return bk64 ? launch_glds_cfg<MODE, 64, 64, 64, 3, 2, 2>(a, classes, st) : hipErrorNotSupported;
+    case 8: return bk64 ? launch_glds_cfg<MODE, 256, 64, 64, 2, 4, 1>(a, classes, st) : hipErrorNotSupported;
+    case 9: return bk64 ? launch_glds_cfg<MODE, 128, 32, 64, 3, 4, 1>(a, classes, st) : hipErrorNotSupported;
+    case 10: return launch_glds_cfg<MODE, 256, 32, 32, 3, 4, 1>(a, classes, st);
+    case 11: return launch_glds_cfg<MODE, 128, 32, 32, 4, 4, 1>(a, classes, st);
+    case 12: return launch_glds_cfg<MODE, 256, 64, 32, 3, 4, 1>(a, classes, st);
+    case 13: return bk64 ? launch_glds_cfg<MODE, 128, 64, 64, 4, 2, 2>(a, classes, st) : hipErrorNotSupported;
+    case 14: return launch_glds_cfg<MODE, 128, 128, 32, 4, 2, 2>(a, classes, st);
+    default: return hipErrorNotSupported;
+  }
+}
+
 template <int MODE>
 static hipError_t launch_glds(const ConvFwdArgs& a, int classes, hipStream_t st) {
+  if (g_cfg_override > 0) {
+    const hipError_t e = launch_glds_fixed<MODE>(a, classes, g_cfg_override, st);
+    if (e != hipErrorNotSupported) return e;
+  }
+  // Selection measured by scripts/tune_conv.py on MI355X (Base config shapes,
+  // profiles/r01/tune_conv.txt): 2-stage 128x128 wherever it still yields
+  // ~one block per CU, 64x64 for the 16x16 encoder stage, 128x64 otherwise.
   const bool bk64 = (a.C % 64) == 0;
   const long long M = (long long)a.N * a.Pc * a.Qc * classes;
+  auto nblk = [&](long long bm, long long bn) { return ((M + bm - 1) / bm) * ((a.Cout + bn - 1) / bn); };
   if (a.Cout <= 32) {
     return bk64 ? launch_glds_cfg<MODE, 128, 32, 64, 3, 4, 1>(a, classes, st)
                 : launch_glds_cfg<MODE, 128, 32, 32, 3, 4, 1>(a, classes, st);
   }
-  if (a.Cout <= 64 || (M / 128) * (a.Cout / 128) < 512) {
-    return bk64 ? launch_glds_cfg<MODE, 128, 64, 64, 3, 2, 2>(a, classes, st)
-                : launch_glds_cfg<MODE, 128, 64, 32, 3, 2, 2>(a, classes, st);
+  if (a.Cout > 64 && nblk(128, 128) >= 240) {
+    return bk64 ? launch_glds_cfg<MODE, 128, 128, 64, 2, 2, 2>(a, classes, st)
+                : launch_glds_cfg<MODE, 128, 128, 32, 3, 2, 2>(a, classes, st);
   }
-  return bk64 ? launch_glds_cfg<MODE, 128, 128, 64, 3, 2, 2>(a, classes, st)
-              : launch_glds_cfg<MODE, 128, 128, 32, 3, 2, 2>(a, classes, st);
+  if (bk64 && nblk(128, 64) <= 256) return launch_glds_cfg<MODE, 64, 64, 64, 3, 2, 2>(a, classes, st);
+  return bk64 ? launch_glds_cfg<MODE, 128, 64, 64, 2, 2, 2>(a, classes, st)
+              : launch_glds_cfg<MODE, 128, 64, 32, 3, 2, 2>(a, classes, st);
 }
 
 static bool g_use_glds = std::getenv("UNET_CONV_V1") == nullptr;  // A/B switch for measurements

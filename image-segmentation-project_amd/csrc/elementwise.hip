@@ -54,8 +54,20 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(BnApplyArgs a) {
   extern __shared__ __attribute__((aligned(16))) float coef[];  // [4][C]
   for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
     float m, inv, var;
-    bn_scale_shift(a.bn, c, coef[c], coef[a.C + c], m, inv, var);
-    if (a.res_mode == 2) bn_scale_shift(a.bn2, c, coef[2 * a.C + c], coef[3 * a.C + c], m, inv, var);
+    if (a.bn.training && a.bn.ss) {  // finalised by the producing conv's last block
+      coef[c] = a.bn.ss[c];
+      coef[a.C + c] = a.bn.ss[a.C + c];
+    } else {
+      bn_scale_shift(a.bn, c, coef[c], coef[a.C + c], m, inv, var);
+    }
+    if (a.res_mode == 2) {
+      if (a.bn2.training && a.bn2.ss) {
+        coef[2 * a.C + c] = a.bn2.ss[c];
+        coef[3 * a.C + c] = a.bn2.ss[a.C + c];
+      } else {
+        bn_scale_shift(a.bn2, c, coef[2 * a.C + c], coef[3 * a.C + c], m, inv, var);
+      }
+    }
   }
   __syncthreads();
   float sc1[8], sh1[8], sc2[8], sh2[8];
@@ -96,10 +108,11 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(BnApplyArgs a) {
     }
     if (pix < a.npix) one(pix);
   }
+  // standalone use (no producer finalised the stats): block 0 finalises
   if (blockIdx.x == 0) {
     __syncthreads();
-    bn_finalize_block0(a.bn, threadIdx.x, blockDim.x);
-    if (a.res_mode == 2) bn_finalize_block0(a.bn2, threadIdx.x, blockDim.x);
+    if (!a.bn.ss) bn_finalize_block0(a.bn, threadIdx.x, blockDim.x);
+    if (a.res_mode == 2 && !a.bn2.ss) bn_finalize_block0(a.bn2, threadIdx.x, blockDim.x);
   }
 }
 
@@ -185,6 +198,30 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a) {
     }
     __syncthreads();
   }
+  if (a.ticket && last_block_arrive(a.ticket, gridDim.x, reinterpret_cast<int*>(red), true)) {
+    // coefficients of the apply pass + parameter gradients, once per channel
+    const double inv_n = 1.0 / (double)a.npix;
+    for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+      double s1 = 0.0, s2 = 0.0, t2 = 0.0;
+      for (int r = 0; r < kStatRep; ++r) {
+        const size_t rep = (size_t)r * 2 * a.C;
+        s1 += a.sums[rep + c];
+        s2 += a.sums[rep + a.C + c];
+        if (two) t2 += a.sums2[rep + a.C + c];
+      }
+      a.coef[c] = a.gamma[c] * a.invstd[c];
+      a.coef[a.C + c] = (float)(s1 * inv_n);
+      a.coef[2 * a.C + c] = (float)(s2 * inv_n);
+      a.dgamma[c] = (float)s2;
+      a.dbeta[c] = (float)s1;
+      if (two) {
+        a.coef[3 * a.C + c] = a.gamma2[c] * a.invstd2[c];
+        a.coef[4 * a.C + c] = (float)(t2 * inv_n);
+        a.dgamma2[c] = (float)t2;
+        a.dbeta2[c] = (float)s1;  // same dZ feeds both BNs
+      }
+    }
+  }
 }
 
 hipError_t launch_bn_bwd_reduce(const BnBwdArgs& a, hipStream_t st) {
@@ -207,6 +244,20 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, double i
   // computed once per channel into LDS, then 8 per thread into registers
   extern __shared__ __attribute__((aligned(16))) float coef[];  // [9][C]
   for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+    if (a.coef) {  // finalised by the reduce kernel's last block
+      coef[c] = a.coef[c];
+      coef[a.C + c] = a.coef[a.C + c];
+      coef[2 * a.C + c] = a.coef[2 * a.C + c];
+      coef[3 * a.C + c] = a.mean[c];
+      coef[4 * a.C + c] = a.invstd[c];
+      if (two) {
+        coef[5 * a.C + c] = a.coef[3 * a.C + c];
+        coef[6 * a.C + c] = a.coef[4 * a.C + c];
+        coef[7 * a.C + c] = a.mean2[c];
+        coef[8 * a.C + c] = a.invstd2[c];
+      }
+      continue;
+    }
     double s1 = 0.0, s2 = 0.0, t2 = 0.0;
     for (int r = 0; r < kStatRep; ++r) {
       const size_t rep = (size_t)r * 2 * a.C;

@@ -47,7 +47,9 @@ struct Bn {
   int gamma, beta;        // param indices
   int idx;                // BN ordinal (buffers 3*idx + 0/1)
   int C;
-  size_t stats, bsums, save;  // ws offsets: fp64 [2C] fwd, fp64 [2C] bwd, fp32 mean|invstd
+  size_t stats, bsums, save;  // ws offsets: fp64 [R][2C] fwd, fp64 [R][2C] bwd, fp32 mean|invstd
+  size_t ss, coef;            // fp32 scale|shift [2C], backward coefficients [5C]
+  size_t tfwd, tbwd;          // last-block tickets (zeroed with the fwd / bwd sums)
 };
 
 enum { L_CONV = 0, L_CONVT = 1, L_STEM = 2 };
@@ -284,11 +286,17 @@ static int build_plan(unet_plan* p) {
   Alloc A;
   // zeroed at forward start: BN fwd sums
   p->zero_fwd_off = A.take(0);
-  for (auto& b : p->bns) b.stats = A.take((size_t)kStatRep * 2 * b.C * sizeof(double));
+  for (auto& b : p->bns) {
+    b.stats = A.take((size_t)kStatRep * 2 * b.C * sizeof(double));
+    b.tfwd = A.take(sizeof(unsigned));
+  }
   p->zero_fwd_bytes = A.top - p->zero_fwd_off;
   // zeroed at backward start: BN bwd sums, convT bias sums, head sums, wgrad accumulators
   p->zero_bwd_off = A.take(0);
-  for (auto& b : p->bns) b.bsums = A.take((size_t)kStatRep * 2 * b.C * sizeof(double));
+  for (auto& b : p->bns) {
+    b.bsums = A.take((size_t)kStatRep * 2 * b.C * sizeof(double));
+    b.tbwd = A.take(sizeof(unsigned));
+  }
   for (auto& cv : p->convs)
     if (cv.kind == L_CONVT) cv.bias_acc = A.take((size_t)cv.Co * sizeof(double));
   p->head_usum = A.take((size_t)(c0 / 2 * 4 + 1) * sizeof(double));
@@ -299,7 +307,11 @@ static int build_plan(unet_plan* p) {
     cv.wacc = A.take(n * sizeof(float));
   }
   p->zero_bwd_bytes = A.top - p->zero_bwd_off;
-  for (auto& b : p->bns) b.save = A.take((size_t)2 * b.C * sizeof(float));
+  for (auto& b : p->bns) {
+    b.save = A.take((size_t)2 * b.C * sizeof(float));
+    b.ss = A.take((size_t)2 * b.C * sizeof(float));
+    b.coef = A.take((size_t)5 * b.C * sizeof(float));
+  }
   for (auto& cv : p->convs) {
     if (cv.kind == L_STEM) {
       cv.pk_fwd = A.take((size_t)cv.Co * 64 * 2);
@@ -514,6 +526,8 @@ BnLaunch bn_launch(const Ctx& x, int bi, int64_t npix) {
   l.eps = x.p->cfg.bn_eps;
   l.momentum = x.p->cfg.bn_momentum;
   l.training = x.training;
+  l.ss = x.W<float>(b.ss);
+  l.ticket = x.W<unsigned>(b.tfwd);
   return l;
 }
 
@@ -533,6 +547,7 @@ int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for
   a.y = x.A(out); a.ldy = out.ld;
   a.bias = cv.b >= 0 ? x.prm[cv.b] : nullptr;
   a.stats = (bn_for_stats >= 0 && x.training) ? x.W<double>(x.p->bns[bn_for_stats].stats) : nullptr;
+  if (a.stats) a.bn = bn_launch(x, bn_for_stats, (int64_t)x.p->cfg.N * out.H * out.W);
   a.N = x.p->cfg.N; a.H = in.H; a.W = in.W; a.C = cv.Ci;
   a.P = out.H; a.Q = out.W; a.Cout = cv.Co;
   a.R = cv.R; a.S = cv.S; a.stride = cv.stride; a.pad = cv.pad;
@@ -626,6 +641,8 @@ int bn_backward(const Ctx& x, int bi, const Act& dout, const Act& out, const Act
     a.dbeta2 = grads + x.p->params[b2.beta].flat;
   }
   if (dres) { a.dres = x.A(*dres); a.lddres = dres->ld; }
+  a.ticket = x.W<unsigned>(b.tbwd);
+  a.coef = x.W<float>(b.coef);
   a.npix = npix; a.C = y.C; a.relu = 1;
   CK(launch_bn_bwd_reduce(a, x.st));
   CK(launch_bn_bwd_apply(a, x.st));
@@ -698,6 +715,7 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
     a.w = x.W<bf16_t>(cv.pk_fwd);
     a.y = x.A(p->y0); a.ldy = p->y0.ld;
     a.stats = training ? x.W<double>(p->bns[p->stem_bn].stats) : nullptr;
+    if (a.stats) a.bn = bn_launch(x, p->stem_bn, (int64_t)N * p->y0.H * p->y0.W);
     a.N = N; a.H = p->cfg.H; a.W = p->cfg.W; a.C = 1;
     a.P = p->y0.H; a.Q = p->y0.W; a.Cout = cv.Co;
     a.R = 7; a.S = 7; a.stride = 2; a.pad = 3;
@@ -935,6 +953,11 @@ int unet_backward(unet_plan* p, const float* image, const float* dlogits, const 
     if (!p || !image || !dlogits || !params || !workspace || !grads) { set_err("null argument"); return 1; }
     return run_backward(p, image, dlogits, params, reinterpret_cast<char*>(workspace), grads, stream);
   })
+}
+
+int unet_set_conv_config(int cfg) {
+  set_conv_config(cfg);
+  return 0;
 }
 
 int unet_plan_use_bucket_events(unet_plan* p, int on) {

@@ -17,13 +17,26 @@ constexpr int kStatRep = 16;
 enum { ALOAD_NHWC = 0, ALOAD_STEM = 1 };
 enum { XLOAD_NHWC = 0, XLOAD_STEM = 1 };
 
+// BatchNorm parameters of one layer.  Training: the producer of the batch sums
+// (conv epilogue) finalises them in its LAST block (ticket counter) into
+// ss = {scale[C], shift[C]}, save_mean/save_invstd and the running stats;
+// consumers then only read ss.  Eval: scale/shift from the running stats.
+struct BnLaunch {
+  const double* stats; const float* gamma; const float* beta;
+  float* run_mean; float* run_var; float* save_mean; float* save_invstd;
+  double count; int C; float eps, momentum; int training;
+  float* ss;          // [2][C] scale | shift (written by the finaliser)
+  unsigned* ticket;   // zeroed per step; last arriving block finalises
+};
+
 struct ConvFwdArgs {
   const bf16_t* x; int ldx;      // input NHWC bf16, channel stride ldx (stem: fp32 [N,H,W])
   const bf16_t* w;               // packed weights [Cout][R*S*C] (stem: [64][64])
   bf16_t* y; int ldy;            // output NHWC bf16
   const float* bias;             // [Cout] or null
   const bf16_t* add; int ldadd;  // optional addend (same pixel grid as y)
-  double* stats;                 // optional BN sums [2][Cout] (fp64 atomics)
+  double* stats;                 // optional BN sums [kStatRep][2][Cout] (fp64 atomics)
+  BnLaunch bn;                   // finalised by the last block when bn.ticket != null
   int N, H, W, C;                // input geometry (C = GEMM reduction channels)
   int P, Q, Cout;                // output geometry
   int R, S, stride, pad;
@@ -41,14 +54,10 @@ struct ConvWgradArgs {
 hipError_t launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st);
 hipError_t launch_conv_fwd_v1(const ConvFwdArgs& a, int mode, hipStream_t st);  // register-staged
 void set_conv_impl(int glds);  // 1: LDS-DMA pipelined kernels (default), 0: register-staged v1
+void set_conv_config(int cfg);  // 0: automatic tile selection, >0: fixed tile config (tuning)
 hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st);
 
 // ---- elementwise / reduction kernels (elementwise.hip) ----
-struct BnLaunch {
-  const double* stats; const float* gamma; const float* beta;
-  float* run_mean; float* run_var; float* save_mean; float* save_invstd;
-  double count; int C; float eps, momentum; int training;
-};
 
 // A = act( bn(Y) + residual ), residual: 0 none, 1 identity tensor R, 2 bn2(R)
 struct BnApplyArgs {
@@ -73,8 +82,10 @@ struct BnBwdArgs {
   bf16_t* dy; int lddy;              // apply: dY out
   bf16_t* dy2; int lddy2;            // apply: dY2 out (bn2)
   bf16_t* dres; int lddres;          // apply: dZ out (identity residual) or null
-  float* dgamma; float* dbeta;       // apply: param grads (block 0)
+  float* dgamma; float* dbeta;       // param grads (written by the reduce's last block)
   float* dgamma2; float* dbeta2;
+  unsigned* ticket;                  // zeroed per step; reduce's last block finalises
+  float* coef;                       // [5][C]: k1, mean dZ, mean dZ*xhat, k1b, mean dZ*xhat2
   int64_t npix; int C; int relu;
 };
 hipError_t launch_bn_bwd_reduce(const BnBwdArgs& a, hipStream_t st);

@@ -100,6 +100,9 @@ int unet_conv_fwd(const void* x, int ldx, const void* w, void* y, int ldy, const
 int unet_conv_wgrad(const void* dy, int lddy, const void* x, int ldx, float* dw_acc, int N, int H,
                     int W, int C, int P, int Q, int Cout, int R, int S, int stride, int pad, int stem,
                     hipStream_t stream);
+/* tile configuration of the implicit-GEMM conv kernels: 0 automatic (default),
+ * >0 a fixed configuration from the tuning table (scripts/tune_conv.py) */
+int unet_set_conv_config(int cfg);
 /* kind: 0 conv fwd, 1 conv dgrad, 2 convT fwd, 3 convT dgrad, 4 stem */
 int unet_pack_weight(const float* src, void* dst, int kind, int Co, int Ci, int R, int S,
                      hipStream_t stream);

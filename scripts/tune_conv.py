@@ -1,0 +1,84 @@
+"""Time every implicit-GEMM tile configuration on the U-Net's conv shapes
+(Base config, N=16) in one process, interleaved (cdna_hip_programming.md §5.4
+rule 24).  Prints, per shape and mode, the median us of each config and the
+best one.  usage: python scripts/tune_conv.py [--reps 5]"""
+import argparse
+import importlib
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+importlib.import_module("image-segmentation-project_amd")
+L = importlib.import_module("image-segmentation-project_amd._lib").load()
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--n", type=int, default=16)
+ap.add_argument("--cfgs", type=str, default="0,1,2,3,4,5,6,7,8,9,10,11,12,13,14")
+args = ap.parse_args()
+N = args.n
+CFGS = [int(c) for c in args.cfgs.split(",")]
+S = lambda: torch.cuda.current_stream().cuda_stream
+
+# (name, C_in, C_out, H_in, R, stride, pad) forward geometry of the conv
+SHAPES = [
+    ("enc1 3x3", 64, 64, 128, 3, 1, 1),
+    ("enc2 3x3", 128, 128, 64, 3, 1, 1),
+    ("enc3 3x3", 256, 256, 32, 3, 1, 1),
+    ("enc4 3x3", 512, 512, 16, 3, 1, 1),
+    ("dec4.0", 512, 256, 32, 3, 1, 1),
+    ("dec3.0", 256, 128, 64, 3, 1, 1),
+    ("dec2.0", 128, 64, 128, 3, 1, 1),
+    ("dec1.0", 96, 32, 256, 3, 1, 1),
+    ("dec1.3", 32, 32, 256, 3, 1, 1),
+    ("enc2.0 s2", 64, 128, 128, 3, 2, 1),
+    ("enc3.0 s2", 128, 256, 64, 3, 2, 1),
+    ("enc4.0 s2", 256, 512, 32, 3, 2, 1),
+]
+
+
+def run(mode, C, Co, H, R, st, pad):
+    """mode 0: forward conv; mode 1: dgrad (transposed gather) of that conv."""
+    P = (H + 2 * pad - R) // st + 1
+    if mode == 0:
+        x = torch.randn(N, H, H, C, device="cuda").to(torch.bfloat16)
+        y = torch.empty(N, P, P, Co, device="cuda", dtype=torch.bfloat16)
+        w = torch.randn(Co * R * R * C, device="cuda").to(torch.bfloat16)
+        args_ = (x.data_ptr(), C, w.data_ptr(), y.data_ptr(), Co, 0, 0, 0, 0, N, H, H, C, P, P, Co, R, R, st, pad, 0)
+        flops = 2.0 * N * P * P * Co * C * R * R
+    else:
+        x = torch.randn(N, P, P, Co, device="cuda").to(torch.bfloat16)
+        y = torch.empty(N, H, H, C, device="cuda", dtype=torch.bfloat16)
+        w = torch.randn(Co * R * R * C, device="cuda").to(torch.bfloat16)
+        args_ = (x.data_ptr(), Co, w.data_ptr(), y.data_ptr(), C, 0, 0, 0, 0, N, P, P, Co, H, H, C, R, R, st, pad, 1)
+        flops = 2.0 * N * P * P * Co * C * R * R
+    keep = (x, y, w)
+    return args_, flops, keep
+
+
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+for name, C, Co, H, R, st, pad in SHAPES:
+    for mode in (0, 1):
+        a, flops, keep = run(mode, C, Co, H, R, st, pad)
+        times = {c: [] for c in CFGS}
+        for rep in range(args.reps):
+            for c in CFGS:
+                L.unet_set_conv_config(c)
+                if L.unet_conv_fwd(*a, S()) != 0:
+                    times[c] = None
+                    continue
+                if times[c] is None:
+                    continue
+                e0.record()
+                for _ in range(5):
+                    L.unet_conv_fwd(*a, S())
+                e1.record()
+                torch.cuda.synchronize()
+                times[c].append(e0.elapsed_time(e1) / 5 * 1e3)
+        L.unet_set_conv_config(0)
+        res = {c: sorted(t)[len(t) // 2] for c, t in times.items() if t}
+        best = min(res, key=res.get)
+        line = " ".join(f"{c}:{res[c]:.0f}" for c in sorted(res))
+        print(f"{name:10s} {'fwd' if mode == 0 else 'dgrad':5s} best cfg {best:2d} {res[best]:7.1f}us "
+              f"{flops / res[best] / 1e6:6.0f} TF | auto {res.get(0, 0):.0f}us | {line}", flush=True)
