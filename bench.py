@@ -26,6 +26,19 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
 
 
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (scripts/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md
+    HBM section), or None when that kernel was not profiled."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        table = json.load(f)
+    ent = table.get(kernel)
+    return None if ent is None else ent["bytes_per_launch"]
+
+
 def cpu_baseline(batch: int, h: int, steps: int, threads: int):
     """Time the oracle (fp32 torch-CPU restatement of the reference path) on host cores."""
     import oracle
@@ -130,8 +143,19 @@ def main():
     plan.profile(False)
     conv = [r for r in recs if r[2] > 0]
     conv_ms = sum(r[1] for r in conv)
-    achieved_tflops = sum(r[2] for r in conv) / 1e9 / conv_ms if conv_ms > 0 else 0.0
+    conv_tflops = sum(r[2] for r in conv) / 1e9 / conv_ms if conv_ms > 0 else 0.0
     kernel_ms_total = sum(r[1] for r in recs)
+    # dominant kernel = the conv template instance with the most event time
+    by_kernel = {}
+    for name, ms_, fl, kern in conv:
+        k = by_kernel.setdefault(kern, [0.0, 0.0, 0])
+        k[0] += ms_
+        k[1] += fl
+        k[2] += 1
+    dom = max(by_kernel, key=lambda k: by_kernel[k][0])
+    dom_ms, dom_fl, dom_n = by_kernel[dom]
+    achieved_tflops = dom_fl / 1e9 / dom_ms
+    traffic = pmc_traffic(dom)
     line = {
         "metric": "images/sec + mIoU, 512x512 U-Net bf16 at 1/2/4/8 MI355X",
         "value": round(imgs / dt, 3),
@@ -151,9 +175,12 @@ def main():
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "achieved": round(achieved_tflops, 2), "peak": MFMA_BF16_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved_tflops / MFMA_BF16_PEAK_TFLOPS, 4),
-                     "traffic": None,
-                     "kernel": "implicit-GEMM conv (fwd+dgrad+wgrad launches, algorithmic FLOPs / event time)",
-                     "conv_ms_per_step": round(conv_ms, 3), "kernel_ms_per_step": round(kernel_ms_total, 3),
+                     "traffic": traffic,
+                     "kernel": dom, "launches_per_step": dom_n,
+                     "avg_launch_us": round(dom_ms / dom_n * 1e3, 2),
+                     "kernel_ms_per_step": round(dom_ms, 3),
+                     "conv_family_tflops": round(conv_tflops, 2), "conv_ms_per_step": round(conv_ms, 3),
+                     "all_kernels_ms_per_step": round(kernel_ms_total, 3),
                      "step_tflops": round(step_tflops, 2),
                      "step_frac": round(step_tflops / MFMA_BF16_PEAK_TFLOPS, 4)},
         "graph": bool(use_graph),

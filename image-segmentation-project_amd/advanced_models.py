@@ -84,7 +84,9 @@ class _Plan:
         _lib.check(self.lib.unet_profile_enable(self.handle, 1 if on else 0), "unet_profile_enable")
 
     def profile_report(self):
-        """[(name, ms, flops)] for every launch recorded since profile(True)."""
+        """[(name, ms, flops, kernel)] for every launch recorded since profile(True);
+        kernel = the conv kernel's template instance (as rocprofv3 names it) for
+        conv launches, "" otherwise."""
         n = self.lib.unet_profile_report(self.handle, None, 0)
         if n < 0:
             _lib.check(1, "unet_profile_report")
@@ -92,8 +94,8 @@ class _Plan:
         self.lib.unet_profile_report(self.handle, buf, n + 16)
         out = []
         for line in buf.value.decode().splitlines():
-            name, ms, fl = line.split("\t")
-            out.append((name, float(ms), float(fl)))
+            name, ms, fl, kern = (line.split("\t") + [""])[:4]
+            out.append((name, float(ms), float(fl), kern))
         return out
 
     def tensor_views(self):

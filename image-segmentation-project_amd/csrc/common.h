@@ -135,3 +135,31 @@ __device__ __forceinline__ void bn_finalize(const unet::BnLaunch& p) {
     }
   }
 }
+
+// Last block of a BN-backward reduction (bn_bwd_reduce_kernel or a fused
+// conv-dgrad epilogue): per-channel coefficients of the apply pass and the
+// parameter gradients dgamma = sum dZ*xhat, dbeta = sum dZ.
+__device__ __forceinline__ void bn_bwd_finalize(const unet::BnBwdArgs& a) {
+  const bool two = a.y2 != nullptr;
+  const double inv_n = 1.0 / (double)a.npix;
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+    double s1 = 0.0, s2 = 0.0, t2 = 0.0;
+    for (int r = 0; r < unet::kStatRep; ++r) {
+      const size_t rep = (size_t)r * 2 * a.C;
+      s1 += a.sums[rep + c];
+      s2 += a.sums[rep + a.C + c];
+      if (two) t2 += a.sums2[rep + a.C + c];
+    }
+    a.coef[c] = a.gamma[c] * a.invstd[c];
+    a.coef[a.C + c] = (float)(s1 * inv_n);
+    a.coef[2 * a.C + c] = (float)(s2 * inv_n);
+    a.dgamma[c] = (float)s2;
+    a.dbeta[c] = (float)s1;
+    if (two) {
+      a.coef[3 * a.C + c] = a.gamma2[c] * a.invstd2[c];
+      a.coef[4 * a.C + c] = (float)(t2 * inv_n);
+      a.dgamma2[c] = (float)t2;
+      a.dbeta2[c] = (float)s1;  // same dZ feeds both BNs
+    }
+  }
+}

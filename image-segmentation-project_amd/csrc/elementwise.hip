@@ -198,30 +198,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a) {
     }
     __syncthreads();
   }
-  if (a.ticket && last_block_arrive(a.ticket, gridDim.x, reinterpret_cast<int*>(red), true)) {
-    // coefficients of the apply pass + parameter gradients, once per channel
-    const double inv_n = 1.0 / (double)a.npix;
-    for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
-      double s1 = 0.0, s2 = 0.0, t2 = 0.0;
-      for (int r = 0; r < kStatRep; ++r) {
-        const size_t rep = (size_t)r * 2 * a.C;
-        s1 += a.sums[rep + c];
-        s2 += a.sums[rep + a.C + c];
-        if (two) t2 += a.sums2[rep + a.C + c];
-      }
-      a.coef[c] = a.gamma[c] * a.invstd[c];
-      a.coef[a.C + c] = (float)(s1 * inv_n);
-      a.coef[2 * a.C + c] = (float)(s2 * inv_n);
-      a.dgamma[c] = (float)s2;
-      a.dbeta[c] = (float)s1;
-      if (two) {
-        a.coef[3 * a.C + c] = a.gamma2[c] * a.invstd2[c];
-        a.coef[4 * a.C + c] = (float)(t2 * inv_n);
-        a.dgamma2[c] = (float)t2;
-        a.dbeta2[c] = (float)s1;  // same dZ feeds both BNs
-      }
-    }
-  }
+  if (a.ticket && last_block_arrive(a.ticket, gridDim.x, reinterpret_cast<int*>(red), true)) bn_bwd_finalize(a);
 }
 
 hipError_t launch_bn_bwd_reduce(const BnBwdArgs& a, hipStream_t st) {

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -99,10 +100,12 @@ struct unet_plan {
   hipEvent_t events[8] = {};
   int nevents = 0;
   bool want_events = false;  // DDP overlap: record one hipEvent per gradient bucket
+  // BN-backward reductions fused into the producing conv dgrad (UNET_NO_BWD_FUSE=1: off, A/B only)
+  bool fuse_bwd = std::getenv("UNET_NO_BWD_FUSE") == nullptr;
   double flops_fwd = 0, flops_train = 0;
   std::vector<std::pair<std::string, Act>> named;  // debug / test introspection
   // per-launch HIP-event profiler (unet_profile_*): one record per kernel
-  struct ProfRec { std::string name; double flops; int e0, e1; };
+  struct ProfRec { std::string name; double flops; int e0, e1; std::string kernel; };
   bool prof = false;
   std::vector<hipEvent_t> evpool;
   int evused = 0;
@@ -129,7 +132,7 @@ struct ProfScope {
   ~ProfScope() {
     if (p->prof && e0 >= 0) {
       const int e1 = prof_event(p, st);
-      if (e1 >= 0) p->recs.push_back({name, flops, e0, e1});
+      if (e1 >= 0) p->recs.push_back({name, flops, e0, e1, flops > 0 ? unet::last_kernel_tag() : ""});
     }
   }
 };
@@ -555,8 +558,10 @@ int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for
   return 0;
 }
 
-// conv dgrad: dx = dgrad(dy) (+ addend)
-int conv_dgrad(const Ctx& x, int ci, const Act& dy, const Act& dx, const Act* add) {
+// conv dgrad: dx = dgrad(dy) (+ addend).  fuse: dx is dA of that BN(+ReLU);
+// the epilogue stores dZ and runs the BN-backward reduction (ConvFwdArgs::bb).
+int conv_dgrad(const Ctx& x, int ci, const Act& dy, const Act& dx, const Act* add,
+               const BnBwdArgs* fuse = nullptr) {
   const Conv& cv = x.p->convs[ci];
   ProfScope ps(x.p, x.st, "dgrad " + pname(x, cv.w), conv_flops(x.p, cv, cv.kind == L_CONVT ? dy : dy));
   ConvFwdArgs a = {};
@@ -564,17 +569,14 @@ int conv_dgrad(const Ctx& x, int ci, const Act& dy, const Act& dx, const Act* ad
   a.w = x.W<bf16_t>(cv.pk_dgrad);
   a.y = x.A(dx); a.ldy = dx.ld;
   if (add && add->ld) { a.add = x.A(*add); a.ldadd = add->ld; }
+  if (fuse) a.bb = *fuse;
   a.N = x.p->cfg.N;
   a.H = dy.H; a.W = dy.W;
   a.P = dx.H; a.Q = dx.W;
   a.R = cv.R; a.S = cv.S; a.stride = cv.stride; a.pad = cv.pad;
-  if (cv.kind == L_CONVT) {  // ordinary k2s2 conv of dY: reduce over Co, produce Ci
-    a.C = cv.Co; a.Cout = cv.Ci;
-    CK(launch_conv_fwd(a, MODE_FWD, x.st));
-  } else {
-    a.C = cv.Co; a.Cout = cv.Ci;
-    CK(launch_conv_fwd(a, MODE_TRANS, x.st));
-  }
+  a.C = cv.Co; a.Cout = cv.Ci;
+  // convT: an ordinary k2s2 conv of dY; conv: the transposed gather
+  CK(launch_conv_fwd(a, cv.kind == L_CONVT ? MODE_FWD : MODE_TRANS, x.st));
   return 0;
 }
 
@@ -616,13 +618,11 @@ int bn_apply(const Ctx& x, int bi, const Act& y, const Act& out, int res_mode, c
   return 0;
 }
 
-// BN(+ReLU) backward for out = relu(bn(y) [+ bn2(y2) | + res]).
-int bn_backward(const Ctx& x, int bi, const Act& dout, const Act& out, const Act& y, const Act& dy,
-                int bi2, const Act* y2, const Act* dy2, const Act* dres, float* grads) {
+// BN(+ReLU) backward argument block for out = relu(bn(y) [+ bn2(y2) | + res]).
+BnBwdArgs bwd_args(const Ctx& x, int bi, const Act& dout, const Act& out, const Act& y, const Act& dy,
+                   int bi2, const Act* y2, const Act* dy2, const Act* dres, float* grads) {
   BnBwdArgs a = {};
   const Bn& b = x.p->bns[bi];
-  const int64_t npix = (int64_t)x.p->cfg.N * y.H * y.W;
-  ProfScope ps(x.p, x.st, "bn_bwd " + pname(x, b.gamma), 0);
   a.da = x.A(dout); a.ldda = dout.ld;
   a.act = x.A(out); a.ldact = out.ld;
   a.y = x.A(y); a.ldy = y.ld;
@@ -643,8 +643,20 @@ int bn_backward(const Ctx& x, int bi, const Act& dout, const Act& out, const Act
   if (dres) { a.dres = x.A(*dres); a.lddres = dres->ld; }
   a.ticket = x.W<unsigned>(b.tbwd);
   a.coef = x.W<float>(b.coef);
-  a.npix = npix; a.C = y.C; a.relu = 1;
-  CK(launch_bn_bwd_reduce(a, x.st));
+  a.npix = (int64_t)x.p->cfg.N * y.H * y.W; a.C = y.C; a.relu = 1;
+  return a;
+}
+
+// fused: the producer of dA already stored dZ (in dA's buffer, which then also
+// serves as the identity-residual gradient) and reduced it; only apply runs.
+int bn_backward(const Ctx& x, int bi, BnBwdArgs a, bool fused) {
+  ProfScope ps(x.p, x.st, "bn_bwd " + pname(x, x.p->bns[bi].gamma), 0);
+  if (fused) {
+    a.relu = 0;
+    a.dres = nullptr;
+  } else {
+    CK(launch_bn_bwd_reduce(a, x.st));
+  }
   CK(launch_bn_bwd_apply(a, x.st));
   return 0;
 }
@@ -785,23 +797,47 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     CK(launch_head_bwd(h, st));
     CK(launch_head_grads(h, st));
   }
+  // BN-backward reductions are fused into the conv dgrad that produces each
+  // BN's dA (all but decoder1's second BN, fed by the head, and the stem BN).
+  const bool fz = p->fuse_bwd;
+  const int nb = (int)p->blocks.size();
+  auto dec_bn1 = [&](int l) {
+    Dec& d = p->decs[l];
+    return bwd_args(x, d.bn1, d.dh, d.h, d.y1, d.dy1, -1, nullptr, nullptr, nullptr, grads);
+  };
+  auto dec_bn2 = [&](int l) {
+    Dec& d = p->decs[l];
+    return bwd_args(x, d.bn2, d.d_out, d.out, d.y2, d.dy2, -1, nullptr, nullptr, nullptr, grads);
+  };
+  auto blk_bn1 = [&](int i) {
+    Block& b = p->blocks[i];
+    return bwd_args(x, b.bn1, b.dh, b.h, b.y1, b.dy1, -1, nullptr, nullptr, nullptr, grads);
+  };
+  auto blk_bn2 = [&](int i) {
+    Block& b = p->blocks[i];
+    if (b.ds >= 0) return bwd_args(x, b.bn2, b.d_out, b.out, b.y2, b.dy2, b.dsbn, &b.yds, &b.dyds, nullptr, grads);
+    return bwd_args(x, b.bn2, b.d_out, b.out, b.y2, b.dy2, -1, nullptr, nullptr, &b.dres, grads);
+  };
   // decoder1 .. decoder4 (+ their up-convs)
   for (int l = 3; l >= 0; --l) {
     Dec& d = p->decs[l];
-    RUN(bn_backward(x, d.bn2, d.d_out, d.out, d.y2, d.dy2, -1, nullptr, nullptr, nullptr, grads));
-    RUN(conv_dgrad(x, d.conv2, d.dy2, d.dh, nullptr));
+    RUN(bn_backward(x, d.bn2, dec_bn2(l), fz && l < 3));
+    const BnBwdArgs f1 = dec_bn1(l);
+    RUN(conv_dgrad(x, d.conv2, d.dy2, d.dh, nullptr, fz ? &f1 : nullptr));
     RUN(conv_wgrad(x, d.conv2, d.dy2, d.h));
-    RUN(bn_backward(x, d.bn1, d.dh, d.h, d.y1, d.dy1, -1, nullptr, nullptr, nullptr, grads));
+    RUN(bn_backward(x, d.bn1, f1, fz));
     RUN(conv_dgrad(x, d.conv1, d.dy1, d.dcat, nullptr));
     RUN(conv_wgrad(x, d.conv1, d.dy1, d.cat));
     // decoder conv biases feed a training-mode BN: their exact gradient is
     // sum(dY) = 0 (BN removes the mean); write it explicitly.
     CK(hipMemsetAsync(grads + p->params[p->convs[d.conv1].b].flat, 0, sizeof(float) * p->convs[d.conv1].Co, st));
     CK(hipMemsetAsync(grads + p->params[p->convs[d.conv2].b].flat, 0, sizeof(float) * p->convs[d.conv2].Co, st));
-    // up-conv: dU = dcat[:, skip:]
+    // up-conv: dU = dcat[:, skip:]; its dgrad is dA of the previous decoder's
+    // (or enc4's) last BN
     const Conv& up = p->convs[d.up];
     Act du = slice(d.dcat, d.cat.C - up.Co, up.Co);
-    RUN(conv_dgrad(x, d.up, du, d.d_up_in, nullptr));
+    const BnBwdArgs fu = l > 0 ? dec_bn2(l - 1) : blk_bn2(nb - 1);
+    RUN(conv_dgrad(x, d.up, du, d.d_up_in, nullptr, fz ? &fu : nullptr));
     RUN(conv_wgrad(x, d.up, du, d.up_in));
     ProfScope ps(p, st, "bias_sum", 0);
     CK(launch_channel_sum(x.A(du), du.ld, (int64_t)N * du.H * du.W, up.Co, x.W<double>(up.bias_acc), st));
@@ -810,23 +846,24 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
   RUN(unpack_bucket(x, 0, grads));
   if (p->nevents) CK(hipEventRecord(p->events[0], st));
   // encoder blocks, deepest first
-  const int nb = (int)p->blocks.size();
   for (int i = nb - 1; i >= 0; --i) {
     Block& b = p->blocks[i];
-    if (b.ds >= 0) {
-      RUN(bn_backward(x, b.bn2, b.d_out, b.out, b.y2, b.dy2, b.dsbn, &b.yds, &b.dyds, nullptr, grads));
-    } else {
-      RUN(bn_backward(x, b.bn2, b.d_out, b.out, b.y2, b.dy2, -1, nullptr, nullptr, &b.dres, grads));
-    }
-    RUN(conv_dgrad(x, b.conv2, b.dy2, b.dh, nullptr));
+    RUN(bn_backward(x, b.bn2, blk_bn2(i), fz));
+    const BnBwdArgs f1 = blk_bn1(i);
+    RUN(conv_dgrad(x, b.conv2, b.dy2, b.dh, nullptr, fz ? &f1 : nullptr));
     RUN(conv_wgrad(x, b.conv2, b.dy2, b.h));
-    RUN(bn_backward(x, b.bn1, b.dh, b.h, b.y1, b.dy1, -1, nullptr, nullptr, nullptr, grads));
+    RUN(bn_backward(x, b.bn1, f1, fz));
+    // the last writer of d_in produces dA of the previous block's bn2
+    BnBwdArgs fp = {};
+    const BnBwdArgs* fprev = nullptr;
+    if (fz && i > 0) { fp = blk_bn2(i - 1); fprev = &fp; }
     if (b.ds >= 0) {
       RUN(conv_dgrad(x, b.conv1, b.dy1, b.d_in, b.skip_add.ld ? &b.skip_add : nullptr));
-      RUN(conv_dgrad(x, b.ds, b.dyds, b.d_in, &b.d_in));
+      RUN(conv_dgrad(x, b.ds, b.dyds, b.d_in, &b.d_in, fprev));
       RUN(conv_wgrad(x, b.ds, b.dyds, b.in));
     } else {
-      RUN(conv_dgrad(x, b.conv1, b.dy1, b.d_in, &b.dres));
+      // identity path: dZ of bn2 (held in d_out when fused)
+      RUN(conv_dgrad(x, b.conv1, b.dy1, b.d_in, fz ? &b.d_out : &b.dres, fprev));
     }
     RUN(conv_wgrad(x, b.conv1, b.dy1, b.in));
     // bucket boundaries: enc4 done at i == 13, enc3 at i == 7
@@ -845,7 +882,9 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
       ProfScope ps(p, st, "maxpool_bwd", 0);
       CK(launch_maxpool_bwd(m, st));
     }
-    RUN(bn_backward(x, p->stem_bn, p->d_x1, p->x1, p->y0, p->d_y0, -1, nullptr, nullptr, nullptr, grads));
+    RUN(bn_backward(x, p->stem_bn,
+                    bwd_args(x, p->stem_bn, p->d_x1, p->x1, p->y0, p->d_y0, -1, nullptr, nullptr, nullptr, grads),
+                    false));
     const Conv& cv = p->convs[p->stem_conv];
     ConvWgradArgs a = {};
     a.dy = x.A(p->d_y0); a.lddy = p->d_y0.ld;
@@ -984,7 +1023,7 @@ int unet_profile_report(unet_plan* p, char* buf, int64_t buflen) {
   for (const auto& r : p->recs) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, p->evpool[r.e0], p->evpool[r.e1]) != hipSuccess) ms = -1.f;
-    std::snprintf(line, sizeof(line), "%s\t%.6f\t%.6e\n", r.name.c_str(), ms, r.flops);
+    std::snprintf(line, sizeof(line), "%s\t%.6f\t%.6e\t%s\n", r.name.c_str(), ms, r.flops, r.kernel.c_str());
     out += line;
   }
   if (buf && buflen > 0) std::snprintf(buf, (size_t)buflen, "%s", out.c_str());

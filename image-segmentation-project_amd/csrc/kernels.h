@@ -29,46 +29,6 @@ struct BnLaunch {
   unsigned* ticket;   // zeroed per step; last arriving block finalises
 };
 
-struct ConvFwdArgs {
-  const bf16_t* x; int ldx;      // input NHWC bf16, channel stride ldx (stem: fp32 [N,H,W])
-  const bf16_t* w;               // packed weights [Cout][R*S*C] (stem: [64][64])
-  bf16_t* y; int ldy;            // output NHWC bf16
-  const float* bias;             // [Cout] or null
-  const bf16_t* add; int ldadd;  // optional addend (same pixel grid as y)
-  double* stats;                 // optional BN sums [kStatRep][2][Cout] (fp64 atomics)
-  BnLaunch bn;                   // finalised by the last block when bn.ticket != null
-  int N, H, W, C;                // input geometry (C = GEMM reduction channels)
-  int P, Q, Cout;                // output geometry
-  int R, S, stride, pad;
-  int mblocks, nblocks, Pc, Qc;  // filled by the launcher
-};
-
-struct ConvWgradArgs {
-  const bf16_t* dy; int lddy;    // gradient wrt conv output [N,P,Q,Cout]
-  const bf16_t* x; int ldx;      // conv input [N,H,W,C] (stem: fp32 image)
-  float* dw;                     // fp32 accumulator [Cout][R*S*C] (stem: [64][64])
-  int N, H, W, C, P, Q, Cout, R, S, stride, pad;
-  int px_per_split, co_blocks, c_blocks;  // filled by the launcher
-};
-
-hipError_t launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st);
-hipError_t launch_conv_fwd_v1(const ConvFwdArgs& a, int mode, hipStream_t st);  // register-staged
-void set_conv_impl(int glds);  // 1: LDS-DMA pipelined kernels (default), 0: register-staged v1
-void set_conv_config(int cfg);  // 0: automatic tile selection, >0: fixed tile config (tuning)
-hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st);
-
-// ---- elementwise / reduction kernels (elementwise.hip) ----
-
-// A = act( bn(Y) + residual ), residual: 0 none, 1 identity tensor R, 2 bn2(R)
-struct BnApplyArgs {
-  const bf16_t* y; int ldy;
-  bf16_t* out; int ldo;
-  const bf16_t* res; int ldr;
-  BnLaunch bn, bn2;
-  int64_t npix; int C; int res_mode; int relu;
-};
-hipError_t launch_bn_apply(const BnApplyArgs& a, hipStream_t st);
-
 // backward: dZ = dA * (A > 0); sums over pixels of dZ and dZ*xhat (and for bn2)
 struct BnBwdArgs {
   const bf16_t* da; int ldda;
@@ -88,6 +48,52 @@ struct BnBwdArgs {
   float* coef;                       // [5][C]: k1, mean dZ, mean dZ*xhat, k1b, mean dZ*xhat2
   int64_t npix; int C; int relu;
 };
+struct ConvFwdArgs {
+  const bf16_t* x; int ldx;      // input NHWC bf16, channel stride ldx (stem: fp32 [N,H,W])
+  const bf16_t* w;               // packed weights [Cout][R*S*C] (stem: [64][64])
+  bf16_t* y; int ldy;            // output NHWC bf16
+  const float* bias;             // [Cout] or null
+  const bf16_t* add; int ldadd;  // optional addend (same pixel grid as y)
+  double* stats;                 // optional BN sums [kStatRep][2][Cout] (fp64 atomics)
+  BnLaunch bn;                   // finalised by the last block when bn.ticket != null
+  // fused BN(+ReLU) backward reduction (conv dgrad producing dA of a BN):
+  // when bb.sums != null the epilogue writes dZ = dA * (act > 0) instead of dA
+  // and adds sum dZ, sum dZ*xhat (and dZ*xhat2) into bb.sums / bb.sums2; the
+  // last block runs bn_bwd_finalize (common.h).
+  BnBwdArgs bb;
+  int N, H, W, C;                // input geometry (C = GEMM reduction channels)
+  int P, Q, Cout;                // output geometry
+  int R, S, stride, pad;
+  int mblocks, nblocks, Pc, Qc;  // filled by the launcher
+};
+
+struct ConvWgradArgs {
+  const bf16_t* dy; int lddy;    // gradient wrt conv output [N,P,Q,Cout]
+  const bf16_t* x; int ldx;      // conv input [N,H,W,C] (stem: fp32 image)
+  float* dw;                     // fp32 accumulator [Cout][R*S*C] (stem: [64][64])
+  int N, H, W, C, P, Q, Cout, R, S, stride, pad;
+  int px_per_split, co_blocks, c_blocks;  // filled by the launcher
+};
+
+hipError_t launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st);
+hipError_t launch_conv_fwd_v1(const ConvFwdArgs& a, int mode, hipStream_t st);  // register-staged
+void set_conv_impl(int glds);  // 1: LDS-DMA pipelined kernels (default), 0: register-staged v1
+void set_conv_config(int cfg);  // 0: automatic tile selection, >0: fixed tile config (tuning)
+hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st);
+const char* last_kernel_tag();  // template instance of the last conv launch (profiler)
+
+// ---- elementwise / reduction kernels (elementwise.hip) ----
+
+// A = act( bn(Y) + residual ), residual: 0 none, 1 identity tensor R, 2 bn2(R)
+struct BnApplyArgs {
+  const bf16_t* y; int ldy;
+  bf16_t* out; int ldo;
+  const bf16_t* res; int ldr;
+  BnLaunch bn, bn2;
+  int64_t npix; int C; int res_mode; int relu;
+};
+hipError_t launch_bn_apply(const BnApplyArgs& a, hipStream_t st);
+
 hipError_t launch_bn_bwd_reduce(const BnBwdArgs& a, hipStream_t st);
 hipError_t launch_bn_bwd_apply(const BnBwdArgs& a, hipStream_t st);
 

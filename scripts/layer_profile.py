@@ -14,6 +14,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=16)
 ap.add_argument("--size", type=int, default=512)
 ap.add_argument("--top", type=int, default=40)
+ap.add_argument("--all", action="store_true")
 args = ap.parse_args()
 
 torch.manual_seed(0)
@@ -46,7 +47,7 @@ fl = sum(r[2] for r in recs)
 print(f"launches {len(recs)}  sum of kernel ms {tot:.3f}  conv TFLOP/s over conv launches "
       f"{sum(r[2] for r in recs if r[2] > 0) / 1e9 / sum(r[1] for r in recs if r[2] > 0):.1f}")
 by_kind = defaultdict(lambda: [0.0, 0.0, 0])
-for name, ms_, f in recs:
+for name, ms_, f, _ in recs:
     k = name.split(" ")[0]
     by_kind[k][0] += ms_
     by_kind[k][1] += f
@@ -55,6 +56,11 @@ for k, (t, f, n) in sorted(by_kind.items(), key=lambda kv: -kv[1][0]):
     tf = f / 1e9 / t if t > 0 and f > 0 else 0
     print(f"{k:12s} n={n:3d} {t:8.3f} ms  {100 * t / tot:5.1f}%  {tf:7.1f} TFLOP/s")
 print("--- top launches")
-for name, ms_, f in sorted(recs, key=lambda r: -r[1])[: args.top]:
+for name, ms_, f, kern in sorted(recs, key=lambda r: -r[1])[: args.top]:
     tf = f / 1e9 / ms_ if ms_ > 0 and f > 0 else 0
-    print(f"{name:40s} {ms_ * 1e3:9.1f} us  {tf:7.1f} TFLOP/s")
+    print(f"{name:40s} {ms_ * 1e3:9.1f} us  {tf:7.1f} TFLOP/s  {kern}")
+if args.all:
+    print("--- all launches in order")
+    for name, ms_, f, kern in recs:
+        tf = f / 1e9 / ms_ if ms_ > 0 and f > 0 else 0
+        print(f"{name:40s} {ms_ * 1e3:9.1f} us  {tf:7.1f} TFLOP/s  {kern}")

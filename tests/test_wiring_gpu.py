@@ -65,6 +65,13 @@ def run(pkg, golden, cuda):
     return ref, x, y, out.detach().cpu(), v, grads
 
 
+def _masked(a, b, act):
+    """dA buffers consumed by a BN+ReLU hold dZ = dA * (act > 0) when the BN
+    backward reduction is fused into their producer: compare under the mask."""
+    m = (act > 0).float()
+    return _rel(a * m, b * m)
+
+
 def _check(rows):
     for name, e in rows:
         print(f"{name:28s} {e:.3e}")
@@ -137,7 +144,7 @@ def test_backward_ops(run):
         rows += [(p + "d.y2", _rel(v[p + "d.y2"], dy2)), (f"g decoder{lvl}.4.weight", _rel(grads[f"decoder{lvl}.4.weight"], dg)),
                  (f"g decoder{lvl}.4.bias", _rel(grads[f"decoder{lvl}.4.bias"], db))]
         dh = torch.nn.grad.conv2d_input(v[p + "h"].shape, W(dec[3]), v[p + "d.y2"], padding=1)
-        rows.append((p + "d.h", _rel(v[p + "d.h"], dh)))
+        rows.append((p + "d.h", _masked(v[p + "d.h"], dh, v[p + "h"])))
         gw = torch.nn.grad.conv2d_weight(v[p + "h"], dec[3].weight.shape, v[p + "d.y2"], padding=1)
         rows.append((f"g decoder{lvl}.3.weight", _rel(grads[f"decoder{lvl}.3.weight"], gw)))
         dy1, dg, db = local_bn_bwd(v[p + "y1"], v[p + "d.h"], dec[1], out=v[p + "h"])
@@ -154,7 +161,7 @@ def test_backward_ops(run):
         bl = up.bias.detach().clone().requires_grad_(True)
         F.conv_transpose2d(xin, wl, bl, stride=2).backward(du)
         tgt = "enc4.2.d.out" if lvl == 4 else f"dec{lvl + 1}.d.out"
-        rows += [(tgt + " (convT dgrad)", _rel(v[tgt], xin.grad)),
+        rows += [(tgt + " (convT dgrad)", _masked(v[tgt], xin.grad, v[upin_name])),
                  (f"g upconv{lvl}.weight", _rel(grads[f"upconv{lvl}.weight"], wl.grad)),
                  (f"g upconv{lvl}.bias", _rel(grads[f"upconv{lvl}.bias"], bl.grad))]
     # encoder blocks
@@ -187,7 +194,7 @@ def test_backward_ops(run):
                      (f"g {p}downsample.1.weight", _rel(grads[p + "downsample.1.weight"], gd.grad)),
                      (f"g {p}downsample.1.bias", _rel(grads[p + "downsample.1.bias"], bd.grad))]
         dh = torch.nn.grad.conv2d_input(v[p + "h"].shape, W(blk.conv2), v[p + "d.y2"], padding=1)
-        rows.append((p + "d.h", _rel(v[p + "d.h"], dh)))
+        rows.append((p + "d.h", _masked(v[p + "d.h"], dh, v[p + "h"])))
         rows.append((f"g {p}conv2.weight", _rel(grads[p + "conv2.weight"],
                                                  torch.nn.grad.conv2d_weight(v[p + "h"], blk.conv2.weight.shape, v[p + "d.y2"], padding=1))))
         dy1, dg, db = local_bn_bwd(v[p + "y1"], v[p + "d.h"], blk.bn1, out=v[p + "h"])
@@ -204,7 +211,7 @@ def test_backward_ops(run):
             lvl = {1: 2, 2: 3, 3: 4}[s]
             din = din + v[f"dec{lvl}.d.cat"][:, :inp.shape[1]]
         tgt = "d.p0" if i == 0 else names[i - 1][0] + "d.out"
-        rows.append((tgt + " (block dgrad)", _rel(v[tgt], din)))
+        rows.append((tgt + " (block dgrad)", _rel(v[tgt], din) if i == 0 else _masked(v[tgt], din, inp)))
         rows.append((f"g {p}conv1.weight", _rel(grads[p + "conv1.weight"], torch.nn.grad.conv2d_weight(
             inp, blk.conv1.weight.shape, v[p + "d.y1"], stride=st, padding=1))))
     # maxpool + stem
