@@ -15,6 +15,7 @@ from .train import (evaluate, quick_train, train_epoch, train_model, TensorLoade
                     GraphedTrainStep)
 from .synthetic import random_batch, synthetic_cells  # noqa: F401
 from . import ddp  # noqa: F401
+from .ddp import enable_data_parallel  # noqa: F401
 from ._lib import LIB_PATH  # noqa: F401
 
 __version__ = "0.1.0"
