@@ -29,6 +29,16 @@
 
 namespace unet {
 
+// template instance of the last conv launch ("name<args>", as rocprofv3 prints
+// the kernel symbol) for the per-launch profiler's kernel column
+static thread_local char g_kernel_tag[96];
+template <typename... T>
+static void set_kernel_tag(const char* fmt, T... v) {
+  std::snprintf(g_kernel_tag, sizeof(g_kernel_tag), fmt, v...);
+}
+static void set_kernel_tag(const char* tag) { std::snprintf(g_kernel_tag, sizeof(g_kernel_tag), "%s", tag); }
+const char* last_kernel_tag() { return g_kernel_tag; }
+
 // ---------------------------------------------------------------------------
 // LDS swizzles (cdna_hip_programming.md §2/T2) for ds_read_b128 fragment reads
 // of the 16x16x32 MFMA: lane l reads row (l&15), 16-B chunk (l>>4) [+4*kk].
@@ -783,24 +793,34 @@ conv_wgrad_kernel(ConvWgradArgs a) {
 // ---------------------------------------------------------------------------
 // 3x3 stride-1 weight gradient with an LDS input halo (all 9 taps per block).
 //
-// Block = 64 output channels x 32 input channels x 9 taps (72 fp32 acc / lane)
+// Block = 64 output channels x CI input channels x 9 taps (CI = 32: 4 waves,
+// CI = 64: 8 waves; each wave owns 32 co x 16 ci x 9 taps = 72 fp32 acc/lane)
 // and a split-K range of TH x TW pixel tiles.  Per tile one LDS-DMA stage
-// holds dY [TH*TW px][64 co] and the input halo [(TH+2)(TW+2) px][32 ci];
+// holds dY [TH*TW px][64 co] and the input halo [(TH+2)(TW+2) px][CI ci];
 // every tap reads the halo at a row offset, so the input is fetched once per
 // tile instead of 9 times.  Operands are pixel-major, fed to the MFMA through
-// ds_read_b64_tr_b16.
+// ds_read_b64_tr_b16.  The grid is sized to ~one block per CU; each block
+// stores its fp32 partial dW with plain stores into its split's slab and
+// wgrad_slab_reduce_kernel sums the splits (fp32 atomics into dW when no slab:
+// they run at ~1.3 TB/s chip-wide, MI355X_MICROARCH.md "Global float atomics").
 // ---------------------------------------------------------------------------
-template <int TW, int NS>
-__global__ void __launch_bounds__(256)
+template <int TW, int NS, int CI>
+__global__ void __launch_bounds__(CI * 8)
 wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
+  constexpr int NW = CI / 8;            // waves
   constexpr int TH = 128 / TW;
   constexpr int HW2 = TW + 2;
   constexpr int HROWS = (TH + 2) * HW2;
-  constexpr int A_BYTES = 128 * 128;    // dY: 128 px x 64 co (128-B rows)
-  constexpr int B_BYTES = 16 * 1024;    // halo: up to 256 rows x 32 ci (64-B rows)
+  constexpr int HROWB = CI * 2;         // halo row bytes
+  constexpr int HCPR = HROWB / 16;      // 16-B chunks per halo row
+  constexpr int HRPI = 1024 / HROWB;    // halo rows per wave instruction
+  constexpr int H_INS = 256 / HRPI / NW;
+  constexpr int A_INS = 16 / NW;        // dY: 128 rows of 128 B = 16 instructions
+  constexpr int A_BYTES = 128 * 128;
+  constexpr int B_BYTES = 256 * HROWB;  // halo capacity: 256 rows
   static_assert(HROWS <= 256, "halo rows");
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int LPS = 8;                // 4 dY + 4 halo glds per wave per stage
+  constexpr int LPS = A_INS + H_INS;    // glds per wave per stage
   extern __shared__ __attribute__((aligned(16))) char smem[];
   typedef TrTile<64, 64, 128> TA;
 
@@ -809,7 +829,7 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
   const int wm = wave & 1, wn = wave >> 1;  // wave tile 32 co x 16 ci
   const int cob = blockIdx.x % a.co_blocks;
   const int cib = blockIdx.x / a.co_blocks;
-  const int co0 = cob * 64, c0 = cib * 32;
+  const int co0 = cob * 64, c0 = cib * CI;
   const int t0 = blockIdx.z * tiles_per_split;
   const int t1 = min(tiles_total, t0 + tiles_per_split);
   const int KT = t1 - t0;
@@ -819,8 +839,8 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
 
   // per-lane constant parts of the loads
-  const int arow = lane >> 3, aslot = lane & 7;  // dY: 8 rows of 128 B per instruction
-  const int hrow = lane >> 2, hslot = lane & 3;  // halo: 16 rows of 64 B per instruction
+  const int arow = lane >> 3, aslot = lane & 7;                // dY: 8 rows of 128 B per instruction
+  const int hrow = lane / HCPR, hslot = lane % HCPR;           // halo: HRPI rows per instruction
 
   auto issue = [&](int kt, int buf) {
     const int t = t0 + kt;
@@ -830,23 +850,29 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
     char* As = smem + buf * STAGE;
     char* Bs = As + A_BYTES;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = (wave * 4 + j) * 8 + arow;  // pixel in tile
+    for (int j = 0; j < A_INS; ++j) {
+      const int row = (wave * A_INS + j) * 8 + arow;  // pixel in tile
       const int f = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
       const int lchunk = ((((aslot >> 1) ^ f)) << 1) | (aslot & 1);
       const int oh = oh0 + row / TW, ow = ow0 + row % TW;
       const unsigned off = (unsigned)((((n * a.P + oh) * a.Q + ow) * a.lddy) + co0 + lchunk * 8) * 2u;
-      glds16(dyr, As + (wave * 4 + j) * 1024, off);
+      glds16(dyr, As + (wave * A_INS + j) * 1024, off);
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = (wave * 4 + j) * 16 + hrow;  // halo row
-      const int lchunk = ((((hslot >> 1) ^ ((row >> 3) & 1))) << 1) | (hslot & 1);
+    for (int j = 0; j < H_INS; ++j) {
+      const int row = (wave * H_INS + j) * HRPI + hrow;  // halo row
+      int lchunk;
+      if constexpr (CI == 32) {
+        lchunk = ((((hslot >> 1) ^ ((row >> 3) & 1))) << 1) | (hslot & 1);
+      } else {
+        const int f = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+        lchunk = ((((hslot >> 1) ^ f)) << 1) | (hslot & 1);
+      }
       const int ih = oh0 - 1 + row / HW2, iw = ow0 - 1 + row % HW2;
       unsigned off = kOOB;
       if (row < HROWS && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
         off = (unsigned)((((n * a.H + ih) * a.W + iw) * a.ldx) + c0 + lchunk * 8) * 2u;
-      glds16(xr, Bs + (wave * 4 + j) * 1024, off);
+      glds16(xr, Bs + (wave * H_INS + j) * 1024, off);
     }
   };
 
@@ -883,7 +909,7 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
 #pragma unroll
         for (int s = 0; s < 3; ++s) {
           const int hr = (ty + r) * HW2 + tx + s;
-          const bf16x8 bfr = tr_read8(Bs + tr_off<32>(hr, col), Bs + tr_off<32>(hr + 4, col));
+          const bf16x8 bfr = tr_read8(Bs + tr_off<CI>(hr, col), Bs + tr_off<CI>(hr + 4, col));
 #pragma unroll
           for (int i = 0; i < 2; ++i)
             acc[r * 3 + s][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[r * 3 + s][i], 0, 0, 0);
@@ -891,9 +917,11 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
     }
   }
   wait_vmcnt<0>();
-  // epilogue: fp32 atomics into dw[co][tap][ci]
+  // epilogue: this split's partial dW[co][tap][ci] (plain stores into the
+  // slab) or fp32 atomics into dW
   const int Krow = 9 * a.C;
   const int c = c0 + wn * 16 + li;
+  float* slab = a.slab ? a.slab + (size_t)blockIdx.z * a.Cout * Krow : nullptr;
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
@@ -901,21 +929,319 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int co = co0 + wm * 32 + i * 16 + 4 * g + e;
-        if (co < a.Cout) atomicAdd(a.dw + (size_t)co * Krow + t * a.C + c, acc[t][i][e]);
+        if (co < a.Cout) {
+          if (slab) slab[(size_t)co * Krow + t * a.C + c] = acc[t][i][e];
+          else atomicAdd(a.dw + (size_t)co * Krow + t * a.C + c, acc[t][i][e]);
+        }
       }
+}
+
+// dW[i] (+)= sum of slab[s][i] over the 8 splits s = 8g .. 8g+7, g = blockIdx.y,
+// all 8 loads in flight at once.  gridDim.y > 1: fp32 atomics into the zeroed
+// dW (gridDim.y adds per element), one dword per lane so every wave
+// instruction covers 256 contiguous bytes (the full-rate atomic shape,
+// MI355X_MICROARCH.md "Global float atomics"); else a plain store.
+__global__ void __launch_bounds__(256) wgrad_slab_reduce_kernel(const float* __restrict__ slab, float* dw,
+                                                                int64_t n, int splits) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int s0 = blockIdx.y * 8;
+  float v[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = s0 + k < splits ? slab[(size_t)(s0 + k) * n + i] : 0.f;
+  const float sum = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+  if (gridDim.y == 1) dw[i] = sum;
+  else atomicAdd(dw + i, sum);
+}
+
+// ---------------------------------------------------------------------------
+// 7x7/s2/p3 stem, 1 -> 64 channels, fp32 image.
+//
+// A block walks a contiguous range of output rows (Q pixels each, Q <= 256).
+// Per row the 7 input rows it needs are fetched once (coalesced fp32, issued
+// into registers one row AHEAD so the loads overlap the current row's work),
+// converted to a bf16 LDS patch, and each thread builds its pixel's im2col row
+// (49 taps padded to K = 64) in LDS.  Forward: D[co][px] = W[co][k] .
+// im2col[px][k]; the BN batch sums are kept in registers over all the block's
+// rows and committed once (replica atomics + last-block finalise).  Weight
+// gradient: D[co][k] += sum_px dY[px][co] . im2col[px][k], both tiles
+// pixel-major and read through ds_read_b64_tr_b16; one fp32-atomic 64x64
+// partial per block.
+// ---------------------------------------------------------------------------
+constexpr int kStemPatchW = 2 * 256 + 8;       // bf16 columns of the 7-row input patch
+constexpr int kStemPatchPT = (7 * (2 * 256 + 6) + 255) / 256;  // patch values per thread (<= 15)
+
+struct StemPatch { float v[kStemPatchPT]; };
+
+// registers <- img rows 2*oh-3 .. 2*oh+3, cols -3 .. 2Q+2 (zero outside)
+__device__ __forceinline__ void stem_fetch(const float* img, int n, int oh, int H, int W, int Q, StemPatch& p) {
+  const int cols = 2 * Q + 6;
+#pragma unroll
+  for (int j = 0; j < kStemPatchPT; ++j) {
+    const int i = threadIdx.x + j * 256;
+    const int r = i / cols, c = i - r * cols;
+    const int ih = 2 * oh - 3 + r, iw = c - 3;
+    p.v[j] = (r < 7 && ih >= 0 && ih < H && iw >= 0 && iw < W) ? img[((size_t)n * H + ih) * W + iw] : 0.f;
+  }
+}
+__device__ __forceinline__ void stem_store_patch(const StemPatch& p, int Q, bf16_t* patch) {
+  const int cols = 2 * Q + 6;
+#pragma unroll
+  for (int j = 0; j < kStemPatchPT; ++j) {
+    const int i = threadIdx.x + j * 256;
+    const int r = i / cols, c = i - r * cols;
+    if (r < 7) patch[r * kStemPatchW + c] = f2bf(p.v[j]);
+  }
+}
+
+// im2col row of pixel px (k = kr*7+ks < 49, zero above) as 8 x 16 B
+__device__ __forceinline__ void stem_im2col_row(const bf16_t* patch, int px, uint4 (&row)[8]) {
+#pragma unroll
+  for (int c8 = 0; c8 < 8; ++c8) {
+    unsigned w[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      unsigned lo = 0, hi = 0;
+      const int k0 = c8 * 8 + 2 * h, k1 = k0 + 1;
+      if (k0 < 49) lo = patch[(k0 / 7) * kStemPatchW + 2 * px + (k0 % 7)];
+      if (k1 < 49) hi = patch[(k1 / 7) * kStemPatchW + 2 * px + (k1 % 7)];
+      w[h] = lo | (hi << 16);
+    }
+    row[c8] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+__global__ void __launch_bounds__(256, 2) stem_fwd_kernel(ConvFwdArgs a, int rows_per_block) {
+  // LDS: weights [64][64] (8 KB) | im2col [256][64] (32 KB) | patch 7 x 520 bf16
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Ws = smem;
+  char* Xs = smem + 64 * 128;
+  bf16_t* patch = reinterpret_cast<bf16_t*>(smem + 64 * 128 + 256 * 128);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float* img = reinterpret_cast<const float*>(a.x);
+  const int total_rows = a.N * a.P;
+  const int r0 = xcd_remap(blockIdx.x, gridDim.x) * rows_per_block;
+  const int r1 = min(total_rows, r0 + rows_per_block);
+  {  // packed weights [64][64] bf16 -> swizzled LDS rows
+    const uint4* wsrc = reinterpret_cast<const uint4*>(a.w);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int i = tid + j * 256, co = i >> 3, ch = i & 7;
+      *reinterpret_cast<uint4*>(Ws + frag_off<64>(co, ch)) = wsrc[i];
+    }
+  }
+  float q0[4][4], q1[4][4];  // per-lane BN sums of channels i*16 + 4*(lane>>4) + e
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) q0[i][e] = q1[i][e] = 0.f;
+  StemPatch pf;
+  if (r0 < r1) stem_fetch(img, r0 / a.P, r0 % a.P, a.H, a.W, a.Q, pf);
+  for (int row = r0; row < r1; ++row) {
+    __syncthreads();  // previous row's patch / im2col consumed
+    stem_store_patch(pf, a.Q, patch);
+    if (row + 1 < r1) stem_fetch(img, (row + 1) / a.P, (row + 1) % a.P, a.H, a.W, a.Q, pf);
+    __syncthreads();
+    {
+      uint4 r8[8];
+      if (tid < a.Q) {
+        stem_im2col_row(patch, tid, r8);
+      } else {
+#pragma unroll
+        for (int c8 = 0; c8 < 8; ++c8) r8[c8] = make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int c8 = 0; c8 < 8; ++c8) *reinterpret_cast<uint4*>(Xs + frag_off<64>(tid, c8)) = r8[c8];
+    }
+    __syncthreads();
+    // 4 waves x (64 px x 64 co): acc[co frag][px frag]
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = kk * 4 + (lane >> 4);
+      bf16x8 wf[4], xf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        wf[i] = *reinterpret_cast<const bf16x8*>(Ws + frag_off<64>(i * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        xf[j] = *reinterpret_cast<const bf16x8*>(Xs + frag_off<64>(wave * 64 + j * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
+    }
+    // bf16 NHWC stores (4 consecutive channels of one pixel per lane) + sums
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int px = wave * 64 + j * 16 + (lane & 15);
+      if (px < a.Q) {
+        bf16_t* yrow = a.y + ((size_t)row * a.Q + px) * a.ldy;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int co = i * 16 + ((lane >> 4) << 2);
+          uint2 o;
+          o.x = pack_bf2(acc[i][j][0], acc[i][j][1]);
+          o.y = pack_bf2(acc[i][j][2], acc[i][j][3]);
+          *reinterpret_cast<uint2*>(yrow + co) = o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { q0[i][e] += acc[i][j][e]; q1[i][e] += acc[i][j][e] * acc[i][j][e]; }
+        }
+      }
+    }
+  }
+  if (!a.stats) return;
+  // fold over the 16 pixel lanes, then the 4 waves, then one replica atomic per channel
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        q0[i][e] += __shfl_xor(q0[i][e], o, 64);
+        q1[i][e] += __shfl_xor(q1[i][e], o, 64);
+      }
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);  // [4 waves][64][2]
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = i * 16 + ((lane >> 4) << 2) + e;
+        red[(wave * 64 + c) * 2] = q0[i][e];
+        red[(wave * 64 + c) * 2 + 1] = q1[i][e];
+      }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) { s0 += red[(w * 64 + tid) * 2]; s1 += red[(w * 64 + tid) * 2 + 1]; }
+    double* rep = a.stats + (size_t)(blockIdx.x % kStatRep) * 2 * 64;
+    atomicAdd(rep + tid, (double)s0);
+    atomicAdd(rep + 64 + tid, (double)s1);
+  }
+  if (a.bn.ticket) {
+    int* flag = reinterpret_cast<int*>(smem + 4 * 64 * 2 * sizeof(float));
+    if (last_block_arrive(a.bn.ticket, gridDim.x, flag, tid < 64)) bn_finalize(a.bn);
+  }
+}
+
+__global__ void __launch_bounds__(256, 2) stem_wgrad_kernel(ConvWgradArgs a, int rows_per_block) {
+  // LDS: dY [256 px][64 co] | im2col [256 px][64 k] (pixel-major tr tiles) | patch
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  typedef TrTile<64, 64, 256> TT;
+  char* Ds = smem;
+  char* Xs = smem + 256 * 128;
+  bf16_t* patch = reinterpret_cast<bf16_t*>(smem + 2 * 256 * 128);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;  // 32 co x 32 k per wave
+  const int g = lane >> 4, li = lane & 15, trq = li >> 2, trp = li & 3;
+  const float* img = reinterpret_cast<const float*>(a.x);
+  const int total_rows = a.N * a.P;
+  const int r0 = xcd_remap(blockIdx.x, gridDim.x) * rows_per_block;
+  const int r1 = min(total_rows, r0 + rows_per_block);
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // register prefetch of the next row: dY (8 x 16 B per thread) + input patch
+  uint4 dyv[8];
+  StemPatch pf;
+  auto fetch = [&](int row) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = tid + j * 256, px = i >> 3, c8 = i & 7;
+      dyv[j] = px < a.Q ? *reinterpret_cast<const uint4*>(a.dy + ((size_t)row * a.Q + px) * a.lddy + c8 * 8)
+                        : make_uint4(0, 0, 0, 0);
+    }
+    stem_fetch(img, row / a.P, row % a.P, a.H, a.W, a.Q, pf);
+  };
+  if (r0 < r1) fetch(r0);
+  for (int row = r0; row < r1; ++row) {
+    __syncthreads();  // previous row's tiles consumed
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = tid + j * 256, px = i >> 3, c8 = i & 7;
+      *reinterpret_cast<uint4*>(Ds + TT::off(px, c8 * 8)) = dyv[j];
+    }
+    stem_store_patch(pf, a.Q, patch);
+    if (row + 1 < r1) fetch(row + 1);
+    __syncthreads();
+    {
+      uint4 r8[8];
+      if (tid < a.Q) {
+        stem_im2col_row(patch, tid, r8);
+      } else {
+#pragma unroll
+        for (int c8 = 0; c8 < 8; ++c8) r8[c8] = make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int c8 = 0; c8 < 8; ++c8) *reinterpret_cast<uint4*>(Xs + TT::off(tid, c8 * 8)) = r8[c8];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {  // 32 px per MFMA k-step
+      const int p_lo = kk * 32 + 8 * g + trq;
+      bf16x8 af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int col = wm * 32 + i * 16 + 4 * trp;
+        af[i] = tr_read8(Ds + TT::off(p_lo, col), Ds + TT::off(p_lo + 4, col));
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = wn * 32 + j * 16 + 4 * trp;
+        bf[j] = tr_read8(Xs + TT::off(p_lo, col), Xs + TT::off(p_lo + 4, col));
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  // D[co][k]: lane holds k = .. + li, co = .. + 4g + e;  dW row length 64
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = wn * 32 + j * 16 + li;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = wm * 32 + i * 16 + 4 * g + e;
+        atomicAdd(a.dw + co * 64 + k, acc[i][j][e]);
+      }
+    }
+}
+
+hipError_t launch_stem_fwd(const ConvFwdArgs& a, hipStream_t st) {
+  if (a.Cout != 64 || a.Q > 256 || a.R != 7 || a.stride != 2 || a.pad != 3) return hipErrorInvalidValue;
+  const int rows = a.N * a.P;
+  const int per = std::max(1, (rows + 511) / 512);  // ~2 blocks per CU
+  const size_t lds = 64 * 128 + 256 * 128 + 7 * kStemPatchW * 2;
+  set_kernel_tag("stem_fwd_kernel");
+  hipLaunchKernelGGL(stem_fwd_kernel, dim3((rows + per - 1) / per), dim3(256), lds, st, a, per);
+  return hipGetLastError();
+}
+
+hipError_t launch_stem_wgrad(const ConvWgradArgs& a, hipStream_t st) {
+  if (a.Cout != 64 || a.Q > 256 || a.R != 7 || a.stride != 2 || a.pad != 3) return hipErrorInvalidValue;
+  const int rows = a.N * a.P;
+  const int per = std::max(1, (rows + 511) / 512);  // ~2 blocks per CU
+  const size_t lds = 2 * 256 * 128 + 7 * kStemPatchW * 2;
+  set_kernel_tag("stem_wgrad_kernel");
+  hipLaunchKernelGGL(stem_wgrad_kernel, dim3((rows + per - 1) / per), dim3(256), lds, st, a, per);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
 // host-side launch selection
 // ---------------------------------------------------------------------------
-// template instance of the last conv launch ("name<args>", as rocprofv3 prints
-// the kernel symbol) for the per-launch profiler's kernel column
-static thread_local char g_kernel_tag[96];
-template <typename... T>
-static void set_kernel_tag(const char* fmt, T... v) {
-  std::snprintf(g_kernel_tag, sizeof(g_kernel_tag), fmt, v...);
-}
-const char* last_kernel_tag() { return g_kernel_tag; }
 
 template <int MODE, int ALOAD, int BM, int BN, int BK, int WM, int WN>
 static hipError_t launch_fwd_cfg(const ConvFwdArgs& a0, int classes, hipStream_t st) {
@@ -1026,6 +1352,7 @@ static bool g_use_glds = std::getenv("UNET_CONV_V1") == nullptr;  // A/B switch 
 void set_conv_impl(int glds) { g_use_glds = glds != 0; }
 
 hipError_t launch_conv_fwd(const ConvFwdArgs& a0, int mode, hipStream_t st) {
+  if (g_use_glds && mode == MODE_STEM) return launch_stem_fwd(a0, st);
   if (g_use_glds && mode != MODE_STEM && a0.C % 32 == 0) {
     ConvFwdArgs a = a0;
     if ((size_t)a.N * a.H * a.W * a.ldx * 2 >= 0x80000000ull) return hipErrorInvalidValue;
@@ -1101,33 +1428,64 @@ static hipError_t launch_wgrad_cfg(const ConvWgradArgs& a0, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <int TW>
+// split-K partials of the last halo wgrad launch, summed by launch_wgrad_finish
+struct PendingReduce { const float* slab; float* dw; int64_t n; int splits; };
+static thread_local PendingReduce g_pending{};
+
+// splits so that the grid is ~one block per CU (the halo kernels hold 96-144 KB
+// of LDS), at least one tile per split
+template <int TW, int CI>
+static void halo_geometry(const ConvWgradArgs& a, int& blocks_xy, int& tiles, int& per, int& splits) {
+  constexpr int TH = 128 / TW;
+  blocks_xy = ((a.Cout + 63) / 64) * (a.C / CI);
+  tiles = a.N * (a.P / TH) * (a.Q / TW);
+  splits = std::max(1, std::min(tiles, 256 / blocks_xy));
+  per = (tiles + splits - 1) / splits;
+  splits = (tiles + per - 1) / per;
+}
+
+template <int TW, int CI>
 static hipError_t launch_wgrad_halo(const ConvWgradArgs& a0, hipStream_t st) {
   ConvWgradArgs a = a0;
-  constexpr int TH = 128 / TW;
   a.co_blocks = (a.Cout + 63) / 64;
-  a.c_blocks = a.C / 32;
-  const int tiles = a.N * (a.P / TH) * (a.Q / TW);
-  const int blocks_xy = a.co_blocks * a.c_blocks;
-  int splits = (2048 + blocks_xy - 1) / blocks_xy;
-  // keep >= 8 tiles (1024 px) per block: ~1 KB of fp32 atomics per 1.2 MFLOP
-  splits = std::max(1, std::min(splits, tiles / 8));
-  const int per = (tiles + splits - 1) / splits;
-  splits = (tiles + per - 1) / per;
-  constexpr int NS = 3;
-  const size_t lds = (size_t)NS * (128 * 128 + 16 * 1024);
-  set_kernel_tag("wgrad3x3_halo_kernel<%d, %d>", TW, NS);
-  hipLaunchKernelGGL((wgrad3x3_halo_kernel<TW, NS>), dim3(blocks_xy, 1, splits), dim3(256), lds, st, a, tiles, per);
+  a.c_blocks = a.C / CI;
+  int blocks_xy, tiles, per, splits;
+  halo_geometry<TW, CI>(a, blocks_xy, tiles, per, splits);
+  const int64_t n = (int64_t)a.Cout * 9 * a.C;
+  if (a.slab && (size_t)splits * n * sizeof(float) > a.slab_bytes) a.slab = nullptr;  // atomics instead
+  constexpr int NS = CI == 64 ? 3 : 4;
+  const size_t lds = (size_t)NS * (128 * 128 + 256 * CI * 2);
+  set_kernel_tag("wgrad3x3_halo_kernel<%d, %d, %d>", TW, NS, CI);
+  hipLaunchKernelGGL((wgrad3x3_halo_kernel<TW, NS, CI>), dim3(blocks_xy, 1, splits), dim3(CI * 8), lds, st, a,
+                     tiles, per);
+  if (a.slab) g_pending = PendingReduce{a.slab, a.dw, n, splits};
+  return hipGetLastError();
+}
+
+bool wgrad_pending() { return g_pending.slab != nullptr; }
+
+hipError_t launch_wgrad_finish(hipStream_t st) {
+  if (!g_pending.slab) return hipSuccess;
+  const PendingReduce r = g_pending;
+  g_pending = PendingReduce{};
+  const int bx = (int)((r.n + 255) / 256);
+  const int G = (r.splits + 7) / 8;
+  set_kernel_tag("wgrad_slab_reduce_kernel");
+  hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3(bx, G), dim3(256), 0, st, r.slab, r.dw, r.n, r.splits);
   return hipGetLastError();
 }
 
 hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st) {
-  if (stem) return launch_wgrad_cfg<XLOAD_STEM, 64, 64, 64, 2, 2>(a, st);
+  if (stem) return g_use_glds ? launch_stem_wgrad(a, st) : launch_wgrad_cfg<XLOAD_STEM, 64, 64, 64, 2, 2>(a, st);
   if (g_use_glds && a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.C % 32 == 0 && a.P == a.H &&
       a.Q == a.W && (size_t)a.N * a.H * a.W * a.ldx * 2 < 0x80000000ull &&
       (size_t)a.N * a.P * a.Q * a.lddy * 2 < 0x80000000ull) {
-    if (a.Q % 32 == 0 && a.P % 4 == 0) return launch_wgrad_halo<32>(a, st);
-    if (a.Q % 16 == 0 && a.P % 8 == 0) return launch_wgrad_halo<16>(a, st);
+    if (a.C % 64 == 0) {
+      if (a.Q % 32 == 0 && a.P % 4 == 0) return launch_wgrad_halo<32, 64>(a, st);
+      if (a.Q % 16 == 0 && a.P % 8 == 0) return launch_wgrad_halo<16, 64>(a, st);
+    }
+    if (a.Q % 32 == 0 && a.P % 4 == 0) return launch_wgrad_halo<32, 32>(a, st);
+    if (a.Q % 16 == 0 && a.P % 8 == 0) return launch_wgrad_halo<16, 32>(a, st);
   }
   if (a.C % 32 || a.Cout % 32) return hipErrorInvalidValue;
   const bool co64 = a.Cout % 64 == 0, c64 = a.C % 64 == 0;

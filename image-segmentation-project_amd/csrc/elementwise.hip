@@ -357,6 +357,18 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(MaxPoolArgs a) {
 __global__ void __launch_bounds__(256) maxpool_bwd_kernel(MaxPoolArgs a) {
   const int CC = a.C >> 3;
   const int64_t total = (int64_t)a.N * a.H * a.W * CC;
+  const BnBwdArgs& bb = a.bb;
+  const bool fz = bb.sums != nullptr;  // launcher: 256 % CC == 0, so c8 is fixed per thread
+  float s1[8], s2[8], mu[8], is[8];
+  {
+    const int c8 = (int)((blockIdx.x * blockDim.x + threadIdx.x) % CC) << 3;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s1[k] = s2[k] = 0.f;
+      mu[k] = fz ? bb.mean[c8 + k] : 0.f;
+      is[k] = fz ? bb.invstd[c8 + k] : 0.f;
+    }
+  }
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t ipix = e / CC;
@@ -396,8 +408,41 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(MaxPoolArgs a) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc[k] += r[k];
     }
-    *reinterpret_cast<uint4*>(a.dx + ipix * a.lddx + c8) = pack8(acc);
+    if (fz) {
+      float av[8];
+      unpack8(*reinterpret_cast<const uint4*>(bb.act + ipix * bb.ldact + c8), av);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] = av[k] > 0.f ? acc[k] : 0.f;
+    }
+    const uint4 o = pack8(acc);
+    *reinterpret_cast<uint4*>(a.dx + ipix * a.lddx + c8) = o;
+    if (fz) {
+      float dz[8], y[8];
+      unpack8(o, dz);
+      unpack8(*reinterpret_cast<const uint4*>(bb.y + ipix * bb.ldy + c8), y);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { s1[k] += dz[k]; s2[k] += dz[k] * (y[k] - mu[k]) * is[k]; }
+    }
   }
+  if (!fz) return;
+  // fold the block's per-thread channel sums (thread t holds chunk t % CC)
+  __shared__ float red[256 * 8];
+  __shared__ int flag;
+  for (int q = 0; q < 2; ++q) {
+    const float* src = q == 0 ? s1 : s2;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[threadIdx.x * 8 + k] = src[k];
+    __syncthreads();
+    for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+      const int chunk = c >> 3, k = c & 7;
+      float acc = 0.f;
+      for (int t = chunk; t < (int)blockDim.x; t += CC) acc += red[t * 8 + k];
+      const size_t rep = (size_t)(blockIdx.x % kStatRep) * 2 * a.C;
+      atomicAdd(bb.sums + rep + q * a.C + c, (double)acc);
+    }
+    __syncthreads();
+  }
+  if (bb.ticket && last_block_arrive(bb.ticket, gridDim.x, &flag, (int)threadIdx.x < a.C)) bn_bwd_finalize(bb);
 }
 
 hipError_t launch_maxpool_fwd(const MaxPoolArgs& a, hipStream_t st) {
@@ -408,6 +453,7 @@ hipError_t launch_maxpool_fwd(const MaxPoolArgs& a, hipStream_t st) {
 }
 hipError_t launch_maxpool_bwd(const MaxPoolArgs& a, hipStream_t st) {
   if (a.C % 8) return hipErrorInvalidValue;
+  if (a.bb.sums && (256 % (a.C / 8) || a.bb.y2)) return hipErrorInvalidValue;
   const int64_t total = (int64_t)a.N * a.H * a.W * (a.C / 8);
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total, 256 * 2)), dim3(256), 0, st, a);
   return hipGetLastError();

@@ -94,6 +94,7 @@ struct unet_plan {
   size_t zero_fwd_off = 0, zero_fwd_bytes = 0;
   size_t zero_bwd_off = 0, zero_bwd_bytes = 0;
   size_t head_usum = 0;
+  size_t wslab = 0, wslab_bytes = 0;  // split-K partials of the halo weight-gradient kernel
   int64_t grad_numel = 0;
   std::vector<std::pair<int64_t, int64_t>> buckets;  // flat element ranges
   std::vector<std::vector<int>> bucket_convs;        // convs to unpack per bucket
@@ -129,12 +130,14 @@ struct ProfScope {
   ProfScope(unet_plan* p_, hipStream_t s, std::string n, double f) : p(p_), st(s), name(std::move(n)), flops(f) {
     if (p->prof) e0 = prof_event(p, st);
   }
-  ~ProfScope() {
+  void close() {
     if (p->prof && e0 >= 0) {
       const int e1 = prof_event(p, st);
       if (e1 >= 0) p->recs.push_back({name, flops, e0, e1, flops > 0 ? unet::last_kernel_tag() : ""});
     }
+    e0 = -1;
   }
+  ~ProfScope() { close(); }
 };
 }  // namespace
 
@@ -332,6 +335,9 @@ static int build_plan(unet_plan* p) {
   p->y0 = act(A, N, H2, W2, c0);
   p->p0 = act(A, N, H4, W4, c0);
   p->pidx = A.take((size_t)N * H4 * W4 * c0);
+  // <= ~256 blocks x (64 co x 64 ci x 9 taps) fp32 partials, or one whole dW
+  p->wslab_bytes = (size_t)40 << 20;
+  p->wslab = A.take(p->wslab_bytes);
   Act cats[4];  // cats[l] for decoder level index l (0 = level 4)
   cats[3] = cat1;
   cats[2] = act(A, N, H4, W4, 2 * c0);
@@ -586,6 +592,7 @@ int conv_wgrad(const Ctx& x, int ci, const Act& dy, const Act& in) {
   ConvWgradArgs a = {};
   a.N = x.p->cfg.N;
   a.dw = x.W<float>(cv.wacc);
+  a.slab = x.W<float>(x.p->wslab); a.slab_bytes = x.p->wslab_bytes;
   a.R = cv.R; a.S = cv.S; a.stride = cv.stride; a.pad = cv.pad;
   if (cv.kind == L_CONVT) {
     // view as conv of dY (input, stride 2) producing X: "dy" := X, "x" := dY
@@ -600,6 +607,11 @@ int conv_wgrad(const Ctx& x, int ci, const Act& dy, const Act& in) {
     a.P = dy.H; a.Q = dy.W; a.Cout = cv.Co;
   }
   CK(launch_conv_wgrad(a, 0, x.st));
+  ps.close();
+  if (wgrad_pending()) {
+    ProfScope pr(x.p, x.st, "wgrad_reduce " + pname(x, cv.w), 0);
+    CK(launch_wgrad_finish(x.st));
+  }
   return 0;
 }
 
@@ -878,13 +890,15 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     m.add = x.A(skip); m.ldadd = skip.ld;
     m.dx = x.A(p->d_x1); m.lddx = p->d_x1.ld;
     m.N = N; m.H = p->x1.H; m.W = p->x1.W; m.C = p->x1.C; m.P = p->p0.H; m.Q = p->p0.W;
+    // the maxpool backward produces dA of the stem BN: fuse its reduction
+    const BnBwdArgs sb = bwd_args(x, p->stem_bn, p->d_x1, p->x1, p->y0, p->d_y0, -1, nullptr, nullptr, nullptr,
+                                  grads);
+    if (fz) m.bb = sb;
     {
       ProfScope ps(p, st, "maxpool_bwd", 0);
       CK(launch_maxpool_bwd(m, st));
     }
-    RUN(bn_backward(x, p->stem_bn,
-                    bwd_args(x, p->stem_bn, p->d_x1, p->x1, p->y0, p->d_y0, -1, nullptr, nullptr, nullptr, grads),
-                    false));
+    RUN(bn_backward(x, p->stem_bn, sb, fz));
     const Conv& cv = p->convs[p->stem_conv];
     ConvWgradArgs a = {};
     a.dy = x.A(p->d_y0); a.lddy = p->d_y0.ld;

@@ -71,6 +71,7 @@ struct ConvWgradArgs {
   const bf16_t* dy; int lddy;    // gradient wrt conv output [N,P,Q,Cout]
   const bf16_t* x; int ldx;      // conv input [N,H,W,C] (stem: fp32 image)
   float* dw;                     // fp32 accumulator [Cout][R*S*C] (stem: [64][64])
+  float* slab; size_t slab_bytes; // optional split-K partial scratch (3x3 s1 halo path)
   int N, H, W, C, P, Q, Cout, R, S, stride, pad;
   int px_per_split, co_blocks, c_blocks;  // filled by the launcher
 };
@@ -80,6 +81,9 @@ hipError_t launch_conv_fwd_v1(const ConvFwdArgs& a, int mode, hipStream_t st);  
 void set_conv_impl(int glds);  // 1: LDS-DMA pipelined kernels (default), 0: register-staged v1
 void set_conv_config(int cfg);  // 0: automatic tile selection, >0: fixed tile config (tuning)
 hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st);
+// sums the split-K slab of the preceding launch_conv_wgrad into dW (no-op if it used atomics)
+hipError_t launch_wgrad_finish(hipStream_t st);
+bool wgrad_pending();
 const char* last_kernel_tag();  // template instance of the last conv launch (profiler)
 
 // ---- elementwise / reduction kernels (elementwise.hip) ----
@@ -101,6 +105,10 @@ struct MaxPoolArgs {
   const bf16_t* x; int ldx; bf16_t* y; int ldy; uint8_t* idx;
   const bf16_t* dy; int lddy; const bf16_t* add; int ldadd; bf16_t* dx; int lddx;
   int N, H, W, C, P, Q;
+  // backward only, optional: dx is dA of a BN(+ReLU) (the stem BN); as in the
+  // conv-dgrad epilogue, store dZ = dA * (act > 0) and run its BN-backward
+  // reduction (bb.sums != null)
+  BnBwdArgs bb;
 };
 hipError_t launch_maxpool_fwd(const MaxPoolArgs& a, hipStream_t st);
 hipError_t launch_maxpool_bwd(const MaxPoolArgs& a, hipStream_t st);

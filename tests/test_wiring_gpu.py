@@ -217,7 +217,7 @@ def test_backward_ops(run):
     # maxpool + stem
     x1 = v["x1"].clone().requires_grad_(True)
     F.max_pool2d(x1, 3, 2, 1).backward(v["d.p0"])
-    rows.append(("d.x1", _rel(v["d.x1"], x1.grad + v["dec1.d.cat"][:, :64])))
+    rows.append(("d.x1", _masked(v["d.x1"], x1.grad + v["dec1.d.cat"][:, :64], v["x1"])))
     dy0, dg, db = local_bn_bwd(v["y0"], v["d.x1"], ref.bn1, out=v["x1"])
     rows += [("d.y0", _rel(v["d.y0"], dy0)), ("g bn1.weight", _rel(grads["bn1.weight"], dg)),
              ("g bn1.bias", _rel(grads["bn1.bias"], db))]
