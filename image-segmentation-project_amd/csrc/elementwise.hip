@@ -6,12 +6,18 @@
 // wave instruction moves 1 KiB; per-channel reductions are kept in registers
 // per thread (each thread owns one 8-channel chunk for its whole pixel loop),
 // folded through LDS once per block and published with fp64 atomics.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
 namespace unet {
 
 constexpr float kMaskThreshold = 8.94069742685133e-08f;  // 0x33C00001, SURVEY.md §0
+
+// grid cap of the BN apply kernels (each block recomputes the per-channel
+// coefficients in its prologue; fewer, longer blocks amortise that)
+static int g_apply_cap = std::getenv("UNET_APPLY_CAP") ? std::atoi(std::getenv("UNET_APPLY_CAP")) : 4096;
 
 static inline int grid_for(int64_t work, int per_block, int cap = 2048) {
   int64_t g = (work + per_block - 1) / per_block;
@@ -124,7 +130,7 @@ static inline dim3 chunk_block(int C) {
 hipError_t launch_bn_apply(const BnApplyArgs& a, hipStream_t st) {
   if (a.C % 8 || a.C / 8 > 256) return hipErrorInvalidValue;
   const int rows = 256 / (a.C / 8);
-  const int g = grid_for(a.npix, rows * 4, 4096);
+  const int g = grid_for(a.npix, rows * 4, g_apply_cap);
   hipLaunchKernelGGL(bn_apply_kernel, dim3(g), chunk_block(a.C), 4 * a.C * sizeof(float), st, a);
   return hipGetLastError();
 }
@@ -306,7 +312,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, double i
 hipError_t launch_bn_bwd_apply(const BnBwdArgs& a, hipStream_t st) {
   if (a.C % 8 || a.C / 8 > 256) return hipErrorInvalidValue;
   const int rows = 256 / (a.C / 8);
-  const int g = grid_for(a.npix, rows * 4, 4096);
+  const int g = grid_for(a.npix, rows * 4, g_apply_cap);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(g), chunk_block(a.C), 9 * a.C * sizeof(float), st, a,
                      1.0 / (double)a.npix);
   return hipGetLastError();
