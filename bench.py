@@ -74,6 +74,8 @@ def main():
     ap.add_argument("--graph", dest="graph", action="store_true", default=None,
                     help="replay the step as one HIP graph (default for --gpus 1)")
     ap.add_argument("--no-graph", dest="graph", action="store_false")
+    ap.add_argument("--torch-adam", action="store_true",
+                    help="torch.optim.Adam (foreach) instead of the fused HIP Adam (optim.py)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -91,7 +93,11 @@ def main():
     if world > 1:
         ddp.enable_data_parallel(model)
     use_graph = args.graph if args.graph is not None else world == 1
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-5, capturable=use_graph)
+    if args.torch_adam:
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-5, capturable=use_graph)
+    else:
+        opt = importlib.import_module("image-segmentation-project_amd.optim").Adam(
+            model.parameters(), lr=1e-3, weight_decay=1e-5)
     crit = pkg.get_loss_function({"loss_fn": "bce"})
     xs, ms = pkg.synthetic_cells(args.batch, args.size, args.size, seed=1234 + rank)
     x = torch.from_numpy(xs).to(dev)
@@ -184,6 +190,7 @@ def main():
                      "step_tflops": round(step_tflops, 2),
                      "step_frac": round(step_tflops / MFMA_BF16_PEAK_TFLOPS, 4)},
         "graph": bool(use_graph),
+        "optimizer": "torch.optim.Adam (foreach)" if args.torch_adam else "fused HIP Adam (unet_adam_step)",
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.batch, args.size, args.cpu_steps, args.cpu_threads)

@@ -15,6 +15,8 @@ from .train import (evaluate, quick_train, train_epoch, train_model, TensorLoade
                     GraphedTrainStep)
 from .synthetic import random_batch, synthetic_cells  # noqa: F401
 from . import ddp  # noqa: F401
+from . import optim  # noqa: F401
+from .optim import Adam  # noqa: F401
 from .ddp import enable_data_parallel  # noqa: F401
 from ._lib import LIB_PATH  # noqa: F401
 

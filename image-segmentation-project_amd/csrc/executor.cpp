@@ -1076,6 +1076,17 @@ int unet_mask_metrics(const float* values, const float* target, int64_t n, int v
   return 0;
 }
 
+int unet_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, float* step_coef,
+                   int64_t n, float lr, float beta1, float beta2, float eps, float weight_decay,
+                   int advance_step, hipStream_t stream) {
+  if (n < 0 || (n > 0 && (!params || !grads || !exp_avg || !exp_avg_sq)) || !step_coef) {
+    set_err("unet_adam_step: null buffer or negative size");
+    return 1;
+  }
+  CK(launch_adam(params, grads, exp_avg, exp_avg_sq, n, step_coef, lr, beta1, beta2, eps, weight_decay, advance_step, stream));
+  return 0;
+}
+
 int unet_conv_fwd(const void* x, int ldx, const void* w, void* y, int ldy, const float* bias, const void* addend,
                   int ldadd, double* stats, int N, int H, int W, int C, int P, int Q, int Cout, int R, int S,
                   int stride, int pad, int mode, hipStream_t stream) {

@@ -157,4 +157,8 @@ hipError_t launch_loss_grad(const float* logits, const float* target, int64_t n,
                             int kind, float alpha, float smooth, const float* gscale, float* dl,
                             hipStream_t st);
 
+// fused Adam over flat fp32 buffers (optim.hip); coef = {step, step_size, sqrt(bc2)} on device
+hipError_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float* coef, float lr,
+                       float beta1, float beta2, float eps, float wd, int advance_step, hipStream_t st);
+
 }  // namespace unet

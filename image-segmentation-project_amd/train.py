@@ -88,7 +88,10 @@ class GraphedTrainStep:
     captured into a single HIP graph and replayed: removes the per-launch host
     cost of the ~250 kernels of a step.  Inputs are static device tensors; pass
     new batches through ``__call__`` (copied in before replay).  The optimizer
-    must be capturable (``torch.optim.Adam(..., capturable=True)``)."""
+    must be capturable (``optim.Adam``, or ``torch.optim.Adam(..., capturable=True)``).
+    Drop every reference to an earlier eager step's loss/outputs before building
+    one: a live autograd graph keeps AccumulateGrad nodes bound to the stream
+    they were created on, and HIP stream capture aborts on them."""
 
     def __init__(self, model, criterion, optimizer, images, masks, warmup: int = 3):
         self.model, self.criterion, self.optimizer = model, criterion, optimizer
@@ -105,7 +108,10 @@ class GraphedTrainStep:
         torch.cuda.current_stream().wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            self.out, self.loss = self._step()
+            out, loss = self._step()
+        # replay rewrites these buffers in place; detached, they do not keep the
+        # captured step's autograd graph alive
+        self.out, self.loss = out.detach(), loss.detach()
 
     def _step(self):
         out = self.model(self.x)
@@ -195,14 +201,15 @@ def train_model(model, train_images, train_masks, val_images, val_masks, criteri
 
 def quick_train(model, train_images, train_masks, val_images, val_masks, config: Dict, device=None,
                 augmentations_per_image: int = 0) -> Dict:
-    """train.py:301-364: Adam (coupled L2) + ReduceLROnPlateau(max, 0.5, thr 0.01, min 1e-6)."""
+    """train.py:301-364: Adam (coupled L2; the fused HIP Adam of optim.py) + ReduceLROnPlateau(max, 0.5, thr 0.01, min 1e-6)."""
     from .losses import get_loss_function
+    from .optim import Adam
     from .utils import get_device
     device = device or get_device()
     model = model.to(device)
     criterion = get_loss_function(config)
-    optimizer = torch.optim.Adam(model.parameters(), lr=config.get("learning_rate", 1e-3),
-                                 weight_decay=config.get("weight_decay", 1e-5))
+    optimizer = Adam(model.parameters(), lr=config.get("learning_rate", 1e-3),
+                     weight_decay=config.get("weight_decay", 1e-5))
     scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optimizer, mode="max", factor=0.5,
                                                            patience=config.get("scheduler_patience", 3),
                                                            threshold=0.01, min_lr=1e-6)

@@ -13,6 +13,8 @@
  *   unet_loss_forward    BCELoss / DiceLoss / ComboLoss forward (losses.py:13-37,161-171)
  *   unet_loss_backward   their gradient wrt the logits
  *   unet_mask_metrics    calculate_metrics tp/fp/fn/tn counts (utils.py:120-151)
+ *   unet_adam_step       optimizer.step() of torch.optim.Adam(model.parameters(),
+ *                        lr, weight_decay) (train.py:49,331-335)
  *   unet_conv_* / unet_maxpool_* / unet_bn_*   single ops of the graph above
  *                        (torchvision BasicBlock, advanced_models.py:197-205) for tests
  *
@@ -89,6 +91,18 @@ int unet_loss_backward(const float* logits, const float* target, int64_t n, int 
  * evaluated bit-exactly as logit >= 0x33C00001); 1: probabilities (p > 0.5). */
 int unet_mask_metrics(const float* values, const float* target, int64_t n, int values_are_prob,
                       double* sums8, hipStream_t stream);
+
+/* ---- optimizer ---- */
+/* One Adam step (coupled L2 weight decay, torch.optim.Adam semantics) over n
+ * fp32 elements of four flat buffers.  step_coef[3] is device memory:
+ * step_coef[0] is the step count (incremented on device, so the call is
+ * graph-capturable) when advance_step != 0, and [1], [2] then receive
+ * step_size = lr/(1-b1^t) and sqrt(1-b2^t); advance_step = 0 reuses them
+ * (several slices updated in one optimizer step).  exp_avg / exp_avg_sq must
+ * be zero before the first step. */
+int unet_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, float* step_coef,
+                   int64_t n, float lr, float beta1, float beta2, float eps, float weight_decay,
+                   int advance_step, hipStream_t stream);
 
 /* ---- single ops (tests / custom graphs) ---- */
 /* mode 0: conv  y = conv(x, w) [stride, pad]           (w packed [Cout][R][S][C])
