@@ -34,6 +34,25 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
                     pack_bf2(f[6], f[7]));
 }
 
+// ---- LDS-DMA staging (buffer_load ... lds): lane l of one wave instruction
+// writes 16 B at lds_wave_base + 16*l; an offset >= num_records (kOOB) reads
+// as zeros (conv padding, tile tails) ----
+constexpr unsigned kOOB = 0x80000000u;
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, char* lds_wave_base, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, 0,
+                                           0, 0);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

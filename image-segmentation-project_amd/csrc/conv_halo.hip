@@ -1,0 +1,320 @@
+// Weight-stationary halo convolution for the 3x3 / stride-1 / pad-1 layers
+// with few channels (SURVEY.md §8(a) rows a3 enc1 BasicBlocks and a6
+// decoder1/decoder2 blocks: C <= 96 input and <= 128 output channels at 128^2
+// and 256^2).  Forward conv and its data gradient (FLIP: the transposed
+// gather of s1 p1 is the same stencil with the taps mirrored, on the dgrad
+// weight pack [Cin][R][S][Cout]).
+//
+// The implicit-GEMM kernel (conv_kernels.hip) re-fetches every input pixel
+// once per tap and per output tile, and at K = 9*C <= 864 its k-loop is only
+// 9..27 steps long, so its pipeline never reaches steady state.  Here a
+// persistent block keeps ALL 9 taps of its COT output channels in LDS
+// (<= 74 KB, loaded once) and streams TH x 16 output-pixel tiles through a
+// double-buffered LDS halo of (TH+2) x 18 input pixels: each input byte
+// crosses L2 -> LDS ~1.3 times instead of 9, the next tile's halo (LDS-DMA,
+// buffer_load ... lds) lands while the current one is computed, and the
+// BN-statistics epilogue is reduced once per block instead of once per tile.
+//
+// LDS images are panels of 32 channels = 64-B rows (a halo pixel or a weight
+// row).  An MFMA operand fragment reads 16 CONSECUTIVE rows starting at an
+// arbitrary row (tap shift); with the 16-B chunk XOR-swizzled by bit 2 of the
+// row (chunk ^ ((row >> 1) & 2)) every ds_read_b128 lane group hits 16
+// distinct bank slots for every start row (exhaustively checked for the
+// gfx950 lane grouping {0-3,12-15,20-27}, ...).  The swizzle is applied on
+// the DMA source side (cdna_hip_programming.md §5.4 rule 21).
+//
+// GEMM view per tile: D[co][px] += W[co][(tap, c)] . X[px + shift(tap)][c],
+// v_mfma_f32_16x16x32_bf16 with A = weight fragment (16 co x 32 c), B = halo
+// fragment (16 px of one output row x 32 c); each wave owns RW output rows x
+// COT channels (acc[RW][FN]).
+#include <cstdio>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace unet {
+
+void conv_kernel_tag(const char* tag);  // conv_kernels.hip: per-launch profiler column
+
+__device__ __forceinline__ int ws_off(int row, int chunk) {  // byte offset of (row, logical 16-B chunk)
+  return row * 64 + ((chunk ^ ((row >> 1) & 2)) << 4);
+}
+
+template <int NP, int FN, int TH, int NW, bool FLIP>
+__global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int ntiles, int ncg) {
+  constexpr int COT = FN * 16;               // output channels per block
+  constexpr int RW = TH / NW;                // output rows per wave
+  constexpr int HWD = 18;                    // halo width (16 + 2)
+  constexpr int HP = (TH + 2) * HWD;         // halo pixels
+  constexpr int HPR = (HP + 15) / 16 * 16;   // rows per panel (16 rows per DMA instruction)
+  constexpr int PANEL = HPR * 64;
+  constexpr int HBUF = NP * PANEL;
+  constexpr int WBYTES = 9 * NP * COT * 64;
+  constexpr int H_INS = NP * HPR / 16;
+  constexpr int W_INS = 9 * NP * COT / 16;
+  constexpr int CIN = NP * 32;
+  static_assert(TH % NW == 0 && RW >= 1, "rows per wave");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* wl = smem;
+  char* hl = smem + WBYTES;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cg = blockIdx.x % ncg;
+  const int nslot = gridDim.x / ncg;
+  const int co0 = cg * COT;
+  const int tq = a.Q >> 4, tp = a.P / TH;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (unsigned)((size_t)a.Cout * 9 * CIN * 2));
+
+  // ---- all 9 taps of this block's output channels, once: [tap][panel][co][32 c]
+  for (int ins = wave; ins < W_INS; ins += NW) {
+    const int rowg = ins * 16 + (lane >> 2);
+    const int co = rowg % COT, tpn = rowg / COT;
+    const int p = tpn % NP, tap = tpn / NP;
+    const int lchunk = (lane & 3) ^ ((co >> 1) & 2);
+    unsigned off = kOOB;
+    if (co0 + co < a.Cout) off = (unsigned)(((co0 + co) * 9 * CIN + tap * CIN + p * 32 + lchunk * 8) * 2);
+    glds16(wr, wl + ins * 1024, off);
+  }
+
+  auto issue_halo = [&](int t, int b) {
+    const int n = t / (tp * tq);
+    const int rem = t - n * (tp * tq);
+    const int oh0 = (rem / tq) * TH, ow0 = (rem % tq) << 4;
+    for (int ins = wave; ins < H_INS; ins += NW) {
+      const int rowg = ins * 16 + (lane >> 2);
+      const int p = rowg / HPR, hp = rowg - p * HPR;
+      const int lchunk = (lane & 3) ^ ((hp >> 1) & 2);
+      const int hr = hp / HWD, hc = hp - hr * HWD;
+      const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
+      unsigned off = kOOB;
+      if (hp < HP && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+        off = (unsigned)((((n * a.H + ih) * a.W + iw) * a.ldx + p * 32 + lchunk * 8) * 2);
+      glds16(xr, hl + b * HBUF + ins * 1024, off);
+    }
+  };
+
+  // ---- epilogue constants (bias, BN mean / invstd of the fused backward) in
+  // LDS behind the halo buffers; the BN sums are the only registers kept
+  // across tiles
+  const BnBwdArgs& bb = a.bb;
+  const bool fbwd = bb.sums != nullptr;
+  const bool stats = a.stats != nullptr || fbwd;
+  float* cst = reinterpret_cast<float*>(hl + 2 * HBUF);  // [3][COT]
+  for (int c = tid; c < COT; c += NW * 64) {
+    const int co = co0 + c;
+    const bool ok = co < a.Cout;
+    cst[c] = (a.bias && ok) ? a.bias[co] : 0.f;
+    cst[COT + c] = (fbwd && ok) ? bb.mean[co] : 0.f;
+    cst[2 * COT + c] = (fbwd && ok) ? bb.invstd[co] : 0.f;
+  }
+  float q0[FN][4], q1[FN][4];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) q0[i][e] = q1[i][e] = 0.f;
+
+  int t = blockIdx.x / ncg;
+  if (t < ntiles) issue_halo(t, 0);
+  wait_vmcnt<0>();
+  __syncthreads();
+
+  for (int k = 0; t < ntiles; ++k, t += nslot) {
+    const int b = k & 1;
+    if (t + nslot < ntiles) issue_halo(t + nslot, b ^ 1);  // lands while this tile computes
+    const int n = t / (tp * tq);
+    const int rem = t - n * (tp * tq);
+    const int oh0 = (rem / tq) * TH, ow0 = (rem % tq) << 4;
+    size_t pix[RW];
+#pragma unroll
+    for (int j = 0; j < RW; ++j) pix[j] = ((size_t)n * a.P + oh0 + wave * RW + j) * a.Q + ow0 + (lane & 15);
+    // per-pixel epilogue operands of this tile, fetched now so their latency
+    // hides behind the MFMA loop (dgrad only: the forward has none)
+    uint2 uadd[RW][FN], uact[RW][FN], uy[RW][FN];
+    if (FLIP) {
+#pragma unroll
+      for (int j = 0; j < RW; ++j)
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+          const int co = min(co0 + i * 16 + ((lane >> 4) << 2), a.Cout - 4);
+          uadd[j][i] = a.add ? *reinterpret_cast<const uint2*>(a.add + pix[j] * a.ldadd + co) : make_uint2(0, 0);
+          uact[j][i] = fbwd ? *reinterpret_cast<const uint2*>(bb.act + pix[j] * bb.ldact + co) : make_uint2(0, 0);
+          uy[j][i] = fbwd ? *reinterpret_cast<const uint2*>(bb.y + pix[j] * bb.ldy + co) : make_uint2(0, 0);
+        }
+    }
+    const char* H = hl + b * HBUF;
+    f32x4 acc[RW][FN];
+#pragma unroll
+    for (int j = 0; j < RW; ++j)
+#pragma unroll
+      for (int i = 0; i < FN; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+#pragma unroll 1
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const int tap = r * 3 + s;
+          bf16x8 A[FN];
+#pragma unroll
+          for (int i = 0; i < FN; ++i)
+            A[i] = *reinterpret_cast<const bf16x8*>(wl + (tap * NP + p) * COT * 64 +
+                                                     ws_off(i * 16 + (lane & 15), lane >> 4));
+          const int dr = FLIP ? 2 - r : r, ds = FLIP ? 2 - s : s;
+#pragma unroll
+          for (int j = 0; j < RW; ++j) {
+            const int hp = (wave * RW + j + dr) * HWD + ds + (lane & 15);
+            const bf16x8 B = *reinterpret_cast<const bf16x8*>(H + p * PANEL + ws_off(hp, lane >> 4));
+#pragma unroll
+            for (int i = 0; i < FN; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B, acc[j][i], 0, 0, 0);
+          }
+        }
+
+    // ---- tile epilogue: bias, addend, ReLU mask (fused BN backward), bf16 store, sums
+#pragma unroll
+    for (int j = 0; j < RW; ++j) {
+#pragma unroll
+      for (int i = 0; i < FN; ++i) {
+        const int cl = i * 16 + ((lane >> 4) << 2);
+        const int co = co0 + cl;
+        if (co >= a.Cout) continue;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[j][i][e] + cst[cl + e];
+        if (FLIP) {
+          const uint2 u = uadd[j][i], m = uact[j][i];
+          v[0] += __uint_as_float(u.x << 16); v[1] += __uint_as_float(u.x & 0xffff0000u);
+          v[2] += __uint_as_float(u.y << 16); v[3] += __uint_as_float(u.y & 0xffff0000u);
+          if (fbwd) {
+            if (!(__uint_as_float(m.x << 16) > 0.f)) v[0] = 0.f;
+            if (!(__uint_as_float(m.x & 0xffff0000u) > 0.f)) v[1] = 0.f;
+            if (!(__uint_as_float(m.y << 16) > 0.f)) v[2] = 0.f;
+            if (!(__uint_as_float(m.y & 0xffff0000u) > 0.f)) v[3] = 0.f;
+          }
+        }
+        uint2 o;
+        o.x = pack_bf2(v[0], v[1]);
+        o.y = pack_bf2(v[2], v[3]);
+        *reinterpret_cast<uint2*>(a.y + pix[j] * a.ldy + co) = o;
+        if (FLIP && fbwd) {
+          const float dz[4] = {__uint_as_float(o.x << 16), __uint_as_float(o.x & 0xffff0000u),
+                               __uint_as_float(o.y << 16), __uint_as_float(o.y & 0xffff0000u)};
+          const uint2 u = uy[j][i];
+          const float yv[4] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                               __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            q0[i][e] += dz[e];
+            q1[i][e] += dz[e] * (yv[e] - cst[COT + cl + e]) * cst[2 * COT + cl + e];
+          }
+        } else if (stats) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { q0[i][e] += v[e]; q1[i][e] += v[e] * v[e]; }
+        }
+      }
+    }
+    wait_vmcnt<0>();               // the next tile's halo has landed (this wave's part)
+    __builtin_amdgcn_s_barrier();  // ... everyone's part; buffer b is free for reuse
+  }
+  if (!stats) return;
+
+  // ---- block reduction of the BN sums: 16 pixel lanes, then the NW waves
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        q0[i][e] += __shfl_xor(q0[i][e], o, 64);
+        q1[i][e] += __shfl_xor(q1[i][e], o, 64);
+      }
+  float* red = reinterpret_cast<float*>(smem);  // [NW][COT][2]; all LDS reads above are done
+  __syncthreads();
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int cl = i * 16 + ((lane >> 4) << 2) + e;
+        red[(wave * COT + cl) * 2 + 0] = q0[i][e];
+        red[(wave * COT + cl) * 2 + 1] = q1[i][e];
+      }
+  }
+  __syncthreads();
+  for (int cl = tid; cl < COT; cl += NW * 64) {
+    const int co = co0 + cl;
+    if (co < a.Cout) {
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        s0 += red[(w * COT + cl) * 2];
+        s1 += red[(w * COT + cl) * 2 + 1];
+      }
+      const size_t rep = (size_t)(blockIdx.x % kStatRep) * 2 * a.Cout;
+      double* dst = fbwd ? bb.sums + rep : a.stats + rep;
+      atomicAdd(dst + co, (double)s0);
+      atomicAdd(dst + a.Cout + co, (double)s1);
+    }
+  }
+  unsigned* ticket = fbwd ? bb.ticket : a.bn.ticket;
+  if (ticket) {
+    int* flag = reinterpret_cast<int*>(smem + NW * COT * 2 * sizeof(float));
+    if (last_block_arrive(ticket, gridDim.x, flag, tid < COT)) {
+      if (fbwd) bn_bwd_finalize(bb);
+      else bn_finalize(a.bn);
+    }
+  }
+}
+
+template <int NP, int FN, int TH, int NW, bool FLIP>
+static hipError_t launch_ws(const ConvFwdArgs& a, hipStream_t st) {
+  constexpr int COT = FN * 16;
+  constexpr int HPR = ((TH + 2) * 18 + 15) / 16 * 16;
+  constexpr size_t lds = (size_t)9 * NP * COT * 64 + 2 * (size_t)NP * HPR * 64 + 3 * COT * sizeof(float);
+  static_assert(lds <= 163840, "LDS");
+  const int ncg = (a.Cout + COT - 1) / COT;
+  const int ntiles = a.N * (a.P / TH) * (a.Q / 16);
+  const int per_cu = 163840 / (int)lds >= 2 ? 2 : 1;  // resident blocks per CU (LDS-limited)
+  int slots = 256 * per_cu / ncg;
+  if (slots > ntiles) slots = ntiles;
+  if (slots < 1) slots = 1;
+  char tag[96];
+  std::snprintf(tag, sizeof(tag), "conv3x3_ws_kernel<%d, %d, %d, %d, %s>", NP, FN, TH, NW, FLIP ? "true" : "false");
+  conv_kernel_tag(tag);
+  hipLaunchKernelGGL((conv3x3_ws_kernel<NP, FN, TH, NW, FLIP>), dim3(slots * ncg), dim3(NW * 64), lds, st, a,
+                     ntiles, ncg);
+  return hipGetLastError();
+}
+
+template <bool FLIP>
+static hipError_t launch_ws_shape(const ConvFwdArgs& a, hipStream_t st) {
+  const int C = a.C, Co = a.Cout;
+  if (C == 64 && Co % 64 == 0 && a.P % 16 == 0) return launch_ws<2, 4, 16, 8, FLIP>(a, st);
+  if (C == 32 && Co == 32 && a.P % 16 == 0) return launch_ws<1, 2, 16, 4, FLIP>(a, st);
+  if (C == 32 && Co == 96 && a.P % 16 == 0) return launch_ws<1, 6, 16, 8, FLIP>(a, st);
+  if (C == 32 && Co % 64 == 0 && a.P % 16 == 0) return launch_ws<1, 4, 16, 8, FLIP>(a, st);
+  if (C == 96 && Co == 32 && a.P % 8 == 0) return launch_ws<3, 2, 8, 4, FLIP>(a, st);
+  return hipErrorNotSupported;
+}
+
+static int g_ws_disabled = std::getenv("UNET_NO_WS") != nullptr;  // A/B switch for measurements
+void set_conv_ws(int on) { g_ws_disabled = on ? 0 : 1; }
+
+// 3x3 / s1 / p1 conv (mode 0) or its data gradient (mode 1, dgrad weight pack)
+// when the shape is covered; hipErrorNotSupported otherwise (the caller falls
+// back to the implicit-GEMM kernel).
+hipError_t launch_conv3x3_ws(const ConvFwdArgs& a, int mode, hipStream_t st) {
+  if (g_ws_disabled) return hipErrorNotSupported;
+  if (a.R != 3 || a.S != 3 || a.stride != 1 || a.pad != 1) return hipErrorNotSupported;
+  if (a.H != a.P || a.W != a.Q || a.Q % 16 || a.ldx % 8 || a.ldy % 4) return hipErrorNotSupported;
+  // no second BN (downsample) in the fused backward epilogue: those layers
+  // are never 3x3 s1 with <= 96 channels
+  if ((a.add && a.ldadd % 4) || (a.bb.sums && (a.bb.y2 || a.bb.ldact % 4 || a.bb.ldy % 4)))
+    return hipErrorNotSupported;
+  if ((size_t)a.N * a.H * a.W * a.ldx * 2 >= 0x80000000ull) return hipErrorNotSupported;
+  if (mode == 0 && (a.add || a.bb.sums)) return hipErrorNotSupported;  // forward epilogue: bias + BN sums only
+  return mode == 0 ? launch_ws_shape<false>(a, st) : launch_ws_shape<true>(a, st);
+}
+
+}  // namespace unet

@@ -37,6 +37,7 @@ static void set_kernel_tag(const char* fmt, T... v) {
   std::snprintf(g_kernel_tag, sizeof(g_kernel_tag), fmt, v...);
 }
 static void set_kernel_tag(const char* tag) { std::snprintf(g_kernel_tag, sizeof(g_kernel_tag), "%s", tag); }
+void conv_kernel_tag(const char* tag) { set_kernel_tag(tag); }
 const char* last_kernel_tag() { return g_kernel_tag; }
 
 // ---------------------------------------------------------------------------
@@ -423,21 +424,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x4 (&acc)
 // s_barrier (never __syncthreads inside the loop: its vmcnt(0) would drain
 // the pipeline).
 // ---------------------------------------------------------------------------
-constexpr unsigned kOOB = 0x80000000u;
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
-}
-
-__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, char* lds_wave_base, unsigned voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, 0,
-                                           0, 0);
-}
+// kOOB, wait_vmcnt, make_rsrc, glds16: common.h
 
 template <int BK>
 __device__ __forceinline__ int swz_chunk(int row, int p) {  // physical slot p -> logical chunk (involution)
@@ -1356,6 +1343,10 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a0, int mode, hipStream_t st) {
   if (g_use_glds && mode != MODE_STEM && a0.C % 32 == 0) {
     ConvFwdArgs a = a0;
     if ((size_t)a.N * a.H * a.W * a.ldx * 2 >= 0x80000000ull) return hipErrorInvalidValue;
+    if (g_cfg_override <= 0) {
+      const hipError_t e = launch_conv3x3_ws(a, mode == MODE_TRANS ? 1 : 0, st);
+      if (e != hipErrorNotSupported) return e;
+    }
     if (mode == MODE_TRANS) {
       if (a.P % a.stride || a.Q % a.stride) return hipErrorInvalidValue;
       a.Pc = a.P / a.stride;

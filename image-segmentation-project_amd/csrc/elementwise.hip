@@ -84,35 +84,45 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(BnApplyArgs a) {
     sc2[k] = a.res_mode == 2 ? coef[2 * a.C + c8 + k] : 0.f;
     sh2[k] = a.res_mode == 2 ? coef[3 * a.C + c8 + k] : 0.f;
   }
-  auto one = [&](int64_t pix) {
-    float v[8];
-    unpack8(*reinterpret_cast<const uint4*>(a.y + pix * a.ldy + c8), v);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = v[k] * sc1[k] + sh1[k];
-    if (a.res_mode) {
-      float r[8];
-      unpack8(*reinterpret_cast<const uint4*>(a.res + pix * a.ldr + c8), r);
-      if (a.res_mode == 2) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) r[k] = r[k] * sc2[k] + sh2[k];
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] += r[k];
-    }
-    if (a.relu) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
-    }
-    *reinterpret_cast<uint4*>(a.out + pix * a.ldo + c8) = pack8(v);
-  };
+  // PPT pixels per thread per pass, every load issued before any is consumed
+  // (out may alias nothing the loads read, but the compiler cannot know that)
+  constexpr int PPT = 4;
   if (row < rows) {
     const int64_t stride = (int64_t)gridDim.x * rows;
-    int64_t pix = (int64_t)blockIdx.x * rows + row;
-    for (; pix + stride < a.npix; pix += 2 * stride) {
-      one(pix);
-      one(pix + stride);
+    for (int64_t base = (int64_t)blockIdx.x * rows + row; base < a.npix; base += PPT * stride) {
+      uint4 uy[PPT], ur[PPT];
+#pragma unroll
+      for (int u = 0; u < PPT; ++u) {
+        const int64_t pix = base + u * stride;
+        uy[u] = pix < a.npix ? *reinterpret_cast<const uint4*>(a.y + pix * a.ldy + c8) : make_uint4(0, 0, 0, 0);
+        ur[u] = (a.res_mode && pix < a.npix) ? *reinterpret_cast<const uint4*>(a.res + pix * a.ldr + c8)
+                                             : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < PPT; ++u) {
+        const int64_t pix = base + u * stride;
+        if (pix >= a.npix) break;
+        float v[8];
+        unpack8(uy[u], v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = v[k] * sc1[k] + sh1[k];
+        if (a.res_mode) {
+          float r[8];
+          unpack8(ur[u], r);
+          if (a.res_mode == 2) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) r[k] = r[k] * sc2[k] + sh2[k];
+          }
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] += r[k];
+        }
+        if (a.relu) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
+        }
+        *reinterpret_cast<uint4*>(a.out + pix * a.ldo + c8) = pack8(v);
+      }
     }
-    if (pix < a.npix) one(pix);
   }
   // standalone use (no producer finalised the stats): block 0 finalises
   if (blockIdx.x == 0) {
@@ -130,7 +140,7 @@ static inline dim3 chunk_block(int C) {
 hipError_t launch_bn_apply(const BnApplyArgs& a, hipStream_t st) {
   if (a.C % 8 || a.C / 8 > 256) return hipErrorInvalidValue;
   const int rows = 256 / (a.C / 8);
-  const int g = grid_for(a.npix, rows * 4, g_apply_cap);
+  const int g = grid_for(a.npix, rows * 4, g_apply_cap);  // 4 pixels per thread: one pass
   hipLaunchKernelGGL(bn_apply_kernel, dim3(g), chunk_block(a.C), 4 * a.C * sizeof(float), st, a);
   return hipGetLastError();
 }
@@ -164,26 +174,41 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a) {
     mu[k] = a.mean[c8 + k]; is[k] = a.invstd[c8 + k];
     mu2[k] = two ? a.mean2[c8 + k] : 0.f; is2[k] = two ? a.invstd2[c8 + k] : 0.f;
   }
-  auto one = [&](int64_t pix) {
-    float dz[8], y[8];
-    load_dz(a, pix, c8, dz);
-    unpack8(*reinterpret_cast<const uint4*>(a.y + pix * a.ldy + c8), y);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { s1[k] += dz[k]; s2[k] += dz[k] * (y[k] - mu[k]) * is[k]; }
-    if (two) {
-      unpack8(*reinterpret_cast<const uint4*>(a.y2 + pix * a.ldy2 + c8), y);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) t2[k] += dz[k] * (y[k] - mu2[k]) * is2[k];
-    }
-  };
+  constexpr int PPT = 4;
   if (row < rows) {
     const int64_t stride = (int64_t)gridDim.x * rows;
-    int64_t pix = (int64_t)blockIdx.x * rows + row;
-    for (; pix + stride < a.npix; pix += 2 * stride) {
-      one(pix);
-      one(pix + stride);
+    for (int64_t base = (int64_t)blockIdx.x * rows + row; base < a.npix; base += PPT * stride) {
+      uint4 uda[PPT], uact[PPT], uy[PPT], uy2[PPT];
+#pragma unroll
+      for (int u = 0; u < PPT; ++u) {
+        const int64_t pix = base + u * stride;
+        const bool in = pix < a.npix;
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        uda[u] = in ? *reinterpret_cast<const uint4*>(a.da + pix * a.ldda + c8) : z;
+        uact[u] = (in && a.relu) ? *reinterpret_cast<const uint4*>(a.act + pix * a.ldact + c8) : z;
+        uy[u] = in ? *reinterpret_cast<const uint4*>(a.y + pix * a.ldy + c8) : z;
+        uy2[u] = (in && two) ? *reinterpret_cast<const uint4*>(a.y2 + pix * a.ldy2 + c8) : z;
+      }
+#pragma unroll
+      for (int u = 0; u < PPT; ++u) {  // out-of-range pixels load zeros: dz = 0 adds nothing
+        float dz[8], y[8];
+        unpack8(uda[u], dz);
+        if (a.relu) {
+          float av[8];
+          unpack8(uact[u], av);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) dz[k] = av[k] > 0.f ? dz[k] : 0.f;
+        }
+        unpack8(uy[u], y);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { s1[k] += dz[k]; s2[k] += dz[k] * (y[k] - mu[k]) * is[k]; }
+        if (two) {
+          unpack8(uy2[u], y);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) t2[k] += dz[k] * (y[k] - mu2[k]) * is2[k];
+        }
+      }
     }
-    if (pix < a.npix) one(pix);
   }
   // fold rows through LDS: red[row][C]
   extern __shared__ __attribute__((aligned(16))) float red[];
@@ -211,8 +236,8 @@ hipError_t launch_bn_bwd_reduce(const BnBwdArgs& a, hipStream_t st) {
   if (a.C % 8 || a.C / 8 > 256) return hipErrorInvalidValue;
   const int CC = a.C / 8;
   const int rows = 256 / CC;
-  // <= 512 blocks: every block adds into the same C addresses (fp64 atomics)
-  const int g = grid_for(a.npix, rows * 16, 512);
+  // <= 2048 blocks (fp64 atomics spread over kStatRep replicas), 8 pixels per thread
+  const int g = grid_for(a.npix, rows * 8, 2048);
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(g), chunk_block(a.C), (size_t)rows * a.C * sizeof(float), st, a);
   return hipGetLastError();
 }
@@ -283,29 +308,46 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, double i
     mub[k] = two ? coef[7 * a.C + c] : 0.f;
     isb[k] = two ? coef[8 * a.C + c] : 0.f;
   }
-  auto one = [&](int64_t pix) {
-    float dz[8], y[8], o[8];
-    load_dz(a, pix, c8, dz);
-    unpack8(*reinterpret_cast<const uint4*>(a.y + pix * a.ldy + c8), y);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) o[k] = k1[k] * (dz[k] - m1[k] - (y[k] - mu[k]) * is[k] * m2[k]);
-    *reinterpret_cast<uint4*>(a.dy + pix * a.lddy + c8) = pack8(o);
-    if (two) {
-      unpack8(*reinterpret_cast<const uint4*>(a.y2 + pix * a.ldy2 + c8), y);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] = k1b[k] * (dz[k] - m1[k] - (y[k] - mub[k]) * isb[k] * m2b[k]);
-      *reinterpret_cast<uint4*>(a.dy2 + pix * a.lddy2 + c8) = pack8(o);
-    }
-    if (a.dres) *reinterpret_cast<uint4*>(a.dres + pix * a.lddres + c8) = pack8(dz);
-  };
+  constexpr int PPT = 4;
   if (row < rows) {
     const int64_t stride = (int64_t)gridDim.x * rows;
-    int64_t pix = (int64_t)blockIdx.x * rows + row;
-    for (; pix + stride < a.npix; pix += 2 * stride) {
-      one(pix);
-      one(pix + stride);
+    for (int64_t base = (int64_t)blockIdx.x * rows + row; base < a.npix; base += PPT * stride) {
+      uint4 uda[PPT], uact[PPT], uy[PPT], uy2[PPT];
+#pragma unroll
+      for (int u = 0; u < PPT; ++u) {
+        const int64_t pix = base + u * stride;
+        const bool in = pix < a.npix;
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        uda[u] = in ? *reinterpret_cast<const uint4*>(a.da + pix * a.ldda + c8) : z;
+        uact[u] = (in && a.relu) ? *reinterpret_cast<const uint4*>(a.act + pix * a.ldact + c8) : z;
+        uy[u] = in ? *reinterpret_cast<const uint4*>(a.y + pix * a.ldy + c8) : z;
+        uy2[u] = (in && two) ? *reinterpret_cast<const uint4*>(a.y2 + pix * a.ldy2 + c8) : z;
+      }
+#pragma unroll
+      for (int u = 0; u < PPT; ++u) {
+        const int64_t pix = base + u * stride;
+        if (pix >= a.npix) break;
+        float dz[8], y[8], o[8];
+        unpack8(uda[u], dz);
+        if (a.relu) {
+          float av[8];
+          unpack8(uact[u], av);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) dz[k] = av[k] > 0.f ? dz[k] : 0.f;
+        }
+        unpack8(uy[u], y);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = k1[k] * (dz[k] - m1[k] - (y[k] - mu[k]) * is[k] * m2[k]);
+        *reinterpret_cast<uint4*>(a.dy + pix * a.lddy + c8) = pack8(o);
+        if (two) {
+          unpack8(uy2[u], y);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] = k1b[k] * (dz[k] - m1[k] - (y[k] - mub[k]) * isb[k] * m2b[k]);
+          *reinterpret_cast<uint4*>(a.dy2 + pix * a.lddy2 + c8) = pack8(o);
+        }
+        if (a.dres) *reinterpret_cast<uint4*>(a.dres + pix * a.lddres + c8) = pack8(dz);
+      }
     }
-    if (pix < a.npix) one(pix);
   }
 }
 
@@ -321,29 +363,51 @@ hipError_t launch_bn_bwd_apply(const BnBwdArgs& a, hipStream_t st) {
 // ---------------------------------------------------------------------------
 // MaxPool2d(3, 2, 1): torch CPU semantics — first maximum in (kh, kw) scan
 // order wins (strict >), NaN propagates.  Index 0..8 kept as uint8.
+//
+// Both directions walk whole image rows: block b owns rows [b*rpb, (b+1)*rpb)
+// of the output (forward) or input (backward) grid, and a thread keeps one
+// 8-channel chunk (blockDim % CC == 0) while it strides over the row's
+// pixels, so all address math is 32-bit with no per-element division chains;
+// every tap's 16-B load is issued before any is consumed.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) maxpool_fwd_kernel(MaxPoolArgs a) {
+__global__ void __launch_bounds__(256) maxpool_fwd_kernel(MaxPoolArgs a, int rpb) {
   const int CC = a.C >> 3;
-  const int64_t total = (int64_t)a.N * a.P * a.Q * CC;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t opix = e / CC;
-    const int c8 = (int)(e - opix * CC) << 3;
-    const int q = (int)(opix % a.Q);
-    const int p = (int)((opix / a.Q) % a.P);
-    const int n = (int)(opix / ((int64_t)a.P * a.Q));
-    float best[8];
-    int bi[8];
+  const int chunk = threadIdx.x % CC;
+  const int c8 = chunk << 3;
+  const int per_row = a.Q * CC;
+  const int nrows = a.N * a.P;
+  for (int rr = 0; rr < rpb; ++rr) {
+    const int orow = blockIdx.x * rpb + rr;
+    if (orow >= nrows) break;
+    const int n = orow / a.P, p = orow - n * a.P;
+    const bf16_t* xrow[3];
+    bool rok[3];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; bi[k] = -1; }
-    for (int t = 0; t < 9; ++t) {
-      const int kh = t / 3, kw = t - kh * 3;
+    for (int kh = 0; kh < 3; ++kh) {
       const int ih = 2 * p - 1 + kh;
-      const int iw = 2 * q - 1 + kw;
-      const bool ok = ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-      if (ok) {
+      rok[kh] = ih >= 0 && ih < a.H;
+      xrow[kh] = a.x + (size_t)(n * a.H + (rok[kh] ? ih : 0)) * a.W * a.ldx + c8;
+    }
+    for (int e = threadIdx.x; e < per_row; e += blockDim.x) {
+      const int q = e / CC;
+      uint4 u[9];
+      bool ok[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int kh = t / 3, kw = t % 3;
+        const int iw = 2 * q - 1 + kw;
+        ok[t] = rok[kh] && iw >= 0 && iw < a.W;
+        u[t] = ok[t] ? *reinterpret_cast<const uint4*>(xrow[kh] + (size_t)iw * a.ldx) : make_uint4(0, 0, 0, 0);
+      }
+      float best[8];
+      int bi[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; bi[k] = -1; }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        if (!ok[t]) continue;
         float v[8];
-        unpack8(*reinterpret_cast<const uint4*>(a.x + ((int64_t)(n * a.H + ih) * a.W + iw) * a.ldx + c8), v);
+        unpack8(u[t], v);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const bool take = bi[k] < 0 || v[k] > best[k] || (v[k] != v[k] && best[k] == best[k]);
@@ -351,83 +415,100 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(MaxPoolArgs a) {
           bi[k] = take ? t : bi[k];
         }
       }
+      const size_t opix = (size_t)orow * a.Q + q;
+      *reinterpret_cast<uint4*>(a.y + opix * a.ldy + c8) = pack8(best);
+      uint2 ix;
+      ix.x = (unsigned)bi[0] | ((unsigned)bi[1] << 8) | ((unsigned)bi[2] << 16) | ((unsigned)bi[3] << 24);
+      ix.y = (unsigned)bi[4] | ((unsigned)bi[5] << 8) | ((unsigned)bi[6] << 16) | ((unsigned)bi[7] << 24);
+      *reinterpret_cast<uint2*>(a.idx + opix * a.C + c8) = ix;
     }
-    *reinterpret_cast<uint4*>(a.y + opix * a.ldy + c8) = pack8(best);
-    uint2 ix;
-    ix.x = (unsigned)bi[0] | ((unsigned)bi[1] << 8) | ((unsigned)bi[2] << 16) | ((unsigned)bi[3] << 24);
-    ix.y = (unsigned)bi[4] | ((unsigned)bi[5] << 8) | ((unsigned)bi[6] << 16) | ((unsigned)bi[7] << 24);
-    *reinterpret_cast<uint2*>(a.idx + opix * a.C + c8) = ix;
   }
 }
 
-__global__ void __launch_bounds__(256) maxpool_bwd_kernel(MaxPoolArgs a) {
+__global__ void __launch_bounds__(256) maxpool_bwd_kernel(MaxPoolArgs a, int rpb) {
   const int CC = a.C >> 3;
-  const int64_t total = (int64_t)a.N * a.H * a.W * CC;
+  const int chunk = threadIdx.x % CC;
+  const int c8 = chunk << 3;
   const BnBwdArgs& bb = a.bb;
   const bool fz = bb.sums != nullptr;  // launcher: 256 % CC == 0, so c8 is fixed per thread
   float s1[8], s2[8], mu[8], is[8];
-  {
-    const int c8 = (int)((blockIdx.x * blockDim.x + threadIdx.x) % CC) << 3;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      s1[k] = s2[k] = 0.f;
-      mu[k] = fz ? bb.mean[c8 + k] : 0.f;
-      is[k] = fz ? bb.invstd[c8 + k] : 0.f;
-    }
+  for (int k = 0; k < 8; ++k) {
+    s1[k] = s2[k] = 0.f;
+    mu[k] = fz ? bb.mean[c8 + k] : 0.f;
+    is[k] = fz ? bb.invstd[c8 + k] : 0.f;
   }
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t ipix = e / CC;
-    const int c8 = (int)(e - ipix * CC) << 3;
-    const int w = (int)(ipix % a.W);
-    const int h = (int)((ipix / a.W) % a.H);
-    const int n = (int)(ipix / ((int64_t)a.H * a.W));
-    float acc[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-    const int p_lo = h >= 1 ? h / 2 : 0;   // windows with 2p-1 <= h <= 2p+1
+  const int per_row = a.W * CC;
+  const int nrows = a.N * a.H;
+  for (int rr = 0; rr < rpb; ++rr) {
+    const int irow = blockIdx.x * rpb + rr;
+    if (irow >= nrows) break;
+    const int n = irow / a.H, h = irow - n * a.H;
+    // output rows whose window covers h (2p-1 <= h <= 2p+1): p_lo and p_lo+1
+    const int p_lo = h >= 1 ? h / 2 : 0;
     const int p_hi = min((h + 1) / 2, a.P - 1);
-    const int q_lo = w >= 1 ? w / 2 : 0;
-    const int q_hi = min((w + 1) / 2, a.Q - 1);
-    for (int p = p_lo; p <= p_hi; ++p) {
-      const int kh = h - (2 * p - 1);
-      if (kh < 0 || kh > 2) continue;
-      for (int q = q_lo; q <= q_hi; ++q) {
-        const int kw = w - (2 * q - 1);
-        if (kw < 0 || kw > 2) continue;
-        const int64_t opix = ((int64_t)n * a.P + p) * a.Q + q;
-        const uint2 ix = *reinterpret_cast<const uint2*>(a.idx + opix * a.C + c8);
-        float g[8];
-        unpack8(*reinterpret_cast<const uint4*>(a.dy + opix * a.lddy + c8), g);
-        const int want = kh * 3 + kw;
+    for (int e = threadIdx.x; e < per_row; e += blockDim.x) {
+      const int w = e / CC;
+      const size_t ipix = (size_t)irow * a.W + w;
+      const int q0 = w >= 1 ? w / 2 : 0;
+      const int q1 = min((w + 1) / 2, a.Q - 1);
+      uint2 ix[4];
+      uint4 g[4];
+      int want[4];
+      bool ok[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int p = p_lo + (j >> 1);
+        const int q = q0 + (j & 1);
+        const int kh = h - (2 * p - 1), kw = w - (2 * q - 1);
+        ok[j] = p <= p_hi && q <= q1 && kh >= 0 && kh <= 2 && kw >= 0 && kw <= 2;
+        want[j] = kh * 3 + kw;
+        const size_t opix = ((size_t)n * a.P + (ok[j] ? p : 0)) * a.Q + (ok[j] ? q : 0);
+        ix[j] = ok[j] ? *reinterpret_cast<const uint2*>(a.idx + opix * a.C + c8) : make_uint2(0, 0);
+        g[j] = ok[j] ? *reinterpret_cast<const uint4*>(a.dy + opix * a.lddy + c8) : make_uint4(0, 0, 0, 0);
+      }
+      uint4 addv = make_uint4(0, 0, 0, 0), actv = make_uint4(0, 0, 0, 0), yv = make_uint4(0, 0, 0, 0);
+      if (a.add) addv = *reinterpret_cast<const uint4*>(a.add + ipix * a.ldadd + c8);
+      if (fz) {
+        actv = *reinterpret_cast<const uint4*>(bb.act + ipix * bb.ldact + c8);
+        yv = *reinterpret_cast<const uint4*>(bb.y + ipix * bb.ldy + c8);
+      }
+      float acc[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (!ok[j]) continue;
+        float gv[8];
+        unpack8(g[j], gv);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const unsigned word = k < 4 ? ix.x : ix.y;
+          const unsigned word = k < 4 ? ix[j].x : ix[j].y;
           const int b = (word >> ((k & 3) * 8)) & 0xff;
-          if (b == want) acc[k] += g[k];
+          if (b == want[j]) acc[k] += gv[k];
         }
       }
-    }
-    if (a.add) {
-      float r[8];
-      unpack8(*reinterpret_cast<const uint4*>(a.add + ipix * a.ldadd + c8), r);
+      if (a.add) {
+        float r[8];
+        unpack8(addv, r);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] += r[k];
-    }
-    if (fz) {
-      float av[8];
-      unpack8(*reinterpret_cast<const uint4*>(bb.act + ipix * bb.ldact + c8), av);
+        for (int k = 0; k < 8; ++k) acc[k] += r[k];
+      }
+      if (fz) {
+        float av[8];
+        unpack8(actv, av);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] = av[k] > 0.f ? acc[k] : 0.f;
-    }
-    const uint4 o = pack8(acc);
-    *reinterpret_cast<uint4*>(a.dx + ipix * a.lddx + c8) = o;
-    if (fz) {
-      float dz[8], y[8];
-      unpack8(o, dz);
-      unpack8(*reinterpret_cast<const uint4*>(bb.y + ipix * bb.ldy + c8), y);
+        for (int k = 0; k < 8; ++k) acc[k] = av[k] > 0.f ? acc[k] : 0.f;
+      }
+      const uint4 o = pack8(acc);
+      *reinterpret_cast<uint4*>(a.dx + ipix * a.lddx + c8) = o;
+      if (fz) {
+        float dz[8], y[8];
+        unpack8(o, dz);
+        unpack8(yv, y);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) { s1[k] += dz[k]; s2[k] += dz[k] * (y[k] - mu[k]) * is[k]; }
+        for (int k = 0; k < 8; ++k) { s1[k] += dz[k]; s2[k] += dz[k] * (y[k] - mu[k]) * is[k]; }
+      }
     }
   }
   if (!fz) return;
@@ -440,9 +521,9 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(MaxPoolArgs a) {
     for (int k = 0; k < 8; ++k) red[threadIdx.x * 8 + k] = src[k];
     __syncthreads();
     for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
-      const int chunk = c >> 3, k = c & 7;
+      const int ch = c >> 3, k = c & 7;
       float acc = 0.f;
-      for (int t = chunk; t < (int)blockDim.x; t += CC) acc += red[t * 8 + k];
+      for (int t = ch; t < (int)blockDim.x; t += CC) acc += red[t * 8 + k];
       const size_t rep = (size_t)(blockIdx.x % kStatRep) * 2 * a.C;
       atomicAdd(bb.sums + rep + q * a.C + c, (double)acc);
     }
@@ -451,17 +532,23 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(MaxPoolArgs a) {
   if (bb.ticket && last_block_arrive(bb.ticket, gridDim.x, &flag, (int)threadIdx.x < a.C)) bn_bwd_finalize(bb);
 }
 
+static inline int rows_per_block(int nrows, int target_blocks) {
+  return (nrows + target_blocks - 1) / target_blocks;
+}
+
 hipError_t launch_maxpool_fwd(const MaxPoolArgs& a, hipStream_t st) {
-  if (a.C % 8) return hipErrorInvalidValue;
-  const int64_t total = (int64_t)a.N * a.P * a.Q * (a.C / 8);
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total, 256 * 2)), dim3(256), 0, st, a);
+  if (a.C % 8 || 256 % (a.C / 8)) return hipErrorInvalidValue;
+  const int nrows = a.N * a.P;
+  const int rpb = rows_per_block(nrows, 2048);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3((nrows + rpb - 1) / rpb), dim3(256), 0, st, a, rpb);
   return hipGetLastError();
 }
 hipError_t launch_maxpool_bwd(const MaxPoolArgs& a, hipStream_t st) {
-  if (a.C % 8) return hipErrorInvalidValue;
-  if (a.bb.sums && (256 % (a.C / 8) || a.bb.y2)) return hipErrorInvalidValue;
-  const int64_t total = (int64_t)a.N * a.H * a.W * (a.C / 8);
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total, 256 * 2)), dim3(256), 0, st, a);
+  if (a.C % 8 || 256 % (a.C / 8)) return hipErrorInvalidValue;
+  if (a.bb.sums && a.bb.y2) return hipErrorInvalidValue;
+  const int nrows = a.N * a.H;
+  const int rpb = rows_per_block(nrows, 2048);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3((nrows + rpb - 1) / rpb), dim3(256), 0, st, a, rpb);
   return hipGetLastError();
 }
 
@@ -621,11 +708,22 @@ __global__ void __launch_bounds__(256) channel_sum_kernel(const bf16_t* x, int l
 #pragma unroll
   for (int k = 0; k < 8; ++k) s[k] = 0.f;
   if (row < rows) {
-    for (int64_t pix = (int64_t)blockIdx.x * rows + row; pix < npix; pix += (int64_t)gridDim.x * rows) {
-      float v[8];
-      unpack8(*reinterpret_cast<const uint4*>(x + pix * ldx + c8), v);
+    constexpr int PPT = 4;
+    const int64_t stride = (int64_t)gridDim.x * rows;
+    for (int64_t base = (int64_t)blockIdx.x * rows + row; base < npix; base += PPT * stride) {
+      uint4 u[PPT];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) s[k] += v[k];
+      for (int j = 0; j < PPT; ++j) {
+        const int64_t pix = base + j * stride;
+        u[j] = pix < npix ? *reinterpret_cast<const uint4*>(x + pix * ldx + c8) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < PPT; ++j) {
+        float v[8];
+        unpack8(u[j], v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s[k] += v[k];
+      }
     }
   }
   extern __shared__ __attribute__((aligned(16))) float red[];
@@ -637,21 +735,25 @@ __global__ void __launch_bounds__(256) channel_sum_kernel(const bf16_t* x, int l
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float t = 0.f;
     for (int r = 0; r < rows; ++r) t += red[r * C + c];
-    atomicAdd(acc + c, (double)t);
+    atomicAdd(acc + (size_t)(blockIdx.x % kStatRep) * C + c, (double)t);  // replica: no hot address
   }
 }
 
 hipError_t launch_channel_sum(const bf16_t* x, int ldx, int64_t npix, int C, double* acc, hipStream_t st) {
   if (C % 8 || C / 8 > 256) return hipErrorInvalidValue;
   const int CC = C / 8, rows = 256 / CC;
-  hipLaunchKernelGGL(channel_sum_kernel, dim3(grid_for(npix, rows * 8, 1024)), dim3(rows * CC),
+  hipLaunchKernelGGL(channel_sum_kernel, dim3(grid_for(npix, rows * 8, 2048)), dim3(rows * CC),
                      (size_t)rows * C * sizeof(float), st, x, ldx, npix, C, acc);
   return hipGetLastError();
 }
 
+// dst[i] = sum of the kStatRep replicas src[r][i]
 __global__ void d2f_kernel(const double* s, float* d, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) d[i] = (float)s[i];
+  if (i >= n) return;
+  double v = 0.0;
+  for (int r = 0; r < kStatRep; ++r) v += s[(size_t)r * n + i];
+  d[i] = (float)v;
 }
 hipError_t launch_d2f(const double* src, float* dst, int n, hipStream_t st) {
   hipLaunchKernelGGL(d2f_kernel, dim3((n + 255) / 256), dim3(256), 0, st, src, dst, n);
@@ -661,56 +763,98 @@ hipError_t launch_d2f(const double* src, float* dst, int n, hipStream_t st) {
 // ---------------------------------------------------------------------------
 // weight packing: fp32 torch layouts -> bf16 kernel layouts (one launch)
 // ---------------------------------------------------------------------------
+// Every layout change is a transpose of src viewed as [A][B][T] (T = R*S taps):
+//   inner:  dst[a][t][b] = src[a][b][t]   conv fwd (A=Co,B=Ci), convT dgrad (A=Ci,B=Co)
+//   full:   dst[b][t][a] = src[a][b][t]   conv dgrad (A=Co,B=Ci), convT fwd (A=Ci,B=Co)
+// staged through LDS so that both the fp32 reads and the bf16 writes are
+// contiguous runs (the direct gather reads one element per 36-B..18-KB stride).
+constexpr int kPkTA = 64, kPkTB = 16, kPkTmax = 9;
 __global__ void __launch_bounds__(256) pack_kernel(PackTable t) {
   const PackEntry e = t.e[blockIdx.y];
-  const int Co = e.Co, Ci = e.Ci, R = e.R, S = e.S;
-  int total;
-  if (e.kind == PK_STEM) total = (int)Co * 64;
-  else total = (int)Co * Ci * R * S;
-  for (int i = (int)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int)gridDim.x * blockDim.x) {
-    float v = 0.f;
-    switch (e.kind) {
-      case PK_CONV_FWD: {  // dst[co][r][s][ci] <- W[co][ci][r][s]
-        const int ci = (int)(i % Ci); int q = i / Ci;
-        const int s = (int)(q % S); q /= S;
-        const int r = (int)(q % R); const int co = (int)(q / R);
-        v = e.src[(((int)co * Ci + ci) * R + r) * S + s];
-        break;
+  // one LDS buffer for either path: [kPkTB*T][kPkTA+1] tile or a [B*T] row
+  __shared__ float lds[kPkTB * kPkTmax * (kPkTA + 1)];
+  static_assert(512 * kPkTmax <= kPkTB * kPkTmax * (kPkTA + 1), "row fits");
+  if (e.kind == PK_STEM) {  // dst[co][k], k < 49 -> W[co][0][k/7][k%7]
+    const int total = e.Co * 64;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+      const int k = i & 63, co = i >> 6;
+      e.dst[i] = f2bf(k < 49 ? e.src[co * 49 + k] : 0.f);
+    }
+    return;
+  }
+  const bool convt = e.kind == PK_CONVT_FWD || e.kind == PK_CONVT_DGRAD;
+  const int A = convt ? e.Ci : e.Co, B = convt ? e.Co : e.Ci, T = e.R * e.S;
+  const bool full = e.kind == PK_CONV_DGRAD || e.kind == PK_CONVT_FWD;
+  // every load of a pass is issued before the first LDS store (no per-load
+  // round trip to L2)
+  if (!full) {  // one a-row [B][T] -> [T][B] per block iteration
+    constexpr int kMaxPer = 512 * kPkTmax / 256;
+    const int n = B * T;
+    for (int a = blockIdx.x; a < A; a += gridDim.x) {
+      const float* src = e.src + (size_t)a * n;
+      float v[kMaxPer];
+#pragma unroll
+      for (int k = 0; k < kMaxPer; ++k) {
+        const int i = threadIdx.x + 256 * k;
+        v[k] = i < n ? src[i] : 0.f;
       }
-      case PK_CONV_DGRAD: {  // dst[ci][r][s][co] <- W[co][ci][r][s]
-        const int co = (int)(i % Co); int q = i / Co;
-        const int s = (int)(q % S); q /= S;
-        const int r = (int)(q % R); const int ci = (int)(q / R);
-        v = e.src[(((int)co * Ci + ci) * R + r) * S + s];
-        break;
+#pragma unroll
+      for (int k = 0; k < kMaxPer; ++k) {
+        const int i = threadIdx.x + 256 * k;
+        if (i < n) lds[i] = v[k];
       }
-      case PK_CONVT_FWD: {  // dst[co][a][b][ci] <- W[ci][co][a][b]
-        const int ci = (int)(i % Ci); int q = i / Ci;
-        const int b = (int)(q % S); q /= S;
-        const int aa = (int)(q % R); const int co = (int)(q / R);
-        v = e.src[(((int)ci * Co + co) * R + aa) * S + b];
-        break;
-      }
-      case PK_CONVT_DGRAD: {  // dst[ci][a][b][co] <- W[ci][co][a][b]
-        const int co = (int)(i % Co); int q = i / Co;
-        const int b = (int)(q % S); q /= S;
-        const int aa = (int)(q % R); const int ci = (int)(q / R);
-        v = e.src[(((int)ci * Co + co) * R + aa) * S + b];
-        break;
-      }
-      default: {  // PK_STEM: dst[co][k], k < 49 -> W[co][0][k/7][k%7]
-        const int k = (int)(i % 64), co = (int)(i / 64);
-        v = k < 49 ? e.src[(int)co * 49 + k] : 0.f;
+      __syncthreads();
+      bf16_t* dst = e.dst + (size_t)a * n;
+      for (int tt = 0; tt < T; ++tt)
+        for (int b = threadIdx.x; b < B; b += blockDim.x) dst[tt * B + b] = f2bf(lds[b * T + tt]);
+      __syncthreads();
+    }
+    return;
+  }
+  // full transpose in (kPkTA a) x (kPkTB b) x T tiles; tile row j = bl*T + t
+  // maps to dst row b0*T + j, so no index needs a division
+  constexpr int LD = kPkTA + 1;
+  const int ta = (A + kPkTA - 1) / kPkTA, tb = (B + kPkTB - 1) / kPkTB;
+  const int lane = threadIdx.x & 63, sub = threadIdx.x >> 6;  // 4 waves
+  for (int tile_id = blockIdx.x; tile_id < ta * tb; tile_id += gridDim.x) {
+    const int a0 = (tile_id % ta) * kPkTA, b0 = (tile_id / ta) * kPkTB;
+    const int run = min(kPkTB, B - b0) * T;  // valid contiguous floats per a (<= 144)
+    float v[16][3];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int al = sub + 4 * k;
+      const float* src = e.src + ((size_t)(a0 + al) * B + b0) * T;
+#pragma unroll
+      for (int m = 0; m < 3; ++m) {
+        const int j = lane + 64 * m;
+        v[k][m] = (j < run && a0 + al < A) ? src[j] : 0.f;
       }
     }
-    e.dst[i] = f2bf(v);
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+#pragma unroll
+      for (int m = 0; m < 3; ++m) {
+        const int j = lane + 64 * m;
+        if (j < run) lds[j * LD + sub + 4 * k] = v[k][m];
+      }
+    __syncthreads();
+    if (a0 + lane < A) {
+      bf16_t* dst = e.dst + (size_t)b0 * T * A + a0 + lane;
+      for (int j = sub; j < run; j += 4) dst[(size_t)j * A] = f2bf(lds[j * LD + lane]);
+    }
+    __syncthreads();
   }
 }
 
 hipError_t launch_pack(const PackTable& t, hipStream_t st) {
   if (t.n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(pack_kernel, dim3(512, t.n), dim3(256), 0, st, t);
+  for (int i = 0; i < t.n; ++i) {
+    const PackEntry& e = t.e[i];
+    const bool convt = e.kind == PK_CONVT_FWD || e.kind == PK_CONVT_DGRAD;
+    const int B = convt ? e.Co : e.Ci;
+    if (e.kind != PK_STEM && (e.R * e.S > kPkTmax || B * e.R * e.S > 512 * kPkTmax)) return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(pack_kernel, dim3(256, t.n), dim3(256), 0, st, t);
   return hipGetLastError();
 }
 

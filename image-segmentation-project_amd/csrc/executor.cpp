@@ -58,7 +58,7 @@ struct Conv {
   int w, b = -1;  // param indices
   int kind, Ci, Co, R, S, stride, pad;
   size_t pk_fwd = 0, pk_dgrad = 0, wacc = 0;  // ws offsets
-  size_t bias_acc = 0;                        // fp64 [Co] (convT bias grads)
+  size_t bias_acc = 0;                        // fp64 [kStatRep][Co] (convT bias grads)
 };
 
 struct Block {
@@ -309,7 +309,7 @@ static int build_plan(unet_plan* p) {
     b.tbwd = A.take(sizeof(unsigned));
   }
   for (auto& cv : p->convs)
-    if (cv.kind == L_CONVT) cv.bias_acc = A.take((size_t)cv.Co * sizeof(double));
+    if (cv.kind == L_CONVT) cv.bias_acc = A.take((size_t)kStatRep * cv.Co * sizeof(double));
   p->head_usum = A.take((size_t)(c0 / 2 * 4 + 1) * sizeof(double));
   for (auto& cv : p->convs) {
     size_t n;

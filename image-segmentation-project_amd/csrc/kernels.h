@@ -78,6 +78,10 @@ struct ConvWgradArgs {
 
 hipError_t launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st);
 hipError_t launch_conv_fwd_v1(const ConvFwdArgs& a, int mode, hipStream_t st);  // register-staged
+// weight-stationary halo kernel for 3x3/s1/p1 layers with few channels
+// (conv_halo.hip); mode 0 conv, 1 dgrad.  hipErrorNotSupported if not covered.
+hipError_t launch_conv3x3_ws(const ConvFwdArgs& a, int mode, hipStream_t st);
+void set_conv_ws(int on);
 void set_conv_impl(int glds);  // 1: LDS-DMA pipelined kernels (default), 0: register-staged v1
 void set_conv_config(int cfg);  // 0: automatic tile selection, >0: fixed tile config (tuning)
 hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st);
@@ -130,7 +134,9 @@ hipError_t launch_head_fwd(const HeadArgs& a, hipStream_t st);
 hipError_t launch_head_bwd(const HeadArgs& a, hipStream_t st);
 hipError_t launch_head_grads(const HeadArgs& a, hipStream_t st);
 
-// per-channel sum over pixels (ConvTranspose bias grads): out[c] = sum_px x[px][c]
+// per-channel sum over pixels (ConvTranspose bias grads): acc[r][c] += partial
+// sums of x[px][c] (acc: fp64 [kStatRep][C], zeroed); launch_d2f then writes
+// dst[c] = sum_r acc[r][c]
 hipError_t launch_channel_sum(const bf16_t* x, int ldx, int64_t npix, int C, double* acc,
                               hipStream_t st);
 hipError_t launch_d2f(const double* src, float* dst, int n, hipStream_t st);

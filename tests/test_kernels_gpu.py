@@ -71,6 +71,12 @@ CASES_FWD = [  # N, C, H, Co, R, stride, pad
     (2, 64, 32, 128, 3, 2, 1),
     (2, 64, 32, 128, 1, 2, 0),
     (2, 512, 8, 512, 3, 1, 1),
+    # weight-stationary halo kernel (conv_halo.hip): several tiles per block,
+    # two output-channel groups
+    (8, 64, 128, 64, 3, 1, 1),
+    (8, 32, 128, 32, 3, 1, 1),
+    (4, 96, 128, 32, 3, 1, 1),
+    (2, 64, 32, 128, 3, 1, 1),
 ]
 
 
@@ -101,6 +107,9 @@ CASES_DGRAD = [  # N, Ci, H, Co, R, stride, pad  (forward geometry)
     (2, 64, 32, 128, 3, 2, 1),
     (2, 64, 32, 128, 1, 2, 0),
     (1, 256, 16, 512, 3, 2, 1),
+    (8, 64, 128, 64, 3, 1, 1),
+    (4, 96, 128, 32, 3, 1, 1),
+    (4, 128, 64, 64, 3, 1, 1),
 ]
 
 
@@ -271,15 +280,15 @@ def test_bn_forward_backward(L, C, res, cuda):
     close(dgb[C:], bl.grad, rel=5e-3)
 
 
-def test_maxpool_fwd_bwd(L, cuda):
-    N, C, H = 2, 64, 32
+@pytest.mark.parametrize("N,C,H", [(2, 64, 32), (1, 128, 34), (3, 64, 6)])
+def test_maxpool_fwd_bwd(L, cuda, N, C, H):
     g = torch.Generator().manual_seed(7)
     x = bf(torch.randn(N, C, H, H, generator=g)).relu()  # ties at 0, like post-ReLU
     # a slice of a wider (concat) buffer as input
     buf = torch.zeros(N, H, H, C + 32, dtype=torch.bfloat16, device="cuda")
     buf[..., :C] = nhwc(x).cuda()
     xs = buf[..., :C]
-    P = H // 2
+    P = (H - 1) // 2 + 1
     y = torch.empty(N, P, P, C, dtype=torch.bfloat16, device="cuda")
     idx = torch.empty(N, P, P, C, dtype=torch.uint8, device="cuda")
     assert L.unet_maxpool_fwd(xs.data_ptr(), C + 32, y.data_ptr(), idx.data_ptr(), N, H, H, C, S()) == 0
