@@ -36,6 +36,16 @@ namespace unet {
 
 void conv_kernel_tag(const char* tag);  // conv_kernels.hip: per-launch profiler column
 
+// 8-B global load the compiler does not track (its waitcnt pass would
+// otherwise drain the in-flight halo DMA at the first such load,
+// cdna_hip_programming.md §5 item 4(b)); the consumer waits by hand
+// (asm_wait_all) before reading the value.
+__device__ __forceinline__ uint2 ld_u2_asm(const void* p) {
+  uint2 v;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
 __device__ __forceinline__ int ws_off(int row, int chunk) {  // byte offset of (row, logical 16-B chunk)
   return row * 64 + ((chunk ^ ((row >> 1) & 2)) << 4);
 }
@@ -115,6 +125,15 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
 #pragma unroll
     for (int e = 0; e < 4; ++e) q0[i][e] = q1[i][e] = 0.f;
 
+  // loop-invariant fragment offsets: weights (16 co rows from co = 0) and the
+  // halo rows this wave's output rows need for every tap shift
+  const int aoff = ws_off(lane & 15, lane >> 4);
+  int boff[RW + 2][3];
+#pragma unroll
+  for (int h = 0; h < RW + 2; ++h)
+#pragma unroll
+    for (int d = 0; d < 3; ++d) boff[h][d] = ws_off((wave * RW + h) * HWD + d + (lane & 15), lane >> 4);
+
   int t = blockIdx.x / ncg;
   if (t < ntiles) issue_halo(t, 0);
   wait_vmcnt<0>();
@@ -129,20 +148,46 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
     size_t pix[RW];
 #pragma unroll
     for (int j = 0; j < RW; ++j) pix[j] = ((size_t)n * a.P + oh0 + wave * RW + j) * a.Q + ow0 + (lane & 15);
-    // per-pixel epilogue operands of this tile, fetched now so their latency
-    // hides behind the MFMA loop (dgrad only: the forward has none)
+    // per-pixel epilogue operands of this tile (dgrad only: the forward has
+    // none), fetched before the MFMA loop so their latency hides behind it
+    // when the registers allow (PREF), else batched right after it
+    constexpr bool PREF = FLIP && RW * FN <= 8;
     uint2 uadd[RW][FN], uact[RW][FN], uy[RW][FN];
-    if (FLIP) {
+    auto fetch = [&]() {  // conditions hoisted out of the loads (no per-load branch + wait)
+      if (a.add) {
 #pragma unroll
-      for (int j = 0; j < RW; ++j)
+        for (int j = 0; j < RW; ++j)
 #pragma unroll
-        for (int i = 0; i < FN; ++i) {
-          const int co = min(co0 + i * 16 + ((lane >> 4) << 2), a.Cout - 4);
-          uadd[j][i] = a.add ? *reinterpret_cast<const uint2*>(a.add + pix[j] * a.ldadd + co) : make_uint2(0, 0);
-          uact[j][i] = fbwd ? *reinterpret_cast<const uint2*>(bb.act + pix[j] * bb.ldact + co) : make_uint2(0, 0);
-          uy[j][i] = fbwd ? *reinterpret_cast<const uint2*>(bb.y + pix[j] * bb.ldy + co) : make_uint2(0, 0);
-        }
-    }
+          for (int i = 0; i < FN; ++i) {
+            const int co = min(co0 + i * 16 + ((lane >> 4) << 2), a.Cout - 4);
+            const void* src = a.add + pix[j] * a.ldadd + co;
+            uadd[j][i] = PREF ? ld_u2_asm(src) : *reinterpret_cast<const uint2*>(src);
+          }
+      } else {
+#pragma unroll
+        for (int j = 0; j < RW; ++j)
+#pragma unroll
+          for (int i = 0; i < FN; ++i) uadd[j][i] = make_uint2(0, 0);
+      }
+      if (fbwd) {
+#pragma unroll
+        for (int j = 0; j < RW; ++j)
+#pragma unroll
+          for (int i = 0; i < FN; ++i) {
+            const int co = min(co0 + i * 16 + ((lane >> 4) << 2), a.Cout - 4);
+            const void* s1 = bb.act + pix[j] * bb.ldact + co;
+            const void* s2 = bb.y + pix[j] * bb.ldy + co;
+            uact[j][i] = PREF ? ld_u2_asm(s1) : *reinterpret_cast<const uint2*>(s1);
+            uy[j][i] = PREF ? ld_u2_asm(s2) : *reinterpret_cast<const uint2*>(s2);
+          }
+      } else {
+#pragma unroll
+        for (int j = 0; j < RW; ++j)
+#pragma unroll
+          for (int i = 0; i < FN; ++i) uact[j][i] = uy[j][i] = make_uint2(0, 0);
+      }
+    };
+    if (PREF) fetch();
     const char* H = hl + b * HBUF;
     f32x4 acc[RW][FN];
 #pragma unroll
@@ -151,7 +196,7 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
       for (int i = 0; i < FN; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int p = 0; p < NP; ++p)
-#pragma unroll 1
+#pragma unroll
       for (int r = 0; r < 3; ++r)
 #pragma unroll
         for (int s = 0; s < 3; ++s) {
@@ -159,19 +204,26 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
           bf16x8 A[FN];
 #pragma unroll
           for (int i = 0; i < FN; ++i)
-            A[i] = *reinterpret_cast<const bf16x8*>(wl + (tap * NP + p) * COT * 64 +
-                                                     ws_off(i * 16 + (lane & 15), lane >> 4));
+            A[i] = *reinterpret_cast<const bf16x8*>(wl + (tap * NP + p) * COT * 64 + i * 1024 + aoff);
           const int dr = FLIP ? 2 - r : r, ds = FLIP ? 2 - s : s;
 #pragma unroll
           for (int j = 0; j < RW; ++j) {
-            const int hp = (wave * RW + j + dr) * HWD + ds + (lane & 15);
-            const bf16x8 B = *reinterpret_cast<const bf16x8*>(H + p * PANEL + ws_off(hp, lane >> 4));
+            const bf16x8 B = *reinterpret_cast<const bf16x8*>(H + p * PANEL + boff[j + dr][ds]);
 #pragma unroll
             for (int i = 0; i < FN; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B, acc[j][i], 0, 0, 0);
           }
         }
 
     // ---- tile epilogue: bias, addend, ReLU mask (fused BN backward), bf16 store, sums
+    if (FLIP && !PREF) fetch();
+    if (PREF) {  // the asm prefetch (and the next halo) have landed; order every use after the wait
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < RW; ++j)
+#pragma unroll
+        for (int i = 0; i < FN; ++i) asm volatile("" : "+v"(uadd[j][i].x), "+v"(uadd[j][i].y), "+v"(uact[j][i].x),
+                                                  "+v"(uact[j][i].y), "+v"(uy[j][i].x), "+v"(uy[j][i].y));
+    }
 #pragma unroll
     for (int j = 0; j < RW; ++j) {
 #pragma unroll
