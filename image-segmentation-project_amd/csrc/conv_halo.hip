@@ -1,29 +1,34 @@
-// Weight-stationary halo convolution for the 3x3 / stride-1 / pad-1 layers
-// with few channels (SURVEY.md §8(a) rows a3 enc1 BasicBlocks and a6
-// decoder1/decoder2 blocks: C <= 96 input and <= 128 output channels at 128^2
-// and 256^2).  Forward conv and its data gradient (FLIP: the transposed
-// gather of s1 p1 is the same stencil with the taps mirrored, on the dgrad
-// weight pack [Cin][R][S][Cout]).
+// Halo convolutions for the 3x3 / stride-1 / pad-1 layers (SURVEY.md §8(a)
+// rows a3 BasicBlocks and a6 decoder blocks): forward conv and its data
+// gradient (FLIP: the transposed gather of s1 p1 is the same stencil with the
+// taps mirrored, on the dgrad weight pack [Cin][R][S][Cout]).
 //
-// The implicit-GEMM kernel (conv_kernels.hip) re-fetches every input pixel
-// once per tap and per output tile, and at K = 9*C <= 864 its k-loop is only
-// 9..27 steps long, so its pipeline never reaches steady state.  Here a
-// persistent block keeps ALL 9 taps of its COT output channels in LDS
-// (<= 74 KB, loaded once) and streams TH x 16 output-pixel tiles through a
-// double-buffered LDS halo of (TH+2) x 18 input pixels: each input byte
-// crosses L2 -> LDS ~1.3 times instead of 9, the next tile's halo (LDS-DMA,
-// buffer_load ... lds) lands while the current one is computed, and the
-// BN-statistics epilogue is reduced once per block instead of once per tile.
+// The implicit-GEMM kernel (conv_kernels.hip) stages an im2col tile per
+// (tap, channel chunk), so every input pixel crosses L2 -> LDS once per tap
+// (9x) and per output tile.  Here an output tile of TH x 16 pixels reads one
+// (TH+2) x 18 input halo per 32-channel chunk and all 9 taps are MFMA'd from
+// it at a row shift:
+//
+//  * conv3x3_ws_kernel (weight-stationary, C <= 96): a persistent block keeps
+//    ALL 9 taps of its COT output channels in LDS (<= 74 KB, loaded once) and
+//    streams output tiles through a double-buffered halo; the BN-statistics
+//    epilogue is reduced once per block.
+//  * conv3x3_hs_kernel (halo-streamed, C >= 128): one output tile per block;
+//    the K loop walks 32-channel chunks, each stage = that chunk's halo plus
+//    its 9 weight taps, double-buffered by LDS-DMA.  Per stage it moves
+//    ((TH+2)*18 + 9*COT) * 64 B for 2*TH*16*COT*288 flop — 2.5x the flop per
+//    staged byte of a 128x128 im2col tile.
 //
 // LDS images are panels of 32 channels = 64-B rows (a halo pixel or a weight
 // row).  An MFMA operand fragment reads 16 CONSECUTIVE rows starting at an
 // arbitrary row (tap shift); with the 16-B chunk XOR-swizzled by bit 2 of the
 // row (chunk ^ ((row >> 1) & 2)) every ds_read_b128 lane group hits 16
 // distinct bank slots for every start row (exhaustively checked for the
-// gfx950 lane grouping {0-3,12-15,20-27}, ...).  The swizzle is applied on
-// the DMA source side (cdna_hip_programming.md §5.4 rule 21).
+// gfx950 lane grouping {0-3,12-15,20-27}, ...; SQ_LDS_BANK_CONFLICT = 0
+// measured).  The swizzle is applied on the DMA source side
+// (cdna_hip_programming.md §5.4 rule 21).
 //
-// GEMM view per tile: D[co][px] += W[co][(tap, c)] . X[px + shift(tap)][c],
+// GEMM view: D[co][px] += W[co][(tap, c)] . X[px + shift(tap)][c],
 // v_mfma_f32_16x16x32_bf16 with A = weight fragment (16 co x 32 c), B = halo
 // fragment (16 px of one output row x 32 c); each wave owns RW output rows x
 // COT channels (acc[RW][FN]).
@@ -38,8 +43,7 @@ void conv_kernel_tag(const char* tag);  // conv_kernels.hip: per-launch profiler
 
 // 8-B global load the compiler does not track (its waitcnt pass would
 // otherwise drain the in-flight halo DMA at the first such load,
-// cdna_hip_programming.md §5 item 4(b)); the consumer waits by hand
-// (asm_wait_all) before reading the value.
+// cdna_hip_programming.md §5 item 4(b)); the consumer waits by hand.
 __device__ __forceinline__ uint2 ld_u2_asm(const void* p) {
   uint2 v;
   asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
@@ -50,180 +54,135 @@ __device__ __forceinline__ int ws_off(int row, int chunk) {  // byte offset of (
   return row * 64 + ((chunk ^ ((row >> 1) & 2)) << 4);
 }
 
-template <int NP, int FN, int TH, int NW, bool FLIP>
-__global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int ntiles, int ncg) {
-  constexpr int COT = FN * 16;               // output channels per block
-  constexpr int RW = TH / NW;                // output rows per wave
-  constexpr int HWD = 18;                    // halo width (16 + 2)
-  constexpr int HP = (TH + 2) * HWD;         // halo pixels
-  constexpr int HPR = (HP + 15) / 16 * 16;   // rows per panel (16 rows per DMA instruction)
-  constexpr int PANEL = HPR * 64;
-  constexpr int HBUF = NP * PANEL;
-  constexpr int WBYTES = 9 * NP * COT * 64;
-  constexpr int H_INS = NP * HPR / 16;
-  constexpr int W_INS = 9 * NP * COT / 16;
-  constexpr int CIN = NP * 32;
-  static_assert(TH % NW == 0 && RW >= 1, "rows per wave");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* wl = smem;
-  char* hl = smem + WBYTES;
+constexpr int kHW = 18;  // halo width: 16 output columns + 2
 
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int cg = blockIdx.x % ncg;
-  const int nslot = gridDim.x / ncg;
-  const int co0 = cg * COT;
-  const int tq = a.Q >> 4, tp = a.P / TH;
-  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
-  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (unsigned)((size_t)a.Cout * 9 * CIN * 2));
+// Halo of one output tile (TH x 16 at (n, oh0, ow0)): np 32-channel panels of
+// input channels c0 .. c0 + 32*np into LDS, HPR rows per panel.  DMA
+// instructions are dealt round-robin over the NW waves.
+template <int TH, int NW>
+__device__ __forceinline__ void issue_halo_dma(const ConvFwdArgs& a, __amdgpu_buffer_rsrc_t xr, char* dst, int n,
+                                               int oh0, int ow0, int c0, int np, int wave, int lane) {
+  constexpr int HP = (TH + 2) * kHW;
+  constexpr int HPR = (HP + 15) / 16 * 16;
+  const int nins = np * HPR / 16;
+  for (int ins = wave; ins < nins; ins += NW) {
+    const int rowg = ins * 16 + (lane >> 2);
+    const int p = rowg / HPR, hp = rowg - p * HPR;
+    const int lchunk = (lane & 3) ^ ((hp >> 1) & 2);
+    const int hr = hp / kHW, hc = hp - hr * kHW;
+    const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
+    unsigned off = kOOB;
+    if (hp < HP && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+      off = (unsigned)((((n * a.H + ih) * a.W + iw) * a.ldx + c0 + p * 32 + lchunk * 8) * 2);
+    glds16(xr, dst + ins * 1024, off);
+  }
+}
 
-  // ---- all 9 taps of this block's output channels, once: [tap][panel][co][32 c]
-  for (int ins = wave; ins < W_INS; ins += NW) {
+// 9 taps x COT output rows x np panels of 32 reduction channels from kc0,
+// LDS layout [tap][panel][co][32]; weights packed [Cout][9][K = a.C].
+template <int COT, int NW>
+__device__ __forceinline__ void issue_weight_dma(const ConvFwdArgs& a, __amdgpu_buffer_rsrc_t wr, char* dst,
+                                                 int co0, int kc0, int np, int wave, int lane) {
+  const int K = a.C;
+  const int nins = 9 * np * COT / 16;
+  for (int ins = wave; ins < nins; ins += NW) {
     const int rowg = ins * 16 + (lane >> 2);
     const int co = rowg % COT, tpn = rowg / COT;
-    const int p = tpn % NP, tap = tpn / NP;
+    const int p = tpn % np, tap = tpn / np;
     const int lchunk = (lane & 3) ^ ((co >> 1) & 2);
     unsigned off = kOOB;
-    if (co0 + co < a.Cout) off = (unsigned)(((co0 + co) * 9 * CIN + tap * CIN + p * 32 + lchunk * 8) * 2);
-    glds16(wr, wl + ins * 1024, off);
+    if (co0 + co < a.Cout) off = (unsigned)(((co0 + co) * 9 * K + tap * K + kc0 + p * 32 + lchunk * 8) * 2);
+    glds16(wr, dst + ins * 1024, off);
   }
+}
 
-  auto issue_halo = [&](int t, int b) {
-    const int n = t / (tp * tq);
-    const int rem = t - n * (tp * tq);
-    const int oh0 = (rem / tq) * TH, ow0 = (rem % tq) << 4;
-    for (int ins = wave; ins < H_INS; ins += NW) {
-      const int rowg = ins * 16 + (lane >> 2);
-      const int p = rowg / HPR, hp = rowg - p * HPR;
-      const int lchunk = (lane & 3) ^ ((hp >> 1) & 2);
-      const int hr = hp / HWD, hc = hp - hr * HWD;
-      const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
-      unsigned off = kOOB;
-      if (hp < HP && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
-        off = (unsigned)((((n * a.H + ih) * a.W + iw) * a.ldx + p * 32 + lchunk * 8) * 2);
-      glds16(xr, hl + b * HBUF + ins * 1024, off);
+// One 32-channel panel of a tile: 9 taps x RW rows x FN channel fragments.
+// W: the panel's weight image (tap stride WTS bytes, 16-co fragment stride
+// 1 KiB); H: the panel's halo image.
+template <int FN, int RW, int WTS, bool FLIP>
+__device__ __forceinline__ void mfma_panel(f32x4 (&acc)[RW][FN], const char* W, const char* H, int aoff,
+                                           const int (&boff)[RW + 2][3]) {
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      bf16x8 A[FN];
+#pragma unroll
+      for (int i = 0; i < FN; ++i) A[i] = *reinterpret_cast<const bf16x8*>(W + (r * 3 + s) * WTS + i * 1024 + aoff);
+      const int dr = FLIP ? 2 - r : r, ds = FLIP ? 2 - s : s;
+#pragma unroll
+      for (int j = 0; j < RW; ++j) {
+        const bf16x8 B = *reinterpret_cast<const bf16x8*>(H + boff[j + dr][ds]);
+#pragma unroll
+        for (int i = 0; i < FN; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B, acc[j][i], 0, 0, 0);
+      }
     }
-  };
+}
 
-  // ---- epilogue constants (bias, BN mean / invstd of the fused backward) in
-  // LDS behind the halo buffers; the BN sums are the only registers kept
-  // across tiles
-  const BnBwdArgs& bb = a.bb;
-  const bool fbwd = bb.sums != nullptr;
-  const bool stats = a.stats != nullptr || fbwd;
-  float* cst = reinterpret_cast<float*>(hl + 2 * HBUF);  // [3][COT]
-  for (int c = tid; c < COT; c += NW * 64) {
-    const int co = co0 + c;
-    const bool ok = co < a.Cout;
-    cst[c] = (a.bias && ok) ? a.bias[co] : 0.f;
-    cst[COT + c] = (fbwd && ok) ? bb.mean[co] : 0.f;
-    cst[2 * COT + c] = (fbwd && ok) ? bb.invstd[co] : 0.f;
-  }
-  float q0[FN][4], q1[FN][4];
-#pragma unroll
-  for (int i = 0; i < FN; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) q0[i][e] = q1[i][e] = 0.f;
+// Epilogue of one tile: bias, addend, ReLU mask (fused BN backward), bf16
+// store, BN sums accumulated in registers (q0, q1).  cst = LDS [3][COT]
+// bias | mean | invstd.  The per-pixel operands of a dgrad (addend, forward
+// activation, raw conv output of the BN) are fetched by fetch(): early with
+// untracked loads (PREF) so their latency hides behind MFMA work, else right
+// before use; landed() is the matching wait.
+template <int FN, int RW, bool FLIP, bool PREF>
+struct TileEpi {
+  uint2 uadd[RW][FN], uact[RW][FN], uy[RW][FN];
 
-  // loop-invariant fragment offsets: weights (16 co rows from co = 0) and the
-  // halo rows this wave's output rows need for every tap shift
-  const int aoff = ws_off(lane & 15, lane >> 4);
-  int boff[RW + 2][3];
-#pragma unroll
-  for (int h = 0; h < RW + 2; ++h)
-#pragma unroll
-    for (int d = 0; d < 3; ++d) boff[h][d] = ws_off((wave * RW + h) * HWD + d + (lane & 15), lane >> 4);
-
-  int t = blockIdx.x / ncg;
-  if (t < ntiles) issue_halo(t, 0);
-  wait_vmcnt<0>();
-  __syncthreads();
-
-  for (int k = 0; t < ntiles; ++k, t += nslot) {
-    const int b = k & 1;
-    if (t + nslot < ntiles) issue_halo(t + nslot, b ^ 1);  // lands while this tile computes
-    const int n = t / (tp * tq);
-    const int rem = t - n * (tp * tq);
-    const int oh0 = (rem / tq) * TH, ow0 = (rem % tq) << 4;
-    size_t pix[RW];
-#pragma unroll
-    for (int j = 0; j < RW; ++j) pix[j] = ((size_t)n * a.P + oh0 + wave * RW + j) * a.Q + ow0 + (lane & 15);
-    // per-pixel epilogue operands of this tile (dgrad only: the forward has
-    // none), fetched before the MFMA loop so their latency hides behind it
-    // when the registers allow (PREF), else batched right after it
-    constexpr bool PREF = FLIP && RW * FN <= 8;
-    uint2 uadd[RW][FN], uact[RW][FN], uy[RW][FN];
-    auto fetch = [&]() {  // conditions hoisted out of the loads (no per-load branch + wait)
-      if (a.add) {
-#pragma unroll
-        for (int j = 0; j < RW; ++j)
-#pragma unroll
-          for (int i = 0; i < FN; ++i) {
-            const int co = min(co0 + i * 16 + ((lane >> 4) << 2), a.Cout - 4);
-            const void* src = a.add + pix[j] * a.ldadd + co;
-            uadd[j][i] = PREF ? ld_u2_asm(src) : *reinterpret_cast<const uint2*>(src);
-          }
-      } else {
-#pragma unroll
-        for (int j = 0; j < RW; ++j)
-#pragma unroll
-          for (int i = 0; i < FN; ++i) uadd[j][i] = make_uint2(0, 0);
-      }
-      if (fbwd) {
-#pragma unroll
-        for (int j = 0; j < RW; ++j)
-#pragma unroll
-          for (int i = 0; i < FN; ++i) {
-            const int co = min(co0 + i * 16 + ((lane >> 4) << 2), a.Cout - 4);
-            const void* s1 = bb.act + pix[j] * bb.ldact + co;
-            const void* s2 = bb.y + pix[j] * bb.ldy + co;
-            uact[j][i] = PREF ? ld_u2_asm(s1) : *reinterpret_cast<const uint2*>(s1);
-            uy[j][i] = PREF ? ld_u2_asm(s2) : *reinterpret_cast<const uint2*>(s2);
-          }
-      } else {
-#pragma unroll
-        for (int j = 0; j < RW; ++j)
-#pragma unroll
-          for (int i = 0; i < FN; ++i) uact[j][i] = uy[j][i] = make_uint2(0, 0);
-      }
-    };
-    if (PREF) fetch();
-    const char* H = hl + b * HBUF;
-    f32x4 acc[RW][FN];
-#pragma unroll
-    for (int j = 0; j < RW; ++j)
-#pragma unroll
-      for (int i = 0; i < FN; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int p = 0; p < NP; ++p)
-#pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int s = 0; s < 3; ++s) {
-          const int tap = r * 3 + s;
-          bf16x8 A[FN];
-#pragma unroll
-          for (int i = 0; i < FN; ++i)
-            A[i] = *reinterpret_cast<const bf16x8*>(wl + (tap * NP + p) * COT * 64 + i * 1024 + aoff);
-          const int dr = FLIP ? 2 - r : r, ds = FLIP ? 2 - s : s;
-#pragma unroll
-          for (int j = 0; j < RW; ++j) {
-            const bf16x8 B = *reinterpret_cast<const bf16x8*>(H + p * PANEL + boff[j + dr][ds]);
-#pragma unroll
-            for (int i = 0; i < FN; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B, acc[j][i], 0, 0, 0);
-          }
-        }
-
-    // ---- tile epilogue: bias, addend, ReLU mask (fused BN backward), bf16 store, sums
-    if (FLIP && !PREF) fetch();
-    if (PREF) {  // the asm prefetch (and the next halo) have landed; order every use after the wait
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __device__ __forceinline__ void fetch(const ConvFwdArgs& a, const size_t (&pix)[RW], int co0, int lane) {
+    if (!FLIP) return;
+    const BnBwdArgs& bb = a.bb;
+    if (a.add) {  // conditions hoisted out of the loads (no per-load branch + wait)
 #pragma unroll
       for (int j = 0; j < RW; ++j)
 #pragma unroll
-        for (int i = 0; i < FN; ++i) asm volatile("" : "+v"(uadd[j][i].x), "+v"(uadd[j][i].y), "+v"(uact[j][i].x),
-                                                  "+v"(uact[j][i].y), "+v"(uy[j][i].x), "+v"(uy[j][i].y));
+        for (int i = 0; i < FN; ++i) {
+          const int co = min(co0 + i * 16 + ((lane >> 4) << 2), a.Cout - 4);
+          const void* src = a.add + pix[j] * a.ldadd + co;
+          uadd[j][i] = PREF ? ld_u2_asm(src) : *reinterpret_cast<const uint2*>(src);
+        }
+    } else {
+#pragma unroll
+      for (int j = 0; j < RW; ++j)
+#pragma unroll
+        for (int i = 0; i < FN; ++i) uadd[j][i] = make_uint2(0, 0);
     }
+    if (bb.sums) {
+#pragma unroll
+      for (int j = 0; j < RW; ++j)
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+          const int co = min(co0 + i * 16 + ((lane >> 4) << 2), a.Cout - 4);
+          const void* s1 = bb.act + pix[j] * bb.ldact + co;
+          const void* s2 = bb.y + pix[j] * bb.ldy + co;
+          uact[j][i] = PREF ? ld_u2_asm(s1) : *reinterpret_cast<const uint2*>(s1);
+          uy[j][i] = PREF ? ld_u2_asm(s2) : *reinterpret_cast<const uint2*>(s2);
+        }
+    } else {
+#pragma unroll
+      for (int j = 0; j < RW; ++j)
+#pragma unroll
+        for (int i = 0; i < FN; ++i) uact[j][i] = uy[j][i] = make_uint2(0, 0);
+    }
+  }
+
+  __device__ __forceinline__ void landed() {
+    if (!PREF) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < RW; ++j)
+#pragma unroll
+      for (int i = 0; i < FN; ++i)  // order every use after the wait
+        asm volatile("" : "+v"(uadd[j][i].x), "+v"(uadd[j][i].y), "+v"(uact[j][i].x), "+v"(uact[j][i].y),
+                     "+v"(uy[j][i].x), "+v"(uy[j][i].y));
+  }
+
+  __device__ __forceinline__ void store(const ConvFwdArgs& a, const f32x4 (&acc)[RW][FN], const size_t (&pix)[RW],
+                                        int co0, int lane, const float* cst, float (&q0)[FN][4],
+                                        float (&q1)[FN][4]) {
+    constexpr int COT = FN * 16;
+    const bool fbwd = a.bb.sums != nullptr;
+    const bool stats = a.stats != nullptr || fbwd;
 #pragma unroll
     for (int j = 0; j < RW; ++j) {
 #pragma unroll
@@ -249,7 +208,7 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
         o.x = pack_bf2(v[0], v[1]);
         o.y = pack_bf2(v[2], v[3]);
         *reinterpret_cast<uint2*>(a.y + pix[j] * a.ldy + co) = o;
-        if (FLIP && fbwd) {
+        if (FLIP && fbwd) {  // sums of the stored bf16 dZ, as bn_bwd_reduce_kernel would read them
           const float dz[4] = {__uint_as_float(o.x << 16), __uint_as_float(o.x & 0xffff0000u),
                                __uint_as_float(o.y << 16), __uint_as_float(o.y & 0xffff0000u)};
           const uint2 u = uy[j][i];
@@ -266,12 +225,32 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
         }
       }
     }
-    wait_vmcnt<0>();               // the next tile's halo has landed (this wave's part)
-    __builtin_amdgcn_s_barrier();  // ... everyone's part; buffer b is free for reuse
   }
-  if (!stats) return;
+};
 
-  // ---- block reduction of the BN sums: 16 pixel lanes, then the NW waves
+// bias | mean | invstd of the block's COT channels into LDS
+template <int COT>
+__device__ __forceinline__ void load_epi_constants(const ConvFwdArgs& a, float* cst, int co0, int tid, int nthr) {
+  const bool fbwd = a.bb.sums != nullptr;
+  for (int c = tid; c < COT; c += nthr) {
+    const int co = co0 + c;
+    const bool ok = co < a.Cout;
+    cst[c] = (a.bias && ok) ? a.bias[co] : 0.f;
+    cst[COT + c] = (fbwd && ok) ? a.bb.mean[co] : 0.f;
+    cst[2 * COT + c] = (fbwd && ok) ? a.bb.invstd[co] : 0.f;
+  }
+}
+
+// Block reduction of the BN sums (16 pixel lanes, then the NW waves through
+// LDS at `scratch`), fp64 atomics into replica blockIdx.x % kStatRep, and the
+// optional last-block finalisation.
+template <int FN, int NW>
+__device__ __forceinline__ void commit_stats(const ConvFwdArgs& a, float (&q0)[FN][4], float (&q1)[FN][4], int co0,
+                                             char* scratch) {
+  constexpr int COT = FN * 16;
+  const BnBwdArgs& bb = a.bb;
+  const bool fbwd = bb.sums != nullptr;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -281,7 +260,7 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
         q0[i][e] += __shfl_xor(q0[i][e], o, 64);
         q1[i][e] += __shfl_xor(q1[i][e], o, 64);
       }
-  float* red = reinterpret_cast<float*>(smem);  // [NW][COT][2]; all LDS reads above are done
+  float* red = reinterpret_cast<float*>(scratch);  // [NW][COT][2]
   __syncthreads();
   if ((lane & 15) == 0) {
 #pragma unroll
@@ -311,18 +290,186 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
   }
   unsigned* ticket = fbwd ? bb.ticket : a.bn.ticket;
   if (ticket) {
-    int* flag = reinterpret_cast<int*>(smem + NW * COT * 2 * sizeof(float));
-    if (last_block_arrive(ticket, gridDim.x, flag, tid < COT)) {
+    int* flag = reinterpret_cast<int*>(scratch + NW * COT * 2 * sizeof(float));
+    if (last_block_arrive(ticket, gridDim.x * gridDim.y * gridDim.z, flag, tid < COT)) {
       if (fbwd) bn_bwd_finalize(bb);
       else bn_finalize(a.bn);
     }
   }
 }
 
+// ---------------------------------------------------------------------------
+// weight-stationary (C = 32 * NP <= 96)
+// ---------------------------------------------------------------------------
+template <int NP, int FN, int TH, int NW, bool FLIP>
+__global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int ntiles, int ncg) {
+  constexpr int COT = FN * 16;               // output channels per block
+  constexpr int RW = TH / NW;                // output rows per wave
+  constexpr int HPR = ((TH + 2) * kHW + 15) / 16 * 16;
+  constexpr int PANEL = HPR * 64;
+  constexpr int HBUF = NP * PANEL;
+  constexpr int WBYTES = 9 * NP * COT * 64;
+  constexpr bool PREF = FLIP && RW * FN <= 8;
+  static_assert(TH % NW == 0 && RW >= 1, "rows per wave");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* wl = smem;
+  char* hl = smem + WBYTES;
+  float* cst = reinterpret_cast<float*>(hl + 2 * HBUF);  // [3][COT]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cg = blockIdx.x % ncg;
+  const int nslot = gridDim.x / ncg;
+  const int co0 = cg * COT;
+  const int tq = a.Q >> 4, tp = a.P / TH;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (unsigned)((size_t)a.Cout * 9 * a.C * 2));
+
+  issue_weight_dma<COT, NW>(a, wr, wl, co0, 0, NP, wave, lane);  // all 9 taps, once
+  load_epi_constants<COT>(a, cst, co0, tid, NW * 64);
+  float q0[FN][4], q1[FN][4];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) q0[i][e] = q1[i][e] = 0.f;
+
+  // loop-invariant fragment offsets: weights (16 co rows from co = 0) and the
+  // halo rows this wave's output rows need for every tap shift
+  const int aoff = ws_off(lane & 15, lane >> 4);
+  int boff[RW + 2][3];
+#pragma unroll
+  for (int h = 0; h < RW + 2; ++h)
+#pragma unroll
+    for (int d = 0; d < 3; ++d) boff[h][d] = ws_off((wave * RW + h) * kHW + d + (lane & 15), lane >> 4);
+
+  auto tile_origin = [&](int t, int& n, int& oh0, int& ow0) {
+    n = t / (tp * tq);
+    const int rem = t - n * (tp * tq);
+    oh0 = (rem / tq) * TH;
+    ow0 = (rem % tq) << 4;
+  };
+
+  int t = blockIdx.x / ncg;
+  if (t < ntiles) {
+    int n, oh0, ow0;
+    tile_origin(t, n, oh0, ow0);
+    issue_halo_dma<TH, NW>(a, xr, hl, n, oh0, ow0, 0, NP, wave, lane);
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+
+  for (int k = 0; t < ntiles; ++k, t += nslot) {
+    const int b = k & 1;
+    if (t + nslot < ntiles) {  // lands while this tile computes
+      int n, oh0, ow0;
+      tile_origin(t + nslot, n, oh0, ow0);
+      issue_halo_dma<TH, NW>(a, xr, hl + (b ^ 1) * HBUF, n, oh0, ow0, 0, NP, wave, lane);
+    }
+    int n, oh0, ow0;
+    tile_origin(t, n, oh0, ow0);
+    size_t pix[RW];
+#pragma unroll
+    for (int j = 0; j < RW; ++j) pix[j] = ((size_t)n * a.P + oh0 + wave * RW + j) * a.Q + ow0 + (lane & 15);
+    TileEpi<FN, RW, FLIP, PREF> epi;
+    if (PREF) epi.fetch(a, pix, co0, lane);
+    const char* H = hl + b * HBUF;
+    f32x4 acc[RW][FN];
+#pragma unroll
+    for (int j = 0; j < RW; ++j)
+#pragma unroll
+      for (int i = 0; i < FN; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+      mfma_panel<FN, RW, NP * COT * 64, FLIP>(acc, wl + p * COT * 64, H + p * PANEL, aoff, boff);
+    if (!PREF) epi.fetch(a, pix, co0, lane);
+    epi.landed();
+    epi.store(a, acc, pix, co0, lane, cst, q0, q1);
+    wait_vmcnt<0>();               // the next tile's halo has landed (this wave's part)
+    __builtin_amdgcn_s_barrier();  // ... everyone's part; buffer b is free for reuse
+  }
+  if (a.stats || a.bb.sums) commit_stats<FN, NW>(a, q0, q1, co0, smem);
+}
+
+// ---------------------------------------------------------------------------
+// halo-streamed (C >= 128, multiple of 32): one TH x 16 x COT output tile per
+// block, K loop over 32-channel chunks, stage = halo panel + 9 weight taps
+// ---------------------------------------------------------------------------
+template <int FN, int TH, int NW, bool FLIP>
+__global__ void __launch_bounds__(NW * 64) conv3x3_hs_kernel(ConvFwdArgs a, int ncb) {
+  constexpr int COT = FN * 16;
+  constexpr int RW = TH / NW;
+  constexpr int HPR = ((TH + 2) * kHW + 15) / 16 * 16;
+  constexpr int HBYTES = HPR * 64;
+  constexpr int WBYTES = 9 * COT * 64;
+  constexpr int STAGE = HBYTES + WBYTES;
+  constexpr bool PREF = FLIP && RW * FN <= 8;
+  static_assert(TH % NW == 0 && RW >= 1, "rows per wave");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* cst = reinterpret_cast<float*>(smem + 2 * STAGE);  // [3][COT]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int cob = bid % ncb, tile = bid / ncb;
+  const int co0 = cob * COT;
+  const int tq = a.Q >> 4, tp = a.P / TH;
+  const int n = tile / (tp * tq);
+  const int rem = tile - n * (tp * tq);
+  const int oh0 = (rem / tq) * TH, ow0 = (rem % tq) << 4;
+  const int KC = a.C >> 5;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (unsigned)((size_t)a.Cout * 9 * a.C * 2));
+
+  auto issue = [&](int kc, int b) {
+    char* S = smem + b * STAGE;
+    issue_halo_dma<TH, NW>(a, xr, S, n, oh0, ow0, kc * 32, 1, wave, lane);
+    issue_weight_dma<COT, NW>(a, wr, S + HBYTES, co0, kc * 32, 1, wave, lane);
+  };
+  issue(0, 0);
+  load_epi_constants<COT>(a, cst, co0, tid, NW * 64);
+
+  const int aoff = ws_off(lane & 15, lane >> 4);
+  int boff[RW + 2][3];
+#pragma unroll
+  for (int h = 0; h < RW + 2; ++h)
+#pragma unroll
+    for (int d = 0; d < 3; ++d) boff[h][d] = ws_off((wave * RW + h) * kHW + d + (lane & 15), lane >> 4);
+  size_t pix[RW];
+#pragma unroll
+  for (int j = 0; j < RW; ++j) pix[j] = ((size_t)n * a.P + oh0 + wave * RW + j) * a.Q + ow0 + (lane & 15);
+
+  f32x4 acc[RW][FN];
+#pragma unroll
+  for (int j = 0; j < RW; ++j)
+#pragma unroll
+    for (int i = 0; i < FN; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  TileEpi<FN, RW, FLIP, PREF> epi;
+  for (int kc = 0; kc < KC; ++kc) {
+    wait_vmcnt<0>();               // stage kc landed (this wave's part) ...
+    __builtin_amdgcn_s_barrier();  // ... everyone's; and stage kc-1 is no longer read
+    if (kc + 1 < KC) issue(kc + 1, (kc + 1) & 1);
+    else if (PREF) epi.fetch(a, pix, co0, lane);  // epilogue operands ride beside the last chunk
+    const char* S = smem + (kc & 1) * STAGE;
+    mfma_panel<FN, RW, COT * 64, FLIP>(acc, S + HBYTES, S, aoff, boff);
+  }
+  if (!PREF) epi.fetch(a, pix, co0, lane);
+  epi.landed();
+  float q0[FN][4], q1[FN][4];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) q0[i][e] = q1[i][e] = 0.f;
+  epi.store(a, acc, pix, co0, lane, cst, q0, q1);
+  if (a.stats || a.bb.sums) commit_stats<FN, NW>(a, q0, q1, co0, smem);
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
 template <int NP, int FN, int TH, int NW, bool FLIP>
 static hipError_t launch_ws(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int COT = FN * 16;
-  constexpr int HPR = ((TH + 2) * 18 + 15) / 16 * 16;
+  constexpr int HPR = ((TH + 2) * kHW + 15) / 16 * 16;
   constexpr size_t lds = (size_t)9 * NP * COT * 64 + 2 * (size_t)NP * HPR * 64 + 3 * COT * sizeof(float);
   static_assert(lds <= 163840, "LDS");
   const int ncg = (a.Cout + COT - 1) / COT;
@@ -339,34 +486,61 @@ static hipError_t launch_ws(const ConvFwdArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <int FN, int TH, int NW, bool FLIP>
+static hipError_t launch_hs(const ConvFwdArgs& a, hipStream_t st) {
+  constexpr int COT = FN * 16;
+  constexpr int HPR = ((TH + 2) * kHW + 15) / 16 * 16;
+  constexpr size_t lds = 2 * ((size_t)HPR * 64 + 9 * COT * 64) + 3 * COT * sizeof(float);
+  static_assert(lds <= 163840, "LDS");
+  if (a.Cout % COT || a.P % TH) return hipErrorNotSupported;
+  const int ncb = a.Cout / COT;
+  const int ntiles = a.N * (a.P / TH) * (a.Q / 16);
+  char tag[96];
+  std::snprintf(tag, sizeof(tag), "conv3x3_hs_kernel<%d, %d, %d, %s>", FN, TH, NW, FLIP ? "true" : "false");
+  conv_kernel_tag(tag);
+  hipLaunchKernelGGL((conv3x3_hs_kernel<FN, TH, NW, FLIP>), dim3(ntiles * ncb), dim3(NW * 64), lds, st, a, ncb);
+  return hipGetLastError();
+}
+
 template <bool FLIP>
-static hipError_t launch_ws_shape(const ConvFwdArgs& a, hipStream_t st) {
+static hipError_t launch_halo_shape(const ConvFwdArgs& a, hipStream_t st) {
   const int C = a.C, Co = a.Cout;
+  // weight-stationary: every tap of the block's channels fits in LDS
   if (C == 64 && Co % 64 == 0 && a.P % 16 == 0) return launch_ws<2, 4, 16, 8, FLIP>(a, st);
   if (C == 32 && Co == 32 && a.P % 16 == 0) return launch_ws<1, 2, 16, 4, FLIP>(a, st);
   if (C == 32 && Co == 96 && a.P % 16 == 0) return launch_ws<1, 6, 16, 8, FLIP>(a, st);
   if (C == 32 && Co % 64 == 0 && a.P % 16 == 0) return launch_ws<1, 4, 16, 8, FLIP>(a, st);
   if (C == 96 && Co == 32 && a.P % 8 == 0) return launch_ws<3, 2, 8, 4, FLIP>(a, st);
+  // halo-streamed: 256-pixel tiles while they still give >= ~1 block per CU
+  if (C % 32 == 0 && C >= 128 && Co % 64 == 0) {
+    const long long t16 = (long long)a.N * (a.P / 16) * (a.Q / 16) * (Co / 64);
+    // measured exception: a 4-chunk K loop (C = 128) over two rounds of
+    // blocks (enc2 forward) is faster as a 128x128 im2col tile
+    if (!FLIP && C == 128 && t16 > 256 && t16 <= 512) return hipErrorNotSupported;
+    if (a.P % 16 == 0 && t16 >= 256) return launch_hs<4, 16, 8, FLIP>(a, st);
+    if (a.P % 8 == 0) return launch_hs<4, 8, 4, FLIP>(a, st);
+  }
   return hipErrorNotSupported;
 }
 
-static int g_ws_disabled = std::getenv("UNET_NO_WS") != nullptr;  // A/B switch for measurements
-void set_conv_ws(int on) { g_ws_disabled = on ? 0 : 1; }
+static int g_halo_disabled = std::getenv("UNET_NO_HALO") != nullptr;  // A/B switch for measurements
+void set_conv_ws(int on) { g_halo_disabled = on ? 0 : 1; }
 
 // 3x3 / s1 / p1 conv (mode 0) or its data gradient (mode 1, dgrad weight pack)
 // when the shape is covered; hipErrorNotSupported otherwise (the caller falls
 // back to the implicit-GEMM kernel).
 hipError_t launch_conv3x3_ws(const ConvFwdArgs& a, int mode, hipStream_t st) {
-  if (g_ws_disabled) return hipErrorNotSupported;
+  if (g_halo_disabled) return hipErrorNotSupported;
   if (a.R != 3 || a.S != 3 || a.stride != 1 || a.pad != 1) return hipErrorNotSupported;
   if (a.H != a.P || a.W != a.Q || a.Q % 16 || a.ldx % 8 || a.ldy % 4) return hipErrorNotSupported;
-  // no second BN (downsample) in the fused backward epilogue: those layers
-  // are never 3x3 s1 with <= 96 channels
+  // no second BN (downsample) in the fused backward epilogue: a 3x3 s1 conv
+  // never produces dA of a downsample block's BN pair
   if ((a.add && a.ldadd % 4) || (a.bb.sums && (a.bb.y2 || a.bb.ldact % 4 || a.bb.ldy % 4)))
     return hipErrorNotSupported;
   if ((size_t)a.N * a.H * a.W * a.ldx * 2 >= 0x80000000ull) return hipErrorNotSupported;
+  if ((size_t)a.Cout * 9 * a.C * 2 >= 0x80000000ull) return hipErrorNotSupported;
   if (mode == 0 && (a.add || a.bb.sums)) return hipErrorNotSupported;  // forward epilogue: bias + BN sums only
-  return mode == 0 ? launch_ws_shape<false>(a, st) : launch_ws_shape<true>(a, st);
+  return mode == 0 ? launch_halo_shape<false>(a, st) : launch_halo_shape<true>(a, st);
 }
 
 }  // namespace unet

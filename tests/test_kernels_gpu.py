@@ -110,6 +110,10 @@ CASES_DGRAD = [  # N, Ci, H, Co, R, stride, pad  (forward geometry)
     (8, 64, 128, 64, 3, 1, 1),
     (4, 96, 128, 32, 3, 1, 1),
     (4, 128, 64, 64, 3, 1, 1),
+    # halo-streamed kernel (C >= 128): 256- and 128-pixel tiles
+    (4, 256, 32, 256, 3, 1, 1),
+    (2, 512, 16, 512, 3, 1, 1),
+    (2, 128, 64, 256, 3, 1, 1),
 ]
 
 
