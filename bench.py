@@ -30,9 +30,11 @@ def pmc_traffic(kernel: str):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (scripts/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md
     HBM section), or None when that kernel was not profiled."""
-    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if not os.path.exists(path):
+    import glob
+    found = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "*", "pmc_traffic.json")))
+    if not found:
         return None
+    path = found[-1]  # newest profiling session of the newest round
     with open(path) as f:
         table = json.load(f)
     ent = table.get(kernel)

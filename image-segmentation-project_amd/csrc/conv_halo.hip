@@ -125,9 +125,10 @@ __device__ __forceinline__ void mfma_panel(f32x4 (&acc)[RW][FN], const char* W, 
 // activation, raw conv output of the BN) are fetched by fetch(): early with
 // untracked loads (PREF) so their latency hides behind MFMA work, else right
 // before use; landed() is the matching wait.
-template <int FN, int RW, bool FLIP, bool PREF>
+template <int FN, int RW, bool FLIP, bool PREF, bool TWO>
 struct TileEpi {
   uint2 uadd[RW][FN], uact[RW][FN], uy[RW][FN];
+  uint2 uy2[TWO ? RW : 1][TWO ? FN : 1];  // raw conv output of the second BN (downsample pair)
 
   __device__ __forceinline__ void fetch(const ConvFwdArgs& a, const size_t (&pix)[RW], int co0, int lane) {
     if (!FLIP) return;
@@ -157,6 +158,10 @@ struct TileEpi {
           const void* s2 = bb.y + pix[j] * bb.ldy + co;
           uact[j][i] = PREF ? ld_u2_asm(s1) : *reinterpret_cast<const uint2*>(s1);
           uy[j][i] = PREF ? ld_u2_asm(s2) : *reinterpret_cast<const uint2*>(s2);
+          if constexpr (TWO) {
+            const void* s3 = bb.y2 + pix[j] * bb.ldy2 + co;
+            uy2[j][i] = PREF ? ld_u2_asm(s3) : *reinterpret_cast<const uint2*>(s3);
+          }
         }
     } else {
 #pragma unroll
@@ -175,11 +180,17 @@ struct TileEpi {
       for (int i = 0; i < FN; ++i)  // order every use after the wait
         asm volatile("" : "+v"(uadd[j][i].x), "+v"(uadd[j][i].y), "+v"(uact[j][i].x), "+v"(uact[j][i].y),
                      "+v"(uy[j][i].x), "+v"(uy[j][i].y));
+    if constexpr (TWO) {
+#pragma unroll
+      for (int j = 0; j < RW; ++j)
+#pragma unroll
+        for (int i = 0; i < FN; ++i) asm volatile("" : "+v"(uy2[j][i].x), "+v"(uy2[j][i].y));
+    }
   }
 
   __device__ __forceinline__ void store(const ConvFwdArgs& a, const f32x4 (&acc)[RW][FN], const size_t (&pix)[RW],
                                         int co0, int lane, const float* cst, float (&q0)[FN][4],
-                                        float (&q1)[FN][4]) {
+                                        float (&q1)[FN][4], float (&q2)[FN][4]) {
     constexpr int COT = FN * 16;
     const bool fbwd = a.bb.sums != nullptr;
     const bool stats = a.stats != nullptr || fbwd;
@@ -219,6 +230,13 @@ struct TileEpi {
             q0[i][e] += dz[e];
             q1[i][e] += dz[e] * (yv[e] - cst[COT + cl + e]) * cst[2 * COT + cl + e];
           }
+          if constexpr (TWO) {
+            const uint2 w = uy2[j][i];
+            const float y2[4] = {__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+                                 __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) q2[i][e] += dz[e] * (y2[e] - cst[3 * COT + cl + e]) * cst[4 * COT + cl + e];
+          }
         } else if (stats) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) { q0[i][e] += v[e]; q1[i][e] += v[e] * v[e]; }
@@ -228,25 +246,29 @@ struct TileEpi {
   }
 };
 
-// bias | mean | invstd of the block's COT channels into LDS
+// bias | mean | invstd | mean2 | invstd2 of the block's COT channels into LDS
+constexpr int kEpiConsts = 5;
 template <int COT>
 __device__ __forceinline__ void load_epi_constants(const ConvFwdArgs& a, float* cst, int co0, int tid, int nthr) {
   const bool fbwd = a.bb.sums != nullptr;
+  const bool two = fbwd && a.bb.y2 != nullptr;
   for (int c = tid; c < COT; c += nthr) {
     const int co = co0 + c;
     const bool ok = co < a.Cout;
     cst[c] = (a.bias && ok) ? a.bias[co] : 0.f;
     cst[COT + c] = (fbwd && ok) ? a.bb.mean[co] : 0.f;
     cst[2 * COT + c] = (fbwd && ok) ? a.bb.invstd[co] : 0.f;
+    cst[3 * COT + c] = (two && ok) ? a.bb.mean2[co] : 0.f;
+    cst[4 * COT + c] = (two && ok) ? a.bb.invstd2[co] : 0.f;
   }
 }
 
 // Block reduction of the BN sums (16 pixel lanes, then the NW waves through
 // LDS at `scratch`), fp64 atomics into replica blockIdx.x % kStatRep, and the
 // optional last-block finalisation.
-template <int FN, int NW>
-__device__ __forceinline__ void commit_stats(const ConvFwdArgs& a, float (&q0)[FN][4], float (&q1)[FN][4], int co0,
-                                             char* scratch) {
+template <int FN, int NW, bool TWO>
+__device__ __forceinline__ void commit_stats(const ConvFwdArgs& a, float (&q0)[FN][4], float (&q1)[FN][4],
+                                             float (&q2)[FN][4], int co0, char* scratch) {
   constexpr int COT = FN * 16;
   const BnBwdArgs& bb = a.bb;
   const bool fbwd = bb.sums != nullptr;
@@ -259,8 +281,9 @@ __device__ __forceinline__ void commit_stats(const ConvFwdArgs& a, float (&q0)[F
       for (int o = 1; o < 16; o <<= 1) {
         q0[i][e] += __shfl_xor(q0[i][e], o, 64);
         q1[i][e] += __shfl_xor(q1[i][e], o, 64);
+        if (TWO) q2[i][e] += __shfl_xor(q2[i][e], o, 64);
       }
-  float* red = reinterpret_cast<float*>(scratch);  // [NW][COT][2]
+  float* red = reinterpret_cast<float*>(scratch);  // [NW][COT][3]
   __syncthreads();
   if ((lane & 15) == 0) {
 #pragma unroll
@@ -268,29 +291,32 @@ __device__ __forceinline__ void commit_stats(const ConvFwdArgs& a, float (&q0)[F
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int cl = i * 16 + ((lane >> 4) << 2) + e;
-        red[(wave * COT + cl) * 2 + 0] = q0[i][e];
-        red[(wave * COT + cl) * 2 + 1] = q1[i][e];
+        red[(wave * COT + cl) * 3 + 0] = q0[i][e];
+        red[(wave * COT + cl) * 3 + 1] = q1[i][e];
+        red[(wave * COT + cl) * 3 + 2] = TWO ? q2[i][e] : 0.f;
       }
   }
   __syncthreads();
   for (int cl = tid; cl < COT; cl += NW * 64) {
     const int co = co0 + cl;
     if (co < a.Cout) {
-      float s0 = 0.f, s1 = 0.f;
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int w = 0; w < NW; ++w) {
-        s0 += red[(w * COT + cl) * 2];
-        s1 += red[(w * COT + cl) * 2 + 1];
+        s0 += red[(w * COT + cl) * 3];
+        s1 += red[(w * COT + cl) * 3 + 1];
+        s2 += red[(w * COT + cl) * 3 + 2];
       }
       const size_t rep = (size_t)(blockIdx.x % kStatRep) * 2 * a.Cout;
       double* dst = fbwd ? bb.sums + rep : a.stats + rep;
       atomicAdd(dst + co, (double)s0);
       atomicAdd(dst + a.Cout + co, (double)s1);
+      if (TWO) atomicAdd(bb.sums2 + rep + a.Cout + co, (double)s2);
     }
   }
   unsigned* ticket = fbwd ? bb.ticket : a.bn.ticket;
   if (ticket) {
-    int* flag = reinterpret_cast<int*>(scratch + NW * COT * 2 * sizeof(float));
+    int* flag = reinterpret_cast<int*>(scratch + NW * COT * 3 * sizeof(float));
     if (last_block_arrive(ticket, gridDim.x * gridDim.y * gridDim.z, flag, tid < COT)) {
       if (fbwd) bn_bwd_finalize(bb);
       else bn_finalize(a.bn);
@@ -314,7 +340,7 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* wl = smem;
   char* hl = smem + WBYTES;
-  float* cst = reinterpret_cast<float*>(hl + 2 * HBUF);  // [3][COT]
+  float* cst = reinterpret_cast<float*>(hl + 2 * HBUF);  // [kEpiConsts][COT]
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -327,11 +353,11 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
 
   issue_weight_dma<COT, NW>(a, wr, wl, co0, 0, NP, wave, lane);  // all 9 taps, once
   load_epi_constants<COT>(a, cst, co0, tid, NW * 64);
-  float q0[FN][4], q1[FN][4];
+  float q0[FN][4], q1[FN][4], q2[FN][4];
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) q0[i][e] = q1[i][e] = 0.f;
+    for (int e = 0; e < 4; ++e) q0[i][e] = q1[i][e] = q2[i][e] = 0.f;
 
   // loop-invariant fragment offsets: weights (16 co rows from co = 0) and the
   // halo rows this wave's output rows need for every tap shift
@@ -370,7 +396,7 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
     size_t pix[RW];
 #pragma unroll
     for (int j = 0; j < RW; ++j) pix[j] = ((size_t)n * a.P + oh0 + wave * RW + j) * a.Q + ow0 + (lane & 15);
-    TileEpi<FN, RW, FLIP, PREF> epi;
+    TileEpi<FN, RW, FLIP, PREF, false> epi;
     if (PREF) epi.fetch(a, pix, co0, lane);
     const char* H = hl + b * HBUF;
     f32x4 acc[RW][FN];
@@ -383,18 +409,18 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
       mfma_panel<FN, RW, NP * COT * 64, FLIP>(acc, wl + p * COT * 64, H + p * PANEL, aoff, boff);
     if (!PREF) epi.fetch(a, pix, co0, lane);
     epi.landed();
-    epi.store(a, acc, pix, co0, lane, cst, q0, q1);
+    epi.store(a, acc, pix, co0, lane, cst, q0, q1, q2);
     wait_vmcnt<0>();               // the next tile's halo has landed (this wave's part)
     __builtin_amdgcn_s_barrier();  // ... everyone's part; buffer b is free for reuse
   }
-  if (a.stats || a.bb.sums) commit_stats<FN, NW>(a, q0, q1, co0, smem);
+  if (a.stats || a.bb.sums) commit_stats<FN, NW, false>(a, q0, q1, q2, co0, smem);
 }
 
 // ---------------------------------------------------------------------------
 // halo-streamed (C >= 128, multiple of 32): one TH x 16 x COT output tile per
 // block, K loop over 32-channel chunks, stage = halo panel + 9 weight taps
 // ---------------------------------------------------------------------------
-template <int FN, int TH, int NW, bool FLIP>
+template <int FN, int TH, int NW, bool FLIP, bool TWO>
 __global__ void __launch_bounds__(NW * 64) conv3x3_hs_kernel(ConvFwdArgs a, int ncb) {
   constexpr int COT = FN * 16;
   constexpr int RW = TH / NW;
@@ -405,7 +431,7 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_hs_kernel(ConvFwdArgs a, int 
   constexpr bool PREF = FLIP && RW * FN <= 8;
   static_assert(TH % NW == 0 && RW >= 1, "rows per wave");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* cst = reinterpret_cast<float*>(smem + 2 * STAGE);  // [3][COT]
+  float* cst = reinterpret_cast<float*>(smem + 2 * STAGE);  // [kEpiConsts][COT]
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -443,7 +469,7 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_hs_kernel(ConvFwdArgs a, int 
   for (int j = 0; j < RW; ++j)
 #pragma unroll
     for (int i = 0; i < FN; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  TileEpi<FN, RW, FLIP, PREF> epi;
+  TileEpi<FN, RW, FLIP, PREF, TWO> epi;
   for (int kc = 0; kc < KC; ++kc) {
     wait_vmcnt<0>();               // stage kc landed (this wave's part) ...
     __builtin_amdgcn_s_barrier();  // ... everyone's; and stage kc-1 is no longer read
@@ -454,13 +480,13 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_hs_kernel(ConvFwdArgs a, int 
   }
   if (!PREF) epi.fetch(a, pix, co0, lane);
   epi.landed();
-  float q0[FN][4], q1[FN][4];
+  float q0[FN][4], q1[FN][4], q2[FN][4];
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) q0[i][e] = q1[i][e] = 0.f;
-  epi.store(a, acc, pix, co0, lane, cst, q0, q1);
-  if (a.stats || a.bb.sums) commit_stats<FN, NW>(a, q0, q1, co0, smem);
+    for (int e = 0; e < 4; ++e) q0[i][e] = q1[i][e] = q2[i][e] = 0.f;
+  epi.store(a, acc, pix, co0, lane, cst, q0, q1, q2);
+  if (a.stats || a.bb.sums) commit_stats<FN, NW, TWO>(a, q0, q1, q2, co0, smem);
 }
 
 // ---------------------------------------------------------------------------
@@ -470,7 +496,7 @@ template <int NP, int FN, int TH, int NW, bool FLIP>
 static hipError_t launch_ws(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int COT = FN * 16;
   constexpr int HPR = ((TH + 2) * kHW + 15) / 16 * 16;
-  constexpr size_t lds = (size_t)9 * NP * COT * 64 + 2 * (size_t)NP * HPR * 64 + 3 * COT * sizeof(float);
+  constexpr size_t lds = (size_t)9 * NP * COT * 64 + 2 * (size_t)NP * HPR * 64 + kEpiConsts * COT * sizeof(float);
   static_assert(lds <= 163840, "LDS");
   const int ncg = (a.Cout + COT - 1) / COT;
   const int ntiles = a.N * (a.P / TH) * (a.Q / 16);
@@ -486,25 +512,36 @@ static hipError_t launch_ws(const ConvFwdArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <int FN, int TH, int NW, bool FLIP>
+template <int FN, int TH, int NW, bool FLIP, bool TWO>
 static hipError_t launch_hs(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int COT = FN * 16;
   constexpr int HPR = ((TH + 2) * kHW + 15) / 16 * 16;
-  constexpr size_t lds = 2 * ((size_t)HPR * 64 + 9 * COT * 64) + 3 * COT * sizeof(float);
+  constexpr size_t lds = 2 * ((size_t)HPR * 64 + 9 * COT * 64) + kEpiConsts * COT * sizeof(float);
   static_assert(lds <= 163840, "LDS");
   if (a.Cout % COT || a.P % TH) return hipErrorNotSupported;
   const int ncb = a.Cout / COT;
   const int ntiles = a.N * (a.P / TH) * (a.Q / 16);
   char tag[96];
-  std::snprintf(tag, sizeof(tag), "conv3x3_hs_kernel<%d, %d, %d, %s>", FN, TH, NW, FLIP ? "true" : "false");
+  std::snprintf(tag, sizeof(tag), "conv3x3_hs_kernel<%d, %d, %d, %s, %s>", FN, TH, NW, FLIP ? "true" : "false",
+                TWO ? "true" : "false");
   conv_kernel_tag(tag);
-  hipLaunchKernelGGL((conv3x3_hs_kernel<FN, TH, NW, FLIP>), dim3(ntiles * ncb), dim3(NW * 64), lds, st, a, ncb);
+  hipLaunchKernelGGL((conv3x3_hs_kernel<FN, TH, NW, FLIP, TWO>), dim3(ntiles * ncb), dim3(NW * 64), lds, st, a,
+                     ncb);
   return hipGetLastError();
 }
 
 template <bool FLIP>
 static hipError_t launch_halo_shape(const ConvFwdArgs& a, hipStream_t st) {
   const int C = a.C, Co = a.Cout;
+  // dgrad producing dA of a downsample block's BN pair (bn2 + downsample BN):
+  // the halo-streamed kernel with the two-BN epilogue
+  if (FLIP && a.bb.sums && a.bb.y2) {
+    if (!(C % 32 == 0 && C >= 128 && Co % 64 == 0)) return hipErrorNotSupported;
+    const long long t16 = (long long)a.N * (a.P / 16) * (a.Q / 16) * (Co / 64);
+    if (a.P % 16 == 0 && t16 >= 256) return launch_hs<4, 16, 8, true, true>(a, st);
+    if (a.P % 8 == 0) return launch_hs<4, 8, 4, true, true>(a, st);
+    return hipErrorNotSupported;
+  }
   // weight-stationary: every tap of the block's channels fits in LDS
   if (C == 64 && Co % 64 == 0 && a.P % 16 == 0) return launch_ws<2, 4, 16, 8, FLIP>(a, st);
   if (C == 32 && Co == 32 && a.P % 16 == 0) return launch_ws<1, 2, 16, 4, FLIP>(a, st);
@@ -517,8 +554,8 @@ static hipError_t launch_halo_shape(const ConvFwdArgs& a, hipStream_t st) {
     // measured exception: a 4-chunk K loop (C = 128) over two rounds of
     // blocks (enc2 forward) is faster as a 128x128 im2col tile
     if (!FLIP && C == 128 && t16 > 256 && t16 <= 512) return hipErrorNotSupported;
-    if (a.P % 16 == 0 && t16 >= 256) return launch_hs<4, 16, 8, FLIP>(a, st);
-    if (a.P % 8 == 0) return launch_hs<4, 8, 4, FLIP>(a, st);
+    if (a.P % 16 == 0 && t16 >= 256) return launch_hs<4, 16, 8, FLIP, false>(a, st);
+    if (a.P % 8 == 0) return launch_hs<4, 8, 4, FLIP, false>(a, st);
   }
   return hipErrorNotSupported;
 }
@@ -530,12 +567,12 @@ void set_conv_ws(int on) { g_halo_disabled = on ? 0 : 1; }
 // when the shape is covered; hipErrorNotSupported otherwise (the caller falls
 // back to the implicit-GEMM kernel).
 hipError_t launch_conv3x3_ws(const ConvFwdArgs& a, int mode, hipStream_t st) {
-  if (g_halo_disabled) return hipErrorNotSupported;
+  if (g_halo_disabled || a.x2) return hipErrorNotSupported;
   if (a.R != 3 || a.S != 3 || a.stride != 1 || a.pad != 1) return hipErrorNotSupported;
   if (a.H != a.P || a.W != a.Q || a.Q % 16 || a.ldx % 8 || a.ldy % 4) return hipErrorNotSupported;
-  // no second BN (downsample) in the fused backward epilogue: a 3x3 s1 conv
-  // never produces dA of a downsample block's BN pair
-  if ((a.add && a.ldadd % 4) || (a.bb.sums && (a.bb.y2 || a.bb.ldact % 4 || a.bb.ldy % 4)))
+  // fused BN-backward epilogue operands are read 4 channels (8 B) at a time
+  if ((a.add && a.ldadd % 4) ||
+      (a.bb.sums && (a.bb.ldact % 4 || a.bb.ldy % 4 || (a.bb.y2 && a.bb.ldy2 % 4))))
     return hipErrorNotSupported;
   if ((size_t)a.N * a.H * a.W * a.ldx * 2 >= 0x80000000ull) return hipErrorNotSupported;
   if ((size_t)a.Cout * 9 * a.C * 2 >= 0x80000000ull) return hipErrorNotSupported;

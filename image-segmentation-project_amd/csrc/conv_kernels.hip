@@ -266,6 +266,36 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x4 (&acc)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
   const int st = a.stride, Pc = a.Pc, Qc = a.Qc;
+  if constexpr (MODE == MODE_SHUF) {
+    // column j = t*Co + co of input pixel (n, pa, pb) -> y[n, 2pa + t/2, 2pb + t%2, co]
+    // (+ bias[co]); a lane's 4 consecutive columns share t (Co % 4 == 0)
+    const int Co = a.Cout >> 2;
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      const int m = m0 + wm * WTM + j * 16 + (lane & 15);
+      if (m >= Mtot) continue;
+      const int n = m / (Pc * Qc);
+      const int rem = m - n * (Pc * Qc);
+      const int pa = rem / Qc, pb = rem - pa * Qc;
+#pragma unroll
+      for (int i = 0; i < FN; ++i) {
+        const int jj = n0 + wn * WTN + i * 16 + ((lane >> 4) << 2);
+        if (jj >= a.Cout) continue;
+        const int t = jj / Co, co = jj - t * Co;
+        const size_t pix = (size_t)(n * a.P + 2 * pa + (t >> 1)) * a.Q + 2 * pb + (t & 1);
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if (a.bias) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += a.bias[co + e];
+        }
+        uint2 o;
+        o.x = pack_bf2(v[0], v[1]);
+        o.y = pack_bf2(v[2], v[3]);
+        *reinterpret_cast<uint2*>(a.y + pix * a.ldy + co) = o;
+      }
+    }
+    return;
+  }
   const BnBwdArgs& bb = a.bb;
   const bool fbwd = bb.sums != nullptr;
   const bool two = fbwd && bb.y2 != nullptr;
@@ -473,10 +503,15 @@ conv_glds_kernel(ConvFwdArgs a) {
     ti.st = 1; ti.r0 = 0; ti.s0 = 0; ti.nr = a.R; ti.ns = a.S;
   }
   const int cchunks = a.C / BK;
-  const int KT = ti.nr * ti.ns * cchunks;
+  const int KT1 = ti.nr * ti.ns * cchunks;
+  // folded downsample dgrad: class 0 continues its K loop over x2 / w2
+  const bool ext = MODE == MODE_TRANS && a.x2 != nullptr && cls == 0;
+  const int KT = KT1 + (ext ? a.C2 / BK : 0);
   const int Ktot = a.R * a.S * a.C;
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
   const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (unsigned)((size_t)a.Cout * Ktot * 2));
+  const __amdgpu_buffer_rsrc_t x2r = make_rsrc(ext ? a.x2 : a.x, ext ? (unsigned)((size_t)a.N * a.H * a.W * a.ldx2 * 2) : 0u);
+  const __amdgpu_buffer_rsrc_t w2r = make_rsrc(ext ? a.w2 : a.w, ext ? (unsigned)((size_t)a.Cout * a.C2 * 2) : 0u);
 
   // lane geometry inside one wave instruction
   const int lrow = lane / CPR, lslot = lane % CPR;
@@ -497,15 +532,39 @@ conv_glds_kernel(ConvFwdArgs a) {
     }
   }
   int bch[B_INS];
-  unsigned bbase[B_INS];
+  unsigned bbase[B_INS], bbase2[B_INS];
 #pragma unroll
   for (int j = 0; j < B_INS; ++j) {
     const int row = (wave * B_INS + j) * RPI + lrow;
     bch[j] = swz_chunk<BK>(row, lslot);
-    bbase[j] = (row < BN && n0 + row < a.Cout) ? (unsigned)((n0 + row) * Ktot) * 2u : kOOB;
+    const bool ok = row < BN && n0 + row < a.Cout;
+    int wrow = n0 + row;  // packed weight row of GEMM column n0 + row
+    if constexpr (MODE == MODE_SHUF) {  // column t*Co + co -> convT pack row co*4 + t
+      const int Co = a.Cout >> 2, t = wrow / Co;
+      wrow = (wrow - t * Co) * 4 + t;
+    }
+    bbase[j] = ok ? (unsigned)(wrow * Ktot) * 2u : kOOB;
+    bbase2[j] = ok ? (unsigned)((n0 + row) * a.C2) * 2u : kOOB;
   }
 
   auto issue = [&](int kt, int buf) {
+    if (ext && kt >= KT1) {  // downsample range: x2 at the class-0 pixel (aa, ab) itself
+      const int c0 = (kt - KT1) * BK;
+      char* As = smem + buf * STAGE;
+      char* Bs = As + A_BYTES;
+#pragma unroll
+      for (int j = 0; j < A_INS; ++j) {
+        unsigned off = kOOB;
+        if (an[j] >= 0) off = (unsigned)(((an[j] * a.H + aa[j]) * a.W + ab[j]) * a.ldx2 + c0 + ach[j] * 8) * 2u;
+        glds16(x2r, As + (wave * A_INS + j) * 1024, off);
+      }
+#pragma unroll
+      for (int j = 0; j < B_INS; ++j) {
+        const unsigned off = bbase2[j] == kOOB ? kOOB : bbase2[j] + (unsigned)(c0 + bch[j] * 8) * 2u;
+        glds16(w2r, Bs + (wave * B_INS + j) * 1024, off);
+      }
+      return;
+    }
     const int cc = kt % cchunks;
     const int tap = kt / cchunks;
     const int jr = tap / ti.ns, js = tap - jr * ti.ns;
@@ -516,7 +575,7 @@ conv_glds_kernel(ConvFwdArgs a) {
 #pragma unroll
     for (int j = 0; j < A_INS; ++j) {
       int ih, iw;
-      if constexpr (MODE == MODE_FWD) {
+      if constexpr (MODE != MODE_TRANS) {  // MODE_FWD, MODE_SHUF (1x1 over the input grid)
         ih = aa[j] * st - a.pad + r;
         iw = ab[j] * st - a.pad + s;
       } else {
@@ -1308,9 +1367,11 @@ static hipError_t launch_glds_fixed(const ConvFwdArgs& a, int classes, int cfg, 
 
 template <int MODE>
 static hipError_t launch_glds(const ConvFwdArgs& a, int classes, hipStream_t st) {
-  if (g_cfg_override > 0) {
-    const hipError_t e = launch_glds_fixed<MODE>(a, classes, g_cfg_override, st);
-    if (e != hipErrorNotSupported) return e;
+  if constexpr (MODE != MODE_SHUF) {  // tuning overrides: conv / dgrad shapes only
+    if (g_cfg_override > 0) {
+      const hipError_t e = launch_glds_fixed<MODE>(a, classes, g_cfg_override, st);
+      if (e != hipErrorNotSupported) return e;
+    }
   }
   // Selection measured by scripts/tune_conv.py on MI355X (Base config shapes,
   // profiles/r01/tune_conv*.txt): 8-wave 256x256 / 128x128 2-stage tiles
@@ -1339,7 +1400,21 @@ static bool g_use_glds = std::getenv("UNET_CONV_V1") == nullptr;  // A/B switch 
 void set_conv_impl(int glds) { g_use_glds = glds != 0; }
 
 hipError_t launch_conv_fwd(const ConvFwdArgs& a0, int mode, hipStream_t st) {
+  // the folded downsample range exists only in the LDS-DMA transposed kernel
+  if (a0.x2 && (!g_use_glds || mode != MODE_TRANS || a0.C2 != a0.C || a0.stride != 2 || a0.pad != 1))
+    return hipErrorInvalidValue;
   if (g_use_glds && mode == MODE_STEM) return launch_stem_fwd(a0, st);
+  if (mode == MODE_SHUF) {  // convT k2s2 forward: a0 holds the transposed-conv geometry
+    if (!g_use_glds || a0.R != 2 || a0.S != 2 || a0.stride != 2 || a0.pad != 0 || a0.Cout % 4 || a0.C % 32 ||
+        a0.P != 2 * a0.H || a0.Q != 2 * a0.W || a0.stats || a0.add || a0.bb.sums)
+      return hipErrorInvalidValue;
+    if ((size_t)a0.N * a0.H * a0.W * a0.ldx * 2 >= 0x80000000ull) return hipErrorInvalidValue;
+    ConvFwdArgs a = a0;
+    a.Cout = 4 * a0.Cout;
+    a.R = a.S = 1; a.stride = 1; a.pad = 0;
+    a.Pc = a.H; a.Qc = a.W;
+    return launch_glds<MODE_SHUF>(a, 1, st);
+  }
   if (g_use_glds && mode != MODE_STEM && a0.C % 32 == 0) {
     ConvFwdArgs a = a0;
     if ((size_t)a.N * a.H * a.W * a.ldx * 2 >= 0x80000000ull) return hipErrorInvalidValue;

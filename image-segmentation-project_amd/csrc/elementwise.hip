@@ -31,8 +31,8 @@ static inline int grid_for(int64_t work, int per_block, int cap = 2048) {
 // statistics: save_mean/save_invstd for the backward and the running stats
 // (momentum 0.1, unbiased variance), matching torch.nn.BatchNorm2d training.
 // ---------------------------------------------------------------------------
-__device__ void bn_finalize_block0(const BnLaunch& p, int tid, int nthreads) {
-  for (int c = tid; c < p.C; c += nthreads) {
+__device__ void bn_finalize_block0(const BnLaunch& p, int tid, int nthreads, int cbeg, int cend) {
+  for (int c = cbeg + tid; c < cend; c += nthreads) {
     float sc, sh, m, inv, var;
     bn_scale_shift(p, c, sc, sh, m, inv, var);
     if (p.training) {
@@ -46,69 +46,87 @@ __device__ void bn_finalize_block0(const BnLaunch& p, int tid, int nthreads) {
   }
 }
 
-// Thread layout for all per-channel elementwise kernels: chunk = tid % CC
-// (8 channels = one 16-B access), row = tid / CC; a thread keeps its chunk for
-// the whole grid-stride pixel loop, so per-channel coefficients live in
-// registers (no LDS, no bank conflicts) and loads are unrolled 2 pixels deep.
+// Thread layout of the per-channel BN kernels: a block covers one group of
+// CG channels (blockIdx.y; CG = 64 when C % 64 == 0, else C) so its
+// coefficient prologue reads CG channels' replica sums, not C; inside the
+// group chunk = tid % CC (8 channels = one 16-B access), row = tid / CC, and a
+// thread keeps its chunk for the whole grid-stride pixel loop (coefficients in
+// registers).  kBnPPT pixels per thread per pass; the first pass's loads are
+// issued BEFORE the coefficient prologue so the two latencies overlap.
+constexpr int kBnCG = 64;
+constexpr int kBnPPT = 4;
+__host__ __device__ __forceinline__ int bn_group(int C) { return C % kBnCG == 0 ? kBnCG : C; }
+
 __global__ void __launch_bounds__(256) bn_apply_kernel(BnApplyArgs a) {
-  const int CC = a.C >> 3;
+  const int CG = bn_group(a.C);
+  const int CC = CG >> 3;
   const int rows = blockDim.x / CC;
   const int chunk = threadIdx.x % CC, row = threadIdx.x / CC;
-  const int c8 = chunk << 3;
-  // per-channel affine coefficients: computed once per channel into LDS, then
-  // each thread keeps its 8 in registers
-  extern __shared__ __attribute__((aligned(16))) float coef[];  // [4][C]
-  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+  const int cg0 = blockIdx.y * CG;
+  const int c8 = cg0 + (chunk << 3);
+  constexpr int PPT = kBnPPT;
+  const int64_t stride = (int64_t)gridDim.x * rows;
+  uint4 uy[PPT], ur[PPT];
+  auto load = [&](int64_t base) {
+#pragma unroll
+    for (int u = 0; u < PPT; ++u) {
+      const int64_t pix = base + u * stride;
+      uy[u] = pix < a.npix ? *reinterpret_cast<const uint4*>(a.y + pix * a.ldy + c8) : make_uint4(0, 0, 0, 0);
+      ur[u] = (a.res_mode && pix < a.npix) ? *reinterpret_cast<const uint4*>(a.res + pix * a.ldr + c8)
+                                           : make_uint4(0, 0, 0, 0);
+    }
+  };
+  int64_t base = (int64_t)blockIdx.x * rows + row;
+  if (row < rows) load(base);
+  // per-channel affine coefficients of the group into LDS, then 8 per thread
+  // into registers
+  extern __shared__ __attribute__((aligned(16))) float coef[];  // [4][CG]
+  for (int c = threadIdx.x; c < CG; c += blockDim.x) {
+    const int ch = cg0 + c;
     float m, inv, var;
     if (a.bn.training && a.bn.ss) {  // finalised by the producing conv's last block
-      coef[c] = a.bn.ss[c];
-      coef[a.C + c] = a.bn.ss[a.C + c];
+      coef[c] = a.bn.ss[ch];
+      coef[CG + c] = a.bn.ss[a.C + ch];
     } else {
-      bn_scale_shift(a.bn, c, coef[c], coef[a.C + c], m, inv, var);
+      bn_scale_shift(a.bn, ch, coef[c], coef[CG + c], m, inv, var);
     }
     if (a.res_mode == 2) {
       if (a.bn2.training && a.bn2.ss) {
-        coef[2 * a.C + c] = a.bn2.ss[c];
-        coef[3 * a.C + c] = a.bn2.ss[a.C + c];
+        coef[2 * CG + c] = a.bn2.ss[ch];
+        coef[3 * CG + c] = a.bn2.ss[a.C + ch];
       } else {
-        bn_scale_shift(a.bn2, c, coef[2 * a.C + c], coef[3 * a.C + c], m, inv, var);
+        bn_scale_shift(a.bn2, ch, coef[2 * CG + c], coef[3 * CG + c], m, inv, var);
       }
     }
   }
   __syncthreads();
   float sc1[8], sh1[8], sc2[8], sh2[8];
+  const int l8 = chunk << 3;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    sc1[k] = coef[c8 + k];
-    sh1[k] = coef[a.C + c8 + k];
-    sc2[k] = a.res_mode == 2 ? coef[2 * a.C + c8 + k] : 0.f;
-    sh2[k] = a.res_mode == 2 ? coef[3 * a.C + c8 + k] : 0.f;
+    sc1[k] = coef[l8 + k];
+    sh1[k] = coef[CG + l8 + k];
+    sc2[k] = a.res_mode == 2 ? coef[2 * CG + l8 + k] : 0.f;
+    sh2[k] = a.res_mode == 2 ? coef[3 * CG + l8 + k] : 0.f;
   }
-  // PPT pixels per thread per pass, every load issued before any is consumed
-  // (out may alias nothing the loads read, but the compiler cannot know that)
-  constexpr int PPT = 4;
   if (row < rows) {
-    const int64_t stride = (int64_t)gridDim.x * rows;
-    for (int64_t base = (int64_t)blockIdx.x * rows + row; base < a.npix; base += PPT * stride) {
-      uint4 uy[PPT], ur[PPT];
+    for (; base < a.npix; base += PPT * stride) {
+      // this pass's operands; the next pass's loads go out before the math
+      uint4 cy[PPT], cr[PPT];
 #pragma unroll
-      for (int u = 0; u < PPT; ++u) {
-        const int64_t pix = base + u * stride;
-        uy[u] = pix < a.npix ? *reinterpret_cast<const uint4*>(a.y + pix * a.ldy + c8) : make_uint4(0, 0, 0, 0);
-        ur[u] = (a.res_mode && pix < a.npix) ? *reinterpret_cast<const uint4*>(a.res + pix * a.ldr + c8)
-                                             : make_uint4(0, 0, 0, 0);
-      }
+      for (int u = 0; u < PPT; ++u) { cy[u] = uy[u]; cr[u] = ur[u]; }
+      if (base + PPT * stride < a.npix) load(base + PPT * stride);
 #pragma unroll
       for (int u = 0; u < PPT; ++u) {
         const int64_t pix = base + u * stride;
         if (pix >= a.npix) break;
         float v[8];
-        unpack8(uy[u], v);
+        unpack8(cy[u], v);
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = v[k] * sc1[k] + sh1[k];
         if (a.res_mode) {
           float r[8];
-          unpack8(ur[u], r);
+          unpack8(cr[u], r);
           if (a.res_mode == 2) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) r[k] = r[k] * sc2[k] + sh2[k];
@@ -124,11 +142,11 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(BnApplyArgs a) {
       }
     }
   }
-  // standalone use (no producer finalised the stats): block 0 finalises
+  // standalone use (no producer finalised the stats): block (0, g) finalises
+  // its channel group
   if (blockIdx.x == 0) {
-    __syncthreads();
-    if (!a.bn.ss) bn_finalize_block0(a.bn, threadIdx.x, blockDim.x);
-    if (a.res_mode == 2 && !a.bn2.ss) bn_finalize_block0(a.bn2, threadIdx.x, blockDim.x);
+    if (!a.bn.ss) bn_finalize_block0(a.bn, threadIdx.x, blockDim.x, cg0, cg0 + CG);
+    if (a.res_mode == 2 && !a.bn2.ss) bn_finalize_block0(a.bn2, threadIdx.x, blockDim.x, cg0, cg0 + CG);
   }
 }
 
@@ -137,11 +155,23 @@ static inline dim3 chunk_block(int C) {
   return dim3((256 / CC) * CC);
 }
 
+// grid of the grouped BN kernels: x = pixel blocks (kBnPPT pixels per thread
+// per pass, capped so that x * groups <= g_apply_cap), y = channel groups
+static inline dim3 bn_grid(int64_t npix, int C) {
+  const int CG = bn_group(C), groups = C / CG;
+  const int rows = 256 / (CG / 8);
+  const int cap = g_apply_cap / groups > 0 ? g_apply_cap / groups : 1;
+  return dim3(grid_for(npix, rows * kBnPPT, cap), groups);
+}
+
+static inline bool bn_group_ok(int C) {
+  return C % 8 == 0 && bn_group(C) / 8 <= 256;  // rows = 256 / CC, threads past rows*CC idle
+}
+
 hipError_t launch_bn_apply(const BnApplyArgs& a, hipStream_t st) {
-  if (a.C % 8 || a.C / 8 > 256) return hipErrorInvalidValue;
-  const int rows = 256 / (a.C / 8);
-  const int g = grid_for(a.npix, rows * 4, g_apply_cap);  // 4 pixels per thread: one pass
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(g), chunk_block(a.C), 4 * a.C * sizeof(float), st, a);
+  if (!bn_group_ok(a.C)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_apply_kernel, bn_grid(a.npix, a.C), chunk_block(bn_group(a.C)),
+                     4 * bn_group(a.C) * sizeof(float), st, a);
   return hipGetLastError();
 }
 
@@ -243,53 +273,73 @@ hipError_t launch_bn_bwd_reduce(const BnBwdArgs& a, hipStream_t st) {
 }
 
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, double inv_n) {
-  const int CC = a.C >> 3;
+  const int CG = bn_group(a.C);
+  const int CC = CG >> 3;
   const int rows = blockDim.x / CC;
   const int chunk = threadIdx.x % CC, row = threadIdx.x / CC;
-  const int c8 = chunk << 3;
+  const int cg0 = blockIdx.y * CG;
+  const int c8 = cg0 + (chunk << 3);
   const bool two = a.y2 != nullptr;
-  // per channel: k1 = gamma*invstd, m1 = mean(dZ), m2 = mean(dZ*xhat) (x2 for bn2),
-  // computed once per channel into LDS, then 8 per thread into registers
-  extern __shared__ __attribute__((aligned(16))) float coef[];  // [9][C]
-  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+  constexpr int PPT = kBnPPT;
+  const int64_t stride = (int64_t)gridDim.x * rows;
+  uint4 uda[PPT], uact[PPT], uy[PPT], uy2[PPT];
+  auto load = [&](int64_t base) {
+#pragma unroll
+    for (int u = 0; u < PPT; ++u) {
+      const int64_t pix = base + u * stride;
+      const bool in = pix < a.npix;
+      const uint4 z = make_uint4(0, 0, 0, 0);
+      uda[u] = in ? *reinterpret_cast<const uint4*>(a.da + pix * a.ldda + c8) : z;
+      uact[u] = (in && a.relu) ? *reinterpret_cast<const uint4*>(a.act + pix * a.ldact + c8) : z;
+      uy[u] = in ? *reinterpret_cast<const uint4*>(a.y + pix * a.ldy + c8) : z;
+      uy2[u] = (in && two) ? *reinterpret_cast<const uint4*>(a.y2 + pix * a.ldy2 + c8) : z;
+    }
+  };
+  int64_t base = (int64_t)blockIdx.x * rows + row;
+  if (row < rows) load(base);  // first pass in flight during the prologue
+  // per channel of the group: k1 = gamma*invstd, m1 = mean(dZ), m2 =
+  // mean(dZ*xhat) (x2 for bn2) into LDS, then 8 per thread into registers
+  extern __shared__ __attribute__((aligned(16))) float coef[];  // [9][CG]
+  for (int c = threadIdx.x; c < CG; c += blockDim.x) {
+    const int ch = cg0 + c;
     if (a.coef) {  // finalised by the reduce kernel's last block
-      coef[c] = a.coef[c];
-      coef[a.C + c] = a.coef[a.C + c];
-      coef[2 * a.C + c] = a.coef[2 * a.C + c];
-      coef[3 * a.C + c] = a.mean[c];
-      coef[4 * a.C + c] = a.invstd[c];
+      coef[c] = a.coef[ch];
+      coef[CG + c] = a.coef[a.C + ch];
+      coef[2 * CG + c] = a.coef[2 * a.C + ch];
+      coef[3 * CG + c] = a.mean[ch];
+      coef[4 * CG + c] = a.invstd[ch];
       if (two) {
-        coef[5 * a.C + c] = a.coef[3 * a.C + c];
-        coef[6 * a.C + c] = a.coef[4 * a.C + c];
-        coef[7 * a.C + c] = a.mean2[c];
-        coef[8 * a.C + c] = a.invstd2[c];
+        coef[5 * CG + c] = a.coef[3 * a.C + ch];
+        coef[6 * CG + c] = a.coef[4 * a.C + ch];
+        coef[7 * CG + c] = a.mean2[ch];
+        coef[8 * CG + c] = a.invstd2[ch];
       }
       continue;
     }
     double s1 = 0.0, s2 = 0.0, t2 = 0.0;
     for (int r = 0; r < kStatRep; ++r) {
       const size_t rep = (size_t)r * 2 * a.C;
-      s1 += a.sums[rep + c];
-      s2 += a.sums[rep + a.C + c];
-      if (two) t2 += a.sums2[rep + a.C + c];
+      s1 += a.sums[rep + ch];
+      s2 += a.sums[rep + a.C + ch];
+      if (two) t2 += a.sums2[rep + a.C + ch];
     }
-    coef[c] = a.gamma[c] * a.invstd[c];
-    coef[a.C + c] = (float)(s1 * inv_n);
-    coef[2 * a.C + c] = (float)(s2 * inv_n);
-    coef[3 * a.C + c] = a.mean[c];
-    coef[4 * a.C + c] = a.invstd[c];
+    coef[c] = a.gamma[ch] * a.invstd[ch];
+    coef[CG + c] = (float)(s1 * inv_n);
+    coef[2 * CG + c] = (float)(s2 * inv_n);
+    coef[3 * CG + c] = a.mean[ch];
+    coef[4 * CG + c] = a.invstd[ch];
     if (two) {
-      coef[5 * a.C + c] = a.gamma2[c] * a.invstd2[c];
-      coef[6 * a.C + c] = (float)(t2 * inv_n);
-      coef[7 * a.C + c] = a.mean2[c];
-      coef[8 * a.C + c] = a.invstd2[c];
+      coef[5 * CG + c] = a.gamma2[ch] * a.invstd2[ch];
+      coef[6 * CG + c] = (float)(t2 * inv_n);
+      coef[7 * CG + c] = a.mean2[ch];
+      coef[8 * CG + c] = a.invstd2[ch];
     }
     if (blockIdx.x == 0) {
-      a.dgamma[c] = (float)s2;
-      a.dbeta[c] = (float)s1;
+      a.dgamma[ch] = (float)s2;
+      a.dbeta[ch] = (float)s1;
       if (two) {
-        a.dgamma2[c] = (float)t2;
-        a.dbeta2[c] = (float)s1;  // same dZ feeds both BNs
+        a.dgamma2[ch] = (float)t2;
+        a.dbeta2[ch] = (float)s1;  // same dZ feeds both BNs
       }
     }
   }
@@ -297,32 +347,20 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, double i
   float k1[8], m1[8], m2[8], mu[8], is[8], k1b[8], m2b[8], mub[8], isb[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const int c = c8 + k;
+    const int c = (chunk << 3) + k;
     k1[k] = coef[c];
-    m1[k] = coef[a.C + c];
-    m2[k] = coef[2 * a.C + c];
-    mu[k] = coef[3 * a.C + c];
-    is[k] = coef[4 * a.C + c];
-    k1b[k] = two ? coef[5 * a.C + c] : 0.f;
-    m2b[k] = two ? coef[6 * a.C + c] : 0.f;
-    mub[k] = two ? coef[7 * a.C + c] : 0.f;
-    isb[k] = two ? coef[8 * a.C + c] : 0.f;
+    m1[k] = coef[CG + c];
+    m2[k] = coef[2 * CG + c];
+    mu[k] = coef[3 * CG + c];
+    is[k] = coef[4 * CG + c];
+    k1b[k] = two ? coef[5 * CG + c] : 0.f;
+    m2b[k] = two ? coef[6 * CG + c] : 0.f;
+    mub[k] = two ? coef[7 * CG + c] : 0.f;
+    isb[k] = two ? coef[8 * CG + c] : 0.f;
   }
-  constexpr int PPT = 4;
   if (row < rows) {
-    const int64_t stride = (int64_t)gridDim.x * rows;
-    for (int64_t base = (int64_t)blockIdx.x * rows + row; base < a.npix; base += PPT * stride) {
-      uint4 uda[PPT], uact[PPT], uy[PPT], uy2[PPT];
-#pragma unroll
-      for (int u = 0; u < PPT; ++u) {
-        const int64_t pix = base + u * stride;
-        const bool in = pix < a.npix;
-        const uint4 z = make_uint4(0, 0, 0, 0);
-        uda[u] = in ? *reinterpret_cast<const uint4*>(a.da + pix * a.ldda + c8) : z;
-        uact[u] = (in && a.relu) ? *reinterpret_cast<const uint4*>(a.act + pix * a.ldact + c8) : z;
-        uy[u] = in ? *reinterpret_cast<const uint4*>(a.y + pix * a.ldy + c8) : z;
-        uy2[u] = (in && two) ? *reinterpret_cast<const uint4*>(a.y2 + pix * a.ldy2 + c8) : z;
-      }
+    for (bool first = true; base < a.npix; base += PPT * stride, first = false) {
+      if (!first) load(base);
 #pragma unroll
       for (int u = 0; u < PPT; ++u) {
         const int64_t pix = base + u * stride;
@@ -352,11 +390,9 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, double i
 }
 
 hipError_t launch_bn_bwd_apply(const BnBwdArgs& a, hipStream_t st) {
-  if (a.C % 8 || a.C / 8 > 256) return hipErrorInvalidValue;
-  const int rows = 256 / (a.C / 8);
-  const int g = grid_for(a.npix, rows * 4, g_apply_cap);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(g), chunk_block(a.C), 9 * a.C * sizeof(float), st, a,
-                     1.0 / (double)a.npix);
+  if (!bn_group_ok(a.C)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, bn_grid(a.npix, a.C), chunk_block(bn_group(a.C)),
+                     9 * bn_group(a.C) * sizeof(float), st, a, 1.0 / (double)a.npix);
   return hipGetLastError();
 }
 
@@ -611,6 +647,15 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(HeadArgs a) {
   const int chunk = threadIdx.x % CC, row = threadIdx.x / CC;
   const int c8 = chunk << 3;
   const int64_t total = (int64_t)a.N * a.H * a.W;
+  const BnBwdArgs& bb = a.bb;
+  const bool fz = bb.sums != nullptr;
+  float s1[8], s2[8], mu[8], is[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    s1[k] = s2[k] = 0.f;
+    mu[k] = fz ? bb.mean[c8 + k] : 0.f;
+    is[k] = fz ? bb.invstd[c8 + k] : 0.f;
+  }
   float U[8][4];
   float S = 0.f;
 #pragma unroll
@@ -635,28 +680,60 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(HeadArgs a) {
       if (chunk == 0) S += (d[0] + d[1]) + (d[2] + d[3]);
       float x[8], g[8];
       unpack8(*reinterpret_cast<const uint4*>(a.x + pix * a.ldx + c8), x);
+      uint4 yv = make_uint4(0, 0, 0, 0);
+      if (fz) yv = *reinterpret_cast<const uint4*>(bb.y + pix * bb.ldy + c8);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         g[k] = d[0] * Vl[k][0] + d[1] * Vl[k][1] + d[2] * Vl[k][2] + d[3] * Vl[k][3];
 #pragma unroll
         for (int ab = 0; ab < 4; ++ab) U[k][ab] += x[k] * d[ab];
       }
-      *reinterpret_cast<uint4*>(a.dx + pix * a.lddx + c8) = pack8(g);
+      if (fz) {  // x IS the BN+ReLU output (act): ReLU mask, then the BN-backward sums
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g[k] = x[k] > 0.f ? g[k] : 0.f;
+      }
+      const uint4 o = pack8(g);
+      *reinterpret_cast<uint4*>(a.dx + pix * a.lddx + c8) = o;
+      if (fz) {
+        float dz[8], y[8];
+        unpack8(o, dz);  // sums of the stored bf16 dZ, as bn_bwd_reduce_kernel would read them
+        unpack8(yv, y);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { s1[k] += dz[k]; s2[k] += dz[k] * (y[k] - mu[k]) * is[k]; }
+      }
     }
   }
-  const int L = a.Cin * 4 + 1;
+  // red[row][L]: U (Cin*4) | S | fused BN sums dZ (Cin) | dZ*xhat (Cin)
+  const int LU = a.Cin * 4 + 1;
+  const int L = LU + (fz ? 2 * a.Cin : 0);
   if (row < rows) {
 #pragma unroll
     for (int k = 0; k < 8; ++k)
 #pragma unroll
       for (int ab = 0; ab < 4; ++ab) red[row * L + (c8 + k) * 4 + ab] = U[k][ab];
     if (chunk == 0) red[row * L + a.Cin * 4] = S;
+    if (fz) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        red[row * L + LU + c8 + k] = s1[k];
+        red[row * L + LU + a.Cin + c8 + k] = s2[k];
+      }
+    }
   }
   __syncthreads();
   for (int t = threadIdx.x; t < L; t += blockDim.x) {
     float v = 0.f;
     for (int r = 0; r < rows; ++r) v += red[r * L + t];
-    atomicAdd(a.usum + t, (double)v);
+    if (t < LU) {
+      atomicAdd(a.usum + t, (double)v);
+    } else {  // [kStatRep][2][C] replica layout of the BN-backward sums
+      const int q = (t - LU) / a.Cin, c = (t - LU) - q * a.Cin;
+      atomicAdd(bb.sums + (size_t)(blockIdx.x % kStatRep) * 2 * a.Cin + q * a.Cin + c, (double)v);
+    }
+  }
+  if (fz && bb.ticket) {
+    __shared__ int flag;
+    if (last_block_arrive(bb.ticket, gridDim.x, &flag, true)) bn_bwd_finalize(bb);
   }
 }
 
@@ -686,7 +763,8 @@ hipError_t launch_head_bwd(const HeadArgs& a, hipStream_t st) {
   if (a.Cin > kHeadMaxCin || a.Cin % 8) return hipErrorInvalidValue;
   const int64_t total = (int64_t)a.N * a.H * a.W;
   const int CC = a.Cin / 8, rows = 256 / CC;
-  const size_t lds = (size_t)rows * (a.Cin * 4 + 1) * sizeof(float);
+  if (a.bb.sums && (a.bb.C != a.Cin || a.bb.y2)) return hipErrorInvalidValue;
+  const size_t lds = (size_t)rows * (a.Cin * 4 + 1 + (a.bb.sums ? 2 * a.Cin : 0)) * sizeof(float);
   hipLaunchKernelGGL(head_bwd_kernel, dim3(grid_for(total, rows * 8, 1024)), dim3(rows * CC), lds, st, a);
   return hipGetLastError();
 }

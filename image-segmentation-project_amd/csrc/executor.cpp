@@ -565,22 +565,30 @@ int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for
   a.N = x.p->cfg.N; a.H = in.H; a.W = in.W; a.C = cv.Ci;
   a.P = out.H; a.Q = out.W; a.Cout = cv.Co;
   a.R = cv.R; a.S = cv.S; a.stride = cv.stride; a.pad = cv.pad;
-  CK(launch_conv_fwd(a, cv.kind == L_CONVT ? MODE_TRANS : MODE_FWD, x.st));
+  CK(launch_conv_fwd(a, cv.kind == L_CONVT ? MODE_SHUF : MODE_FWD, x.st));
   return 0;
 }
 
 // conv dgrad: dx = dgrad(dy) (+ addend).  fuse: dx is dA of that BN(+ReLU);
 // the epilogue stores dZ and runs the BN-backward reduction (ConvFwdArgs::bb).
+// ds >= 0: the block's 1x1/s2 downsample dgrad (dY = dyds) is folded into this
+// 3x3/s2 conv1 dgrad as a second reduction range of parity class 0.
 int conv_dgrad(const Ctx& x, int ci, const Act& dy, const Act& dx, const Act* add,
-               const BnBwdArgs* fuse = nullptr) {
+               const BnBwdArgs* fuse = nullptr, int ds = -1, const Act* dyds = nullptr) {
   const Conv& cv = x.p->convs[ci];
-  ProfScope ps(x.p, x.st, "dgrad " + pname(x, cv.w), conv_flops(x.p, cv, cv.kind == L_CONVT ? dy : dy));
+  const double fl = conv_flops(x.p, cv, dy) + (ds >= 0 ? conv_flops(x.p, x.p->convs[ds], *dyds) : 0.0);
+  ProfScope ps(x.p, x.st, "dgrad " + pname(x, cv.w) + (ds >= 0 ? " +ds" : ""), fl);
   ConvFwdArgs a = {};
   a.x = x.A(dy); a.ldx = dy.ld;
   a.w = x.W<bf16_t>(cv.pk_dgrad);
   a.y = x.A(dx); a.ldy = dx.ld;
   if (add && add->ld) { a.add = x.A(*add); a.ldadd = add->ld; }
   if (fuse) a.bb = *fuse;
+  if (ds >= 0) {
+    const Conv& dv = x.p->convs[ds];
+    a.x2 = x.A(*dyds); a.ldx2 = dyds->ld;
+    a.w2 = x.W<bf16_t>(dv.pk_dgrad); a.C2 = dv.Co;
+  }
   a.N = x.p->cfg.N;
   a.H = dy.H; a.W = dy.W;
   a.P = dx.H; a.Q = dx.W;
@@ -810,6 +818,10 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     h.gw0 = grads + p->params[p->up0_w].flat; h.gb0 = grads + p->params[p->up0_b].flat;
     h.gwf = grads + p->params[p->fin_w].flat; h.gbf = grads + p->params[p->fin_b].flat;
     h.N = N; h.H = o.H; h.W = o.W; h.Cin = o.C; h.Co = (int)p->params[p->up0_b].numel;
+    if (p->fuse_bwd) {  // the head produces dA of decoder1's last BN: reduce it here
+      const Dec& d = p->decs[3];
+      h.bb = bwd_args(x, d.bn2, d.d_out, d.out, d.y2, d.dy2, -1, nullptr, nullptr, nullptr, grads);
+    }
     ProfScope ps(p, st, "head_bwd", 0);
     CK(launch_head_bwd(h, st));
     CK(launch_head_grads(h, st));
@@ -838,7 +850,7 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
   // decoder1 .. decoder4 (+ their up-convs)
   for (int l = 3; l >= 0; --l) {
     Dec& d = p->decs[l];
-    RUN(bn_backward(x, d.bn2, dec_bn2(l), fz && l < 3));
+    RUN(bn_backward(x, d.bn2, dec_bn2(l), fz));
     const BnBwdArgs f1 = dec_bn1(l);
     RUN(conv_dgrad(x, d.conv2, d.dy2, d.dh, nullptr, fz ? &f1 : nullptr));
     RUN(conv_wgrad(x, d.conv2, d.dy2, d.h));
@@ -875,8 +887,8 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     const BnBwdArgs* fprev = nullptr;
     if (fz && i > 0) { fp = blk_bn2(i - 1); fprev = &fp; }
     if (b.ds >= 0) {
-      RUN(conv_dgrad(x, b.conv1, b.dy1, b.d_in, b.skip_add.ld ? &b.skip_add : nullptr));
-      RUN(conv_dgrad(x, b.ds, b.dyds, b.d_in, &b.d_in, fprev));
+      // conv1 (3x3/s2) and downsample (1x1/s2) data gradients in one launch
+      RUN(conv_dgrad(x, b.conv1, b.dy1, b.d_in, b.skip_add.ld ? &b.skip_add : nullptr, fprev, b.ds, &b.dyds));
       RUN(conv_wgrad(x, b.ds, b.dyds, b.in));
     } else {
       // identity path: dZ of bn2 (held in d_out when fused)

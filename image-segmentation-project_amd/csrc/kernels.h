@@ -7,7 +7,11 @@ namespace unet {
 
 typedef unsigned short bf16_t;
 
-enum { MODE_FWD = 0, MODE_TRANS = 1, MODE_STEM = 2 };
+// MODE_SHUF: ConvTranspose2d(k2, s2) forward as ONE 1x1 GEMM over the input
+// pixels with 4*Cout columns (j = (a*2+b)*Cout + co) and a pixel-shuffle store
+// y[2i+a, 2j+b, co]; every input pixel is staged once instead of once per
+// output parity class.
+enum { MODE_FWD = 0, MODE_TRANS = 1, MODE_STEM = 2, MODE_SHUF = 3 };
 
 // Per-channel fp64 reductions (BN sums) are spread over kStatRep replicas of
 // [2][C] (replica = blockIdx.x % kStatRep) so thousands of blocks do not all
@@ -61,6 +65,10 @@ struct ConvFwdArgs {
   // and adds sum dZ, sum dZ*xhat (and dZ*xhat2) into bb.sums / bb.sums2; the
   // last block runs bn_bwd_finalize (common.h).
   BnBwdArgs bb;
+  // optional second reduction range of parity class 0 (MODE_TRANS only): the
+  // 1x1 / stride-2 downsample dgrad folded into its block's conv1 dgrad.
+  // Output pixels (2p, 2q) also get sum_k x2[n,p,q,k] * w2[co][k], k < C2.
+  const bf16_t* x2; int ldx2; const bf16_t* w2; int C2;
   int N, H, W, C;                // input geometry (C = GEMM reduction channels)
   int P, Q, Cout;                // output geometry
   int R, S, stride, pad;
@@ -128,6 +136,10 @@ struct HeadArgs {
   bf16_t* dx; int lddx;              // backward: dL/dX
   double* usum;                      // backward: [Cin*4 + 1] sums U[c][ab], S
   float* gw0; float* gb0; float* gwf; float* gbf;  // param grads
+  // backward, optional (bb.sums != null): dX is dA of decoder1's last
+  // BN+ReLU; as in the conv-dgrad epilogue, dZ = dA * (act > 0) is stored and
+  // the BN-backward sums (dZ, dZ*xhat) are reduced here (bn_bwd apply follows)
+  BnBwdArgs bb;
   int N, H, W, Cin, Co;
 };
 hipError_t launch_head_fwd(const HeadArgs& a, hipStream_t st);
