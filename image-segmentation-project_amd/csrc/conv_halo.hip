@@ -218,7 +218,8 @@ struct TileEpi {
         uint2 o;
         o.x = pack_bf2(v[0], v[1]);
         o.y = pack_bf2(v[2], v[3]);
-        *reinterpret_cast<uint2*>(a.y + pix[j] * a.ldy + co) = o;
+        if (a.ysplit && co >= a.csplit) *reinterpret_cast<uint2*>(a.ysplit + pix[j] * a.ldysplit + co - a.csplit) = o;
+        else *reinterpret_cast<uint2*>(a.y + pix[j] * a.ldy + co) = o;
         if (FLIP && fbwd) {  // sums of the stored bf16 dZ, as bn_bwd_reduce_kernel would read them
           const float dz[4] = {__uint_as_float(o.x << 16), __uint_as_float(o.x & 0xffff0000u),
                                __uint_as_float(o.y << 16), __uint_as_float(o.y & 0xffff0000u)};

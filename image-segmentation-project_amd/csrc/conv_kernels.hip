@@ -360,7 +360,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x4 (&acc)
         uint2 o;
         o.x = pack_bf2(v[0], v[1]);
         o.y = pack_bf2(v[2], v[3]);
-        *reinterpret_cast<uint2*>(a.y + pix * a.ldy + co) = o;
+        if (a.ysplit && co >= a.csplit) *reinterpret_cast<uint2*>(a.ysplit + pix * a.ldysplit + co - a.csplit) = o;
+        else *reinterpret_cast<uint2*>(a.y + pix * a.ldy + co) = o;
         if (fbwd) {
           const float dz[4] = {__uint_as_float(o.x << 16), __uint_as_float(o.x & 0xffff0000u),
                                __uint_as_float(o.y << 16), __uint_as_float(o.y & 0xffff0000u)};
@@ -748,6 +749,13 @@ conv_wgrad_kernel(ConvWgradArgs a) {
                        ? img[((size_t)n * a.H + ih) * a.W + iw] : 0.f;
           }
           v = pack8(f);
+        } else if constexpr (XLOAD == XLOAD_SHUF) {
+          const int c = c0 + ch * 8, Co = a.C >> 2;
+          if (c < a.C) {
+            const int t = c / Co, co = c - t * Co;
+            const int ih = 2 * p + (t >> 1), iw = 2 * q + (t & 1);
+            v = *reinterpret_cast<const uint4*>(a.x + ((size_t)(n * a.H + ih) * a.W + iw) * a.ldx + co);
+          }
         } else {
           const int ih = p * a.stride - a.pad + r, iw = q * a.stride - a.pad + s;
           if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W && c0 + ch * 8 < a.C)
@@ -1403,6 +1411,9 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a0, int mode, hipStream_t st) {
   // the folded downsample range exists only in the LDS-DMA transposed kernel
   if (a0.x2 && (!g_use_glds || mode != MODE_TRANS || a0.C2 != a0.C || a0.stride != 2 || a0.pad != 1))
     return hipErrorInvalidValue;
+  if (a0.ysplit && (!g_use_glds || mode == MODE_STEM || mode == MODE_SHUF || a0.csplit % 4 || a0.ldysplit % 4 ||
+                    a0.bb.sums || a0.add))
+    return hipErrorInvalidValue;
   if (g_use_glds && mode == MODE_STEM) return launch_stem_fwd(a0, st);
   if (mode == MODE_SHUF) {  // convT k2s2 forward: a0 holds the transposed-conv geometry
     if (!g_use_glds || a0.R != 2 || a0.S != 2 || a0.stride != 2 || a0.pad != 0 || a0.Cout % 4 || a0.C % 32 ||
@@ -1539,6 +1550,15 @@ hipError_t launch_wgrad_finish(hipStream_t st) {
   set_kernel_tag("wgrad_slab_reduce_kernel");
   hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3(bx, G), dim3(256), 0, st, r.slab, r.dw, r.n, r.splits);
   return hipGetLastError();
+}
+
+hipError_t launch_convt_wgrad(const ConvWgradArgs& a0, hipStream_t st) {
+  ConvWgradArgs a = a0;
+  if (a.C % 32 || (a.C / 4) % 8 || a.Cout % 32 || a.H != 2 * a.P || a.W != 2 * a.Q) return hipErrorInvalidValue;
+  a.R = a.S = 1; a.stride = 1; a.pad = 0;
+  if (a.Cout >= 128 && a.C >= 128) return launch_wgrad_cfg<XLOAD_SHUF, 128, 128, 32, 2, 2>(a, st);
+  if (a.Cout % 64 == 0 && a.C % 64 == 0) return launch_wgrad_cfg<XLOAD_SHUF, 64, 64, 64, 2, 2>(a, st);
+  return launch_wgrad_cfg<XLOAD_SHUF, 32, 32, 64, 2, 2>(a, st);
 }
 
 hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st) {

@@ -74,6 +74,11 @@ struct Dec {
   Act up_in, up_out;  // up_out = cat slice
   Act cat, y1, h, y2, out;
   Act d_out, dy2, dh, dy1, dcat, d_up_in;
+  // gradient of the up-conv part of the concat: a slice of dcat, or (split,
+  // when that part is narrower than a 128-B line) its own dense buffer while
+  // dcat then holds only the skip channels
+  Act dcat_up;
+  bool split = false;
 };
 
 }  // namespace unet
@@ -100,6 +105,18 @@ struct unet_plan {
   std::vector<std::vector<int>> bucket_convs;        // convs to unpack per bucket
   hipEvent_t events[8] = {};
   int nevents = 0;
+  // Backward on two streams: the data-gradient chain (dgrad -> BN backward ->
+  // dgrad ...) stays on the caller's stream, every weight gradient (+ split-K
+  // reduce, bias sums, unpack, bucket events) runs on `wstream`, forked after
+  // the BN-backward apply that produces its dY and joined at the end, so the
+  // HBM-bound BN passes and the reduces overlap the MFMA-bound convs.
+  // Measured slower on MI355X (8.39 vs 7.86 ms/step: the LDS-heavy wgrad and
+  // dgrad blocks contend for CUs and delay the critical dgrad chain), so it is
+  // opt-in: UNET_TWO_STREAM=1 (UNET_WS_PRIO=-1/0/1: weight-stream priority).
+  bool two_stream = std::getenv("UNET_TWO_STREAM") != nullptr;
+  hipStream_t wstream = nullptr;
+  std::vector<hipEvent_t> syncpool;
+  int syncused = 0;
   bool want_events = false;  // DDP overlap: record one hipEvent per gradient bucket
   // BN-backward reductions fused into the producing conv dgrad (UNET_NO_BWD_FUSE=1: off, A/B only)
   bool fuse_bwd = std::getenv("UNET_NO_BWD_FUSE") == nullptr;
@@ -396,7 +413,15 @@ static int build_plan(unet_plan* p) {
     d.dy2 = act(A, N, Hl, Wl, oc);
     d.dh = act(A, N, Hl, Wl, oc);
     d.dy1 = act(A, N, Hl, Wl, oc);
-    d.dcat = act(A, N, Hl, Wl, d.cat.C);
+    const int upc = d.up_out.C, skc = d.cat.C - upc;
+    d.split = upc * 2 < 128;
+    if (d.split) {
+      d.dcat = act(A, N, Hl, Wl, skc);
+      d.dcat_up = act(A, N, Hl, Wl, upc);
+    } else {
+      d.dcat = act(A, N, Hl, Wl, d.cat.C);
+      d.dcat_up = slice(d.dcat, skc, upc);
+    }
   }
   for (int l = 0; l < 4; ++l) {
     Dec& d = p->decs[l];
@@ -457,7 +482,9 @@ static int build_plan(unet_plan* p) {
     nm.push_back({pre + "y1", d.y1}); nm.push_back({pre + "h", d.h}); nm.push_back({pre + "y2", d.y2});
     nm.push_back({pre + "out", d.out});
     nm.push_back({pre + "d.out", d.d_out}); nm.push_back({pre + "d.y2", d.dy2}); nm.push_back({pre + "d.h", d.dh});
-    nm.push_back({pre + "d.y1", d.dy1}); nm.push_back({pre + "d.cat", d.dcat});
+    nm.push_back({pre + "d.y1", d.dy1});
+    if (d.split) { nm.push_back({pre + "d.cat.skip", d.dcat}); nm.push_back({pre + "d.cat.up", d.dcat_up}); }
+    else nm.push_back({pre + "d.cat", d.dcat});
   }
 
   // unpack groups per bucket
@@ -521,6 +548,7 @@ struct Ctx {
   float* const* buf;
   hipStream_t st;
   int training;
+  hipStream_t wst = nullptr;  // weight-gradient stream (== st when single-stream)
   bf16_t* A(const Act& a) const { return reinterpret_cast<bf16_t*>(ws + a.off); }
   template <class T> T* W(size_t off) const { return reinterpret_cast<T*>(ws + off); }
 };
@@ -574,7 +602,8 @@ int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for
 // ds >= 0: the block's 1x1/s2 downsample dgrad (dY = dyds) is folded into this
 // 3x3/s2 conv1 dgrad as a second reduction range of parity class 0.
 int conv_dgrad(const Ctx& x, int ci, const Act& dy, const Act& dx, const Act* add,
-               const BnBwdArgs* fuse = nullptr, int ds = -1, const Act* dyds = nullptr) {
+               const BnBwdArgs* fuse = nullptr, int ds = -1, const Act* dyds = nullptr,
+               const Act* dx_split = nullptr) {
   const Conv& cv = x.p->convs[ci];
   const double fl = conv_flops(x.p, cv, dy) + (ds >= 0 ? conv_flops(x.p, x.p->convs[ds], *dyds) : 0.0);
   ProfScope ps(x.p, x.st, "dgrad " + pname(x, cv.w) + (ds >= 0 ? " +ds" : ""), fl);
@@ -584,6 +613,9 @@ int conv_dgrad(const Ctx& x, int ci, const Act& dy, const Act& dx, const Act* ad
   a.y = x.A(dx); a.ldy = dx.ld;
   if (add && add->ld) { a.add = x.A(*add); a.ldadd = add->ld; }
   if (fuse) a.bb = *fuse;
+  if (dx_split) {  // channels >= dx.C go to their own buffer
+    a.ysplit = x.A(*dx_split); a.ldysplit = dx_split->ld; a.csplit = dx.C;
+  }
   if (ds >= 0) {
     const Conv& dv = x.p->convs[ds];
     a.x2 = x.A(*dyds); a.ldx2 = dyds->ld;
@@ -601,29 +633,32 @@ int conv_dgrad(const Ctx& x, int ci, const Act& dy, const Act& dx, const Act* ad
 
 int conv_wgrad(const Ctx& x, int ci, const Act& dy, const Act& in) {
   const Conv& cv = x.p->convs[ci];
-  ProfScope ps(x.p, x.st, "wgrad " + pname(x, cv.w), conv_flops(x.p, cv, dy));
+  ProfScope ps(x.p, x.wst, "wgrad " + pname(x, cv.w), conv_flops(x.p, cv, dy));
   ConvWgradArgs a = {};
   a.N = x.p->cfg.N;
   a.dw = x.W<float>(cv.wacc);
   a.slab = x.W<float>(x.p->wslab); a.slab_bytes = x.p->wslab_bytes;
   a.R = cv.R; a.S = cv.S; a.stride = cv.stride; a.pad = cv.pad;
   if (cv.kind == L_CONVT) {
-    // view as conv of dY (input, stride 2) producing X: "dy" := X, "x" := dY
+    // one GEMM over the input pixels: "dy" := X [Ci], "x" := dY gathered as
+    // 4 output pixels x Co per input pixel (XLOAD_SHUF), dW [Ci][2][2][Co]
     a.dy = x.A(in); a.lddy = in.ld;
     a.x = x.A(dy); a.ldx = dy.ld;
-    a.H = dy.H; a.W = dy.W; a.C = cv.Co;
+    a.H = dy.H; a.W = dy.W; a.C = 4 * cv.Co;
     a.P = in.H; a.Q = in.W; a.Cout = cv.Ci;
+    CK(launch_convt_wgrad(a, x.wst));
+    return 0;
   } else {
     a.dy = x.A(dy); a.lddy = dy.ld;
     a.x = x.A(in); a.ldx = in.ld;
     a.H = in.H; a.W = in.W; a.C = cv.Ci;
     a.P = dy.H; a.Q = dy.W; a.Cout = cv.Co;
   }
-  CK(launch_conv_wgrad(a, 0, x.st));
+  CK(launch_conv_wgrad(a, 0, x.wst));
   ps.close();
   if (wgrad_pending()) {
-    ProfScope pr(x.p, x.st, "wgrad_reduce " + pname(x, cv.w), 0);
-    CK(launch_wgrad_finish(x.st));
+    ProfScope pr(x.p, x.wst, "wgrad_reduce " + pname(x, cv.w), 0);
+    CK(launch_wgrad_finish(x.wst));
   }
   return 0;
 }
@@ -687,7 +722,7 @@ int bn_backward(const Ctx& x, int bi, BnBwdArgs a, bool fused) {
 }
 
 int unpack_bucket(const Ctx& x, int bk, float* grads) {
-  ProfScope ps(x.p, x.st, "unpack", 0);
+  ProfScope ps(x.p, x.wst, "unpack", 0);
   UnpackTable t;
   t.n = 0;
   for (int ci : x.p->bucket_convs[bk]) {
@@ -699,9 +734,9 @@ int unpack_bucket(const Ctx& x, int bk, float* grads) {
     if (cv.kind == L_CONV) { e.kind = UP_CONV; e.Co = cv.Co; e.Ci = cv.Ci; }
     else if (cv.kind == L_CONVT) { e.kind = UP_CONVT; e.Co = cv.Co; e.Ci = cv.Ci; }
     else { e.kind = UP_STEM; e.Co = cv.Co; e.Ci = 1; e.R = 7; e.S = 7; }
-    if (t.n == kMaxPack) { CK(launch_unpack(t, x.st)); t.n = 0; }
+    if (t.n == kMaxPack) { CK(launch_unpack(t, x.wst)); t.n = 0; }
   }
-  CK(launch_unpack(t, x.st));
+  CK(launch_unpack(t, x.wst));
   return 0;
 }
 
@@ -800,11 +835,38 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
   return 0;
 }
 
+// `to` waits for everything issued so far on `from` (fresh pool event per
+// edge, so the order is also right under stream capture)
+static int stream_edge(unet_plan* p, hipStream_t from, hipStream_t to) {
+  if (from == to) return 0;
+  if (p->syncused == (int)p->syncpool.size()) {
+    hipEvent_t e;
+    CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    p->syncpool.push_back(e);
+  }
+  hipEvent_t e = p->syncpool[p->syncused++];
+  CK(hipEventRecord(e, from));
+  CK(hipStreamWaitEvent(to, e, 0));
+  return 0;
+}
+
 static int run_backward(unet_plan* p, const float* image, const float* dlogits, const float* const* prm, char* ws,
                         float* grads, hipStream_t st) {
   Ctx x{p, ws, prm, nullptr, st, 1};
   const int N = p->cfg.N;
   if (p->want_events) RUN(ensure_events(p));
+  if (p->two_stream && !p->wstream) {
+    int least = 0, greatest = 0;
+    CK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    const char* pe = std::getenv("UNET_WS_PRIO");
+    const int sel = pe ? std::atoi(pe) : 0;  // -1: least (lowest), 1: greatest, 0: default
+    const int prio = sel < 0 ? least : (sel > 0 ? greatest : 0);
+    CK(hipStreamCreateWithPriority(&p->wstream, hipStreamNonBlocking, prio));
+  }
+  x.wst = p->two_stream ? p->wstream : st;
+  p->syncused = 0;
+  // fork: the weight stream starts after the zeroing of the accumulators
+  auto fork = [&]() { return stream_edge(p, st, x.wst); };
   CK(hipMemsetAsync(ws + p->zero_bwd_off, 0, p->zero_bwd_bytes, st));
   // head (upconv0 + conv_final)
   {
@@ -851,12 +913,14 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
   for (int l = 3; l >= 0; --l) {
     Dec& d = p->decs[l];
     RUN(bn_backward(x, d.bn2, dec_bn2(l), fz));
+    RUN(fork());
+    RUN(conv_wgrad(x, d.conv2, d.dy2, d.h));
     const BnBwdArgs f1 = dec_bn1(l);
     RUN(conv_dgrad(x, d.conv2, d.dy2, d.dh, nullptr, fz ? &f1 : nullptr));
-    RUN(conv_wgrad(x, d.conv2, d.dy2, d.h));
     RUN(bn_backward(x, d.bn1, f1, fz));
-    RUN(conv_dgrad(x, d.conv1, d.dy1, d.dcat, nullptr));
+    RUN(fork());
     RUN(conv_wgrad(x, d.conv1, d.dy1, d.cat));
+    RUN(conv_dgrad(x, d.conv1, d.dy1, d.dcat, nullptr, nullptr, -1, nullptr, d.split ? &d.dcat_up : nullptr));
     // decoder conv biases feed a training-mode BN: their exact gradient is
     // sum(dY) = 0 (BN removes the mean); write it explicitly.
     CK(hipMemsetAsync(grads + p->params[p->convs[d.conv1].b].flat, 0, sizeof(float) * p->convs[d.conv1].Co, st));
@@ -864,24 +928,33 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     // up-conv: dU = dcat[:, skip:]; its dgrad is dA of the previous decoder's
     // (or enc4's) last BN
     const Conv& up = p->convs[d.up];
-    Act du = slice(d.dcat, d.cat.C - up.Co, up.Co);
+    const Act du = d.dcat_up;
+    RUN(fork());
+    RUN(conv_wgrad(x, d.up, du, d.up_in));
+    {
+      ProfScope ps(p, x.wst, "bias_sum", 0);
+      CK(launch_channel_sum(x.A(du), du.ld, (int64_t)N * du.H * du.W, up.Co, x.W<double>(up.bias_acc), x.wst));
+      CK(launch_d2f(x.W<double>(up.bias_acc), grads + p->params[up.b].flat, up.Co, x.wst));
+    }
     const BnBwdArgs fu = l > 0 ? dec_bn2(l - 1) : blk_bn2(nb - 1);
     RUN(conv_dgrad(x, d.up, du, d.d_up_in, nullptr, fz ? &fu : nullptr));
-    RUN(conv_wgrad(x, d.up, du, d.up_in));
-    ProfScope ps(p, st, "bias_sum", 0);
-    CK(launch_channel_sum(x.A(du), du.ld, (int64_t)N * du.H * du.W, up.Co, x.W<double>(up.bias_acc), st));
-    CK(launch_d2f(x.W<double>(up.bias_acc), grads + p->params[up.b].flat, up.Co, st));
   }
+  // bucket 0 also holds the head's and the decoder biases' gradients (main stream)
+  RUN(stream_edge(p, st, x.wst));
   RUN(unpack_bucket(x, 0, grads));
-  if (p->nevents) CK(hipEventRecord(p->events[0], st));
+  if (p->nevents) CK(hipEventRecord(p->events[0], x.wst));
   // encoder blocks, deepest first
   for (int i = nb - 1; i >= 0; --i) {
     Block& b = p->blocks[i];
     RUN(bn_backward(x, b.bn2, blk_bn2(i), fz));
+    RUN(fork());
+    RUN(conv_wgrad(x, b.conv2, b.dy2, b.h));
+    if (b.ds >= 0) RUN(conv_wgrad(x, b.ds, b.dyds, b.in));
     const BnBwdArgs f1 = blk_bn1(i);
     RUN(conv_dgrad(x, b.conv2, b.dy2, b.dh, nullptr, fz ? &f1 : nullptr));
-    RUN(conv_wgrad(x, b.conv2, b.dy2, b.h));
     RUN(bn_backward(x, b.bn1, f1, fz));
+    RUN(fork());
+    RUN(conv_wgrad(x, b.conv1, b.dy1, b.in));
     // the last writer of d_in produces dA of the previous block's bn2
     BnBwdArgs fp = {};
     const BnBwdArgs* fprev = nullptr;
@@ -889,15 +962,18 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     if (b.ds >= 0) {
       // conv1 (3x3/s2) and downsample (1x1/s2) data gradients in one launch
       RUN(conv_dgrad(x, b.conv1, b.dy1, b.d_in, b.skip_add.ld ? &b.skip_add : nullptr, fprev, b.ds, &b.dyds));
-      RUN(conv_wgrad(x, b.ds, b.dyds, b.in));
     } else {
       // identity path: dZ of bn2 (held in d_out when fused)
       RUN(conv_dgrad(x, b.conv1, b.dy1, b.d_in, fz ? &b.d_out : &b.dres, fprev));
     }
-    RUN(conv_wgrad(x, b.conv1, b.dy1, b.in));
-    // bucket boundaries: enc4 done at i == 13, enc3 at i == 7
-    if (i == 13) { RUN(unpack_bucket(x, 1, grads)); if (p->nevents) CK(hipEventRecord(p->events[1], st)); }
-    if (i == 7) { RUN(unpack_bucket(x, 2, grads)); if (p->nevents) CK(hipEventRecord(p->events[2], st)); }
+    // bucket boundaries (weight stream; BN parameter grads come from the main
+    // stream's reductions): enc4 done at i == 13, enc3 at i == 7
+    if (i == 13 || i == 7) {
+      const int bk = i == 13 ? 1 : 2;
+      RUN(stream_edge(p, st, x.wst));
+      RUN(unpack_bucket(x, bk, grads));
+      if (p->nevents) CK(hipEventRecord(p->events[bk], x.wst));
+    }
   }
   // maxpool + stem
   {
@@ -916,6 +992,7 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
       CK(launch_maxpool_bwd(m, st));
     }
     RUN(bn_backward(x, p->stem_bn, sb, fz));
+    RUN(fork());
     const Conv& cv = p->convs[p->stem_conv];
     ConvWgradArgs a = {};
     a.dy = x.A(p->d_y0); a.lddy = p->d_y0.ld;
@@ -924,11 +1001,13 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     a.P = p->y0.H; a.Q = p->y0.W; a.Cout = cv.Co;
     a.R = 7; a.S = 7; a.stride = 2; a.pad = 3;
     a.x = reinterpret_cast<const bf16_t*>(image);
-    ProfScope ps(p, st, "wgrad input_conv.weight", 2.0 * N * p->y0.H * p->y0.W * cv.Co * 49);
-    CK(launch_conv_wgrad(a, 1, st));
+    ProfScope ps(p, x.wst, "wgrad input_conv.weight", 2.0 * N * p->y0.H * p->y0.W * cv.Co * 49);
+    CK(launch_conv_wgrad(a, 1, x.wst));
   }
   RUN(unpack_bucket(x, 3, grads));
-  if (p->nevents) CK(hipEventRecord(p->events[3], st));
+  if (p->nevents) CK(hipEventRecord(p->events[3], x.wst));
+  // join: the caller's stream (optimizer, next forward) sees every gradient
+  RUN(stream_edge(p, x.wst, st));
   return 0;
 }
 
@@ -966,6 +1045,8 @@ int unet_plan_create(const unet_config* cfg, unet_plan** out) {
 void unet_plan_destroy(unet_plan* p) {
   if (!p) return;
   for (int i = 0; i < p->nevents; ++i) (void)hipEventDestroy(p->events[i]);
+  for (hipEvent_t e : p->syncpool) (void)hipEventDestroy(e);
+  if (p->wstream) (void)hipStreamDestroy(p->wstream);
   delete p;
 }
 

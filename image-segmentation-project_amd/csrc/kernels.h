@@ -19,7 +19,10 @@ enum { MODE_FWD = 0, MODE_TRANS = 1, MODE_STEM = 2, MODE_SHUF = 3 };
 // readers sum the replicas.  Layout everywhere: [kStatRep][2][C].
 constexpr int kStatRep = 16;
 enum { ALOAD_NHWC = 0, ALOAD_STEM = 1 };
-enum { XLOAD_NHWC = 0, XLOAD_STEM = 1 };
+// XLOAD_SHUF: ConvTranspose2d(k2,s2) weight gradient as one GEMM over the
+// INPUT pixels: dW[ci][t][co] = sum_px X[px][ci] * dY[2i + t/2, 2j + t%2][co]
+// (x = dY gathered 4 output pixels per input pixel, C = 4*Co, R = S = 1)
+enum { XLOAD_NHWC = 0, XLOAD_STEM = 1, XLOAD_SHUF = 2 };
 
 // BatchNorm parameters of one layer.  Training: the producer of the batch sums
 // (conv epilogue) finalises them in its LAST block (ticket counter) into
@@ -69,6 +72,10 @@ struct ConvFwdArgs {
   // 1x1 / stride-2 downsample dgrad folded into its block's conv1 dgrad.
   // Output pixels (2p, 2q) also get sum_k x2[n,p,q,k] * w2[co][k], k < C2.
   const bf16_t* x2; int ldx2; const bf16_t* w2; int C2;
+  // optional split output: channels co >= csplit go to ysplit[pix*ldysplit +
+  // co - csplit] instead of y (a concat gradient whose narrow up-conv part is
+  // kept in its own dense buffer so its consumers read whole cache lines)
+  bf16_t* ysplit; int ldysplit; int csplit;
   int N, H, W, C;                // input geometry (C = GEMM reduction channels)
   int P, Q, Cout;                // output geometry
   int R, S, stride, pad;
@@ -93,6 +100,9 @@ void set_conv_ws(int on);
 void set_conv_impl(int glds);  // 1: LDS-DMA pipelined kernels (default), 0: register-staged v1
 void set_conv_config(int cfg);  // 0: automatic tile selection, >0: fixed tile config (tuning)
 hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st);
+// ConvTranspose2d(k2,s2) weight gradient (XLOAD_SHUF): dy = X [N,P,Q,Ci] (Cout = Ci),
+// x = dY [N,H=2P,W=2Q,Co] with C = 4*Co; dw [Ci][4][Co]
+hipError_t launch_convt_wgrad(const ConvWgradArgs& a, hipStream_t st);
 // sums the split-K slab of the preceding launch_conv_wgrad into dW (no-op if it used atomics)
 hipError_t launch_wgrad_finish(hipStream_t st);
 bool wgrad_pending();

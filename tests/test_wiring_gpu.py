@@ -72,6 +72,14 @@ def _masked(a, b, act):
     return _rel(a * m, b * m)
 
 
+def _dcat(v, p):
+    """concat gradient of decoder p: one buffer, or (decoder1) the skip part and
+    the narrow up-conv part the executor keeps in separate dense buffers."""
+    if p + "d.cat" in v:
+        return v[p + "d.cat"]
+    return torch.cat([v[p + "d.cat.skip"], v[p + "d.cat.up"]], 1)
+
+
 def _check(rows):
     for name, e in rows:
         print(f"{name:28s} {e:.3e}")
@@ -150,11 +158,11 @@ def test_backward_ops(run):
         dy1, dg, db = local_bn_bwd(v[p + "y1"], v[p + "d.h"], dec[1], out=v[p + "h"])
         rows += [(p + "d.y1", _rel(v[p + "d.y1"], dy1)), (f"g decoder{lvl}.1.weight", _rel(grads[f"decoder{lvl}.1.weight"], dg))]
         dcat = torch.nn.grad.conv2d_input(v[p + "cat"].shape, W(dec[0]), v[p + "d.y1"], padding=1)
-        rows.append((p + "d.cat", _rel(v[p + "d.cat"], dcat)))
+        rows.append((p + "d.cat", _rel(_dcat(v, p), dcat)))
         gw = torch.nn.grad.conv2d_weight(v[p + "cat"], dec[0].weight.shape, v[p + "d.y1"], padding=1)
         rows.append((f"g decoder{lvl}.0.weight", _rel(grads[f"decoder{lvl}.0.weight"], gw)))
         sk = skips[lvl][1]
-        du = v[p + "d.cat"][:, sk:]
+        du = _dcat(v, p)[:, sk:]
         upin_name = "enc4.2.out" if lvl == 4 else f"dec{lvl + 1}.out"
         xin = v[upin_name].clone().requires_grad_(True)
         wl = W(up).clone().requires_grad_(True)
@@ -209,7 +217,7 @@ def test_backward_ops(run):
             din = din + skip.grad
         if b == 0 and s > 0:
             lvl = {1: 2, 2: 3, 3: 4}[s]
-            din = din + v[f"dec{lvl}.d.cat"][:, :inp.shape[1]]
+            din = din + _dcat(v, f"dec{lvl}.")[:, :inp.shape[1]]
         tgt = "d.p0" if i == 0 else names[i - 1][0] + "d.out"
         rows.append((tgt + " (block dgrad)", _rel(v[tgt], din) if i == 0 else _masked(v[tgt], din, inp)))
         rows.append((f"g {p}conv1.weight", _rel(grads[p + "conv1.weight"], torch.nn.grad.conv2d_weight(
@@ -217,7 +225,7 @@ def test_backward_ops(run):
     # maxpool + stem
     x1 = v["x1"].clone().requires_grad_(True)
     F.max_pool2d(x1, 3, 2, 1).backward(v["d.p0"])
-    rows.append(("d.x1", _masked(v["d.x1"], x1.grad + v["dec1.d.cat"][:, :64], v["x1"])))
+    rows.append(("d.x1", _masked(v["d.x1"], x1.grad + _dcat(v, "dec1.")[:, :64], v["x1"])))
     dy0, dg, db = local_bn_bwd(v["y0"], v["d.x1"], ref.bn1, out=v["x1"])
     rows += [("g bn1.weight", _rel(grads["bn1.weight"], dg)), ("g bn1.bias", _rel(grads["bn1.bias"], db))]
     if "d.y0" in v:  # unfused build only: the fused stem wgrad never stores the stem dY
