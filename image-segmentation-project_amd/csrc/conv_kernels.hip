@@ -1027,14 +1027,30 @@ constexpr int kStemPatchPT = (7 * (2 * 256 + 6) + 255) / 256;  // patch values p
 
 struct StemPatch { float v[kStemPatchPT]; };
 
-// registers <- img rows 2*oh-3 .. 2*oh+3, cols -3 .. 2Q+2 (zero outside)
-__device__ __forceinline__ void stem_fetch(const float* img, int n, int oh, int H, int W, int Q, StemPatch& p) {
-  const int cols = 2 * Q + 6;
+// The stem walks UNITS of <= 256 output pixels: unit u is output row
+// u / nseg, columns q0 = (u % nseg) * 256 .. q0 + Q - 1 (nseg = ceil(Q / 256)),
+// so rows wider than one 256-thread block (the 1024^2 HiRes input) are split.
+struct StemUnit { int n, oh, q0, Qs; size_t row; };
+__device__ __forceinline__ StemUnit stem_unit(int u, int P, int Q) {
+  const int nseg = (Q + 255) >> 8;
+  StemUnit t;
+  const int row = u / nseg;
+  t.row = (size_t)row;
+  t.n = row / P;
+  t.oh = row - t.n * P;
+  t.q0 = (u - row * nseg) << 8;
+  t.Qs = min(256, Q - t.q0);
+  return t;
+}
+
+// registers <- img rows 2*oh-3 .. 2*oh+3, cols 2*q0-3 .. 2*(q0+Q)+2 (zero outside)
+__device__ __forceinline__ void stem_fetch(const float* img, const StemUnit& t, int H, int W, StemPatch& p) {
+  const int cols = 2 * t.Qs + 6;
 #pragma unroll
   for (int j = 0; j < kStemPatchPT; ++j) {
     const int i = threadIdx.x + j * 256;
     const int r = i / cols, c = i - r * cols;
-    const int ih = 2 * oh - 3 + r, iw = c - 3;
+    const int n = t.n, ih = 2 * t.oh - 3 + r, iw = 2 * t.q0 + c - 3;
     p.v[j] = (r < 7 && ih >= 0 && ih < H && iw >= 0 && iw < W) ? img[((size_t)n * H + ih) * W + iw] : 0.f;
   }
 }
@@ -1073,7 +1089,7 @@ __global__ void __launch_bounds__(256, 2) stem_fwd_kernel(ConvFwdArgs a, int row
   bf16_t* patch = reinterpret_cast<bf16_t*>(smem + 64 * 128 + 256 * 128);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* img = reinterpret_cast<const float*>(a.x);
-  const int total_rows = a.N * a.P;
+  const int total_rows = a.N * a.P * ((a.Q + 255) >> 8);  // units
   const int r0 = xcd_remap(blockIdx.x, gridDim.x) * rows_per_block;
   const int r1 = min(total_rows, r0 + rows_per_block);
   {  // packed weights [64][64] bf16 -> swizzled LDS rows
@@ -1090,15 +1106,16 @@ __global__ void __launch_bounds__(256, 2) stem_fwd_kernel(ConvFwdArgs a, int row
 #pragma unroll
     for (int e = 0; e < 4; ++e) q0[i][e] = q1[i][e] = 0.f;
   StemPatch pf;
-  if (r0 < r1) stem_fetch(img, r0 / a.P, r0 % a.P, a.H, a.W, a.Q, pf);
-  for (int row = r0; row < r1; ++row) {
-    __syncthreads();  // previous row's patch / im2col consumed
-    stem_store_patch(pf, a.Q, patch);
-    if (row + 1 < r1) stem_fetch(img, (row + 1) / a.P, (row + 1) % a.P, a.H, a.W, a.Q, pf);
+  if (r0 < r1) stem_fetch(img, stem_unit(r0, a.P, a.Q), a.H, a.W, pf);
+  for (int u = r0; u < r1; ++u) {
+    const StemUnit t = stem_unit(u, a.P, a.Q);
+    __syncthreads();  // previous unit's patch / im2col consumed
+    stem_store_patch(pf, t.Qs, patch);
+    if (u + 1 < r1) stem_fetch(img, stem_unit(u + 1, a.P, a.Q), a.H, a.W, pf);
     __syncthreads();
     {
       uint4 r8[8];
-      if (tid < a.Q) {
+      if (tid < t.Qs) {
         stem_im2col_row(patch, tid, r8);
       } else {
 #pragma unroll
@@ -1134,8 +1151,8 @@ __global__ void __launch_bounds__(256, 2) stem_fwd_kernel(ConvFwdArgs a, int row
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int px = wave * 64 + j * 16 + (lane & 15);
-      if (px < a.Q) {
-        bf16_t* yrow = a.y + ((size_t)row * a.Q + px) * a.ldy;
+      if (px < t.Qs) {
+        bf16_t* yrow = a.y + (t.row * a.Q + t.q0 + px) * a.ldy;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int co = i * 16 + ((lane >> 4) << 2);
@@ -1198,7 +1215,7 @@ __global__ void __launch_bounds__(256, 2) stem_wgrad_kernel(ConvWgradArgs a, int
   const int wm = wave & 1, wn = wave >> 1;  // 32 co x 32 k per wave
   const int g = lane >> 4, li = lane & 15, trq = li >> 2, trp = li & 3;
   const float* img = reinterpret_cast<const float*>(a.x);
-  const int total_rows = a.N * a.P;
+  const int total_rows = a.N * a.P * ((a.Q + 255) >> 8);  // units (stem_unit)
   const int r0 = xcd_remap(blockIdx.x, gridDim.x) * rows_per_block;
   const int r1 = min(total_rows, r0 + rows_per_block);
   f32x4 acc[2][2];
@@ -1207,29 +1224,31 @@ __global__ void __launch_bounds__(256, 2) stem_wgrad_kernel(ConvWgradArgs a, int
   // register prefetch of the next row: dY (8 x 16 B per thread) + input patch
   uint4 dyv[8];
   StemPatch pf;
-  auto fetch = [&](int row) {
+  auto fetch = [&](int u) {
+    const StemUnit t = stem_unit(u, a.P, a.Q);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int i = tid + j * 256, px = i >> 3, c8 = i & 7;
-      dyv[j] = px < a.Q ? *reinterpret_cast<const uint4*>(a.dy + ((size_t)row * a.Q + px) * a.lddy + c8 * 8)
-                        : make_uint4(0, 0, 0, 0);
+      dyv[j] = px < t.Qs ? *reinterpret_cast<const uint4*>(a.dy + (t.row * a.Q + t.q0 + px) * a.lddy + c8 * 8)
+                         : make_uint4(0, 0, 0, 0);
     }
-    stem_fetch(img, row / a.P, row % a.P, a.H, a.W, a.Q, pf);
+    stem_fetch(img, t, a.H, a.W, pf);
   };
   if (r0 < r1) fetch(r0);
   for (int row = r0; row < r1; ++row) {
-    __syncthreads();  // previous row's tiles consumed
+    const StemUnit t = stem_unit(row, a.P, a.Q);
+    __syncthreads();  // previous unit's tiles consumed
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int i = tid + j * 256, px = i >> 3, c8 = i & 7;
       *reinterpret_cast<uint4*>(Ds + TT::off(px, c8 * 8)) = dyv[j];
     }
-    stem_store_patch(pf, a.Q, patch);
+    stem_store_patch(pf, t.Qs, patch);
     if (row + 1 < r1) fetch(row + 1);
     __syncthreads();
     {
       uint4 r8[8];
-      if (tid < a.Q) {
+      if (tid < t.Qs) {
         stem_im2col_row(patch, tid, r8);
       } else {
 #pragma unroll
@@ -1274,8 +1293,8 @@ __global__ void __launch_bounds__(256, 2) stem_wgrad_kernel(ConvWgradArgs a, int
 }
 
 hipError_t launch_stem_fwd(const ConvFwdArgs& a, hipStream_t st) {
-  if (a.Cout != 64 || a.Q > 256 || a.R != 7 || a.stride != 2 || a.pad != 3) return hipErrorInvalidValue;
-  const int rows = a.N * a.P;
+  if (a.Cout != 64 || a.R != 7 || a.stride != 2 || a.pad != 3) return hipErrorInvalidValue;
+  const int rows = a.N * a.P * ((a.Q + 255) / 256);  // 256-pixel units
   const int per = std::max(1, (rows + 511) / 512);  // ~2 blocks per CU
   const size_t lds = 64 * 128 + 256 * 128 + 7 * kStemPatchW * 2;
   set_kernel_tag("stem_fwd_kernel");
@@ -1284,8 +1303,8 @@ hipError_t launch_stem_fwd(const ConvFwdArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_stem_wgrad(const ConvWgradArgs& a, hipStream_t st) {
-  if (a.Cout != 64 || a.Q > 256 || a.R != 7 || a.stride != 2 || a.pad != 3) return hipErrorInvalidValue;
-  const int rows = a.N * a.P;
+  if (a.Cout != 64 || a.R != 7 || a.stride != 2 || a.pad != 3) return hipErrorInvalidValue;
+  const int rows = a.N * a.P * ((a.Q + 255) / 256);  // 256-pixel units
   const int per = std::max(1, (rows + 511) / 512);  // ~2 blocks per CU
   const size_t lds = 2 * 256 * 128 + 7 * kStemPatchW * 2;
   set_kernel_tag("stem_wgrad_kernel");
