@@ -154,16 +154,15 @@ conv_fwd_kernel(ConvFwdArgs a) {
       const int row = tid / CPR + i * A_ROWS_PER_PASS;
       if (row < BM && an[i] >= 0) {
         if constexpr (ALOAD == ALOAD_STEM) {
-          // im2col of the fp32 image: k = ach*8 + e -> (kr, ks) = (k/7, k%7)
+          // im2col of the fp32 image: k = ach*8 + e -> (kr, ks) = (ach, e), ks < 7
           const float* img = reinterpret_cast<const float*>(a.x);
           float f[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const int k = ach * 8 + e;
-            const int kr = k / 7, ks = k - kr * 7;
+            const int kr = ach, ks = e;
             const int ih = aa[i] * st - a.pad + kr;
             const int iw = ab[i] * st - a.pad + ks;
-            f[e] = (k < 49 && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+            f[e] = (kr < 7 && ks < 7 && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
                        ? img[((size_t)an[i] * a.H + ih) * a.W + iw] : 0.f;
           }
           v = pack8(f);
@@ -743,9 +742,9 @@ conv_wgrad_kernel(ConvWgradArgs a) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             const int k = c0 + ch * 8 + e;
-            const int kr = k / 7, ks = k - kr * 7;
+            const int kr = k >> 3, ks = k & 7;  // stem K layout: k = kr*8 + ks, ks < 7
             const int ih = p * a.stride - a.pad + kr, iw = q * a.stride - a.pad + ks;
-            f[e] = (k < 49 && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+            f[e] = (kr < 7 && ks < 7 && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
                        ? img[((size_t)n * a.H + ih) * a.W + iw] : 0.f;
           }
           v = pack8(f);
@@ -858,7 +857,12 @@ conv_wgrad_kernel(ConvWgradArgs a) {
 // wgrad_slab_reduce_kernel sums the splits (fp32 atomics into dW when no slab:
 // they run at ~1.3 TB/s chip-wide, MI355X_MICROARCH.md "Global float atomics").
 // ---------------------------------------------------------------------------
-template <int TW, int NS, int CI>
+// CO32 (Cout = 32 layers, decoder1): a block owns 32 output channels; the
+// two waves of a (wm) pair split each stage's 128 pixels instead of the 64
+// channels (no MFMA on the absent channels 32..63), and their partial dW are
+// summed through LDS before the store.  The dY DMA still moves 128-B rows
+// (pixel p's 32 channels + pixel p+1's, unused).
+template <int TW, int NS, int CI, bool CO32 = false>
 __global__ void __launch_bounds__(CI * 8)
 wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
   constexpr int NW = CI / 8;            // waves
@@ -883,7 +887,7 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
   const int wm = wave & 1, wn = wave >> 1;  // wave tile 32 co x 16 ci
   const int cob = blockIdx.x % a.co_blocks;
   const int cib = blockIdx.x / a.co_blocks;
-  const int co0 = cob * 64, c0 = cib * CI;
+  const int co0 = cob * (CO32 ? 32 : 64), c0 = cib * CI;
   const int t0 = blockIdx.z * tiles_per_split;
   const int t1 = min(tiles_total, t0 + tiles_per_split);
   const int KT = t1 - t0;
@@ -948,12 +952,13 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
     const char* As = smem + (kt % NS) * STAGE;
     const char* Bs = As + A_BYTES;
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
+    for (int k2 = 0; k2 < (CO32 ? 2 : 4); ++k2) {
+      const int kk = CO32 ? wm * 2 + k2 : k2;    // CO32: the wm pair splits the pixels
       const int p_lo = kk * 32 + 8 * g + trq;  // this lane's pixel (first tr read)
       bf16x8 af[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const int col = wm * 32 + i * 16 + 4 * trp;
+        const int col = (CO32 ? 0 : wm * 32) + i * 16 + 4 * trp;
         af[i] = tr_read8(As + TA::off(p_lo, col), As + TA::off(p_lo + 4, col));
       }
       const int ty = p_lo / TW, tx = p_lo % TW;  // p_lo and p_lo+4 share the tile row
@@ -971,6 +976,22 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
     }
   }
   wait_vmcnt<0>();
+  if constexpr (CO32) {  // fold the wm = 1 partials into wm = 0 through LDS
+    __syncthreads();     // every stage consumed: the staging LDS is free
+    f32x4* red = reinterpret_cast<f32x4*>(smem) + (size_t)(wn * 18) * 64 + lane;
+    if (wm == 1) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) red[(t * 2 + i) * 64] = acc[t][i];
+    }
+    __syncthreads();
+    if (wm == 1) return;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[t][i] += red[(t * 2 + i) * 64];
+  }
   // epilogue: this split's partial dW[co][tap][ci] (plain stores into the
   // slab) or fp32 atomics into dW
   const int Krow = 9 * a.C;
@@ -982,7 +1003,7 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int co = co0 + wm * 32 + i * 16 + 4 * g + e;
+        const int co = co0 + (CO32 ? 0 : wm * 32) + i * 16 + 4 * g + e;
         if (co < a.Cout) {
           if (slab) slab[(size_t)co * Krow + t * a.C + c] = acc[t][i][e];
           else atomicAdd(a.dw + (size_t)co * Krow + t * a.C + c, acc[t][i][e]);
@@ -1064,21 +1085,16 @@ __device__ __forceinline__ void stem_store_patch(const StemPatch& p, int Q, bf16
   }
 }
 
-// im2col row of pixel px (k = kr*7+ks < 49, zero above) as 8 x 16 B
+// im2col row of pixel px as 8 x 16 B in the stem K layout k = kr*8 + ks
+// (ks = 7 and kr = 7 are zero): chunk kr is the 8 patch values of row kr from
+// column 2*px on (4-B aligned), read as 4 dwords, with the 8th value masked
 __device__ __forceinline__ void stem_im2col_row(const bf16_t* patch, int px, uint4 (&row)[8]) {
 #pragma unroll
-  for (int c8 = 0; c8 < 8; ++c8) {
-    unsigned w[4];
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      unsigned lo = 0, hi = 0;
-      const int k0 = c8 * 8 + 2 * h, k1 = k0 + 1;
-      if (k0 < 49) lo = patch[(k0 / 7) * kStemPatchW + 2 * px + (k0 % 7)];
-      if (k1 < 49) hi = patch[(k1 / 7) * kStemPatchW + 2 * px + (k1 % 7)];
-      w[h] = lo | (hi << 16);
-    }
-    row[c8] = make_uint4(w[0], w[1], w[2], w[3]);
+  for (int kr = 0; kr < 7; ++kr) {
+    const unsigned* w = reinterpret_cast<const unsigned*>(patch + kr * kStemPatchW + 2 * px);
+    row[kr] = make_uint4(w[0], w[1], w[2], w[3] & 0xffffu);
   }
+  row[7] = make_uint4(0, 0, 0, 0);
 }
 
 __global__ void __launch_bounds__(256, 2) stem_fwd_kernel(ConvFwdArgs a, int rows_per_block) {
@@ -1530,30 +1546,31 @@ static thread_local PendingReduce g_pending{};
 
 // splits so that the grid is ~one block per CU (the halo kernels hold 96-144 KB
 // of LDS), at least one tile per split
-template <int TW, int CI>
+template <int TW, int CI, bool CO32>
 static void halo_geometry(const ConvWgradArgs& a, int& blocks_xy, int& tiles, int& per, int& splits) {
   constexpr int TH = 128 / TW;
-  blocks_xy = ((a.Cout + 63) / 64) * (a.C / CI);
+  blocks_xy = (CO32 ? a.Cout / 32 : (a.Cout + 63) / 64) * (a.C / CI);
   tiles = a.N * (a.P / TH) * (a.Q / TW);
   splits = std::max(1, std::min(tiles, 256 / blocks_xy));
   per = (tiles + splits - 1) / splits;
   splits = (tiles + per - 1) / per;
 }
 
-template <int TW, int CI>
+template <int TW, int CI, bool CO32 = false>
 static hipError_t launch_wgrad_halo(const ConvWgradArgs& a0, hipStream_t st) {
   ConvWgradArgs a = a0;
-  a.co_blocks = (a.Cout + 63) / 64;
+  a.co_blocks = CO32 ? a.Cout / 32 : (a.Cout + 63) / 64;
   a.c_blocks = a.C / CI;
   int blocks_xy, tiles, per, splits;
-  halo_geometry<TW, CI>(a, blocks_xy, tiles, per, splits);
+  halo_geometry<TW, CI, CO32>(a, blocks_xy, tiles, per, splits);
   const int64_t n = (int64_t)a.Cout * 9 * a.C;
   if (a.slab && (size_t)splits * n * sizeof(float) > a.slab_bytes) a.slab = nullptr;  // atomics instead
   constexpr int NS = CI == 64 ? 3 : 4;
   const size_t lds = (size_t)NS * (128 * 128 + 256 * CI * 2);
-  set_kernel_tag("wgrad3x3_halo_kernel<%d, %d, %d>", TW, NS, CI);
-  hipLaunchKernelGGL((wgrad3x3_halo_kernel<TW, NS, CI>), dim3(blocks_xy, 1, splits), dim3(CI * 8), lds, st, a,
-                     tiles, per);
+  if (CO32) set_kernel_tag("wgrad3x3_halo_kernel<%d, %d, %d, true>", TW, NS, CI);
+  else set_kernel_tag("wgrad3x3_halo_kernel<%d, %d, %d>", TW, NS, CI);
+  hipLaunchKernelGGL((wgrad3x3_halo_kernel<TW, NS, CI, CO32>), dim3(blocks_xy, 1, splits), dim3(CI * 8), lds, st,
+                     a, tiles, per);
   if (a.slab) g_pending = PendingReduce{a.slab, a.dw, n, splits};
   return hipGetLastError();
 }
@@ -1589,6 +1606,7 @@ hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st) {
       if (a.Q % 32 == 0 && a.P % 4 == 0) return launch_wgrad_halo<32, 64>(a, st);
       if (a.Q % 16 == 0 && a.P % 8 == 0) return launch_wgrad_halo<16, 64>(a, st);
     }
+    if (a.Cout == 32 && a.Q % 32 == 0 && a.P % 4 == 0) return launch_wgrad_halo<32, 32, true>(a, st);
     if (a.Q % 32 == 0 && a.P % 4 == 0) return launch_wgrad_halo<32, 32>(a, st);
     if (a.Q % 16 == 0 && a.P % 8 == 0) return launch_wgrad_halo<16, 32>(a, st);
   }

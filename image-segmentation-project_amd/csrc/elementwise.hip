@@ -568,6 +568,91 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(MaxPoolArgs a, int rpb
   if (bb.ticket && last_block_arrive(bb.ticket, gridDim.x, &flag, (int)threadIdx.x < a.C)) bn_bwd_finalize(bb);
 }
 
+// Stem forward tail in one pass: act = relu(bn(x)) (x = raw 7x7 conv output)
+// and MaxPool2d(3,2,1) of act.  Pooled pixel (p, q) owns act pixels
+// (2p + a, 2q + b), a, b in {0, 1} (H, W even), so every act pixel is written
+// exactly once; the pooling compares the bf16-ROUNDED act values, exactly as
+// the unfused maxpool reading act back from HBM would.  Replaces bn_apply +
+// maxpool_fwd (act is read back 2.3x by the unfused pooling, PMC).
+__global__ void __launch_bounds__(256) bn_relu_maxpool_fwd_kernel(MaxPoolArgs a, int rpb) {
+  const int CC = a.C >> 3;
+  const int chunk = threadIdx.x % CC;
+  const int c8 = chunk << 3;
+  const int per_row = a.Q * CC;
+  const int nrows = a.N * a.P;
+  __shared__ float coef[2][256];
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+    float m, inv, var;
+    if (a.bn.training && a.bn.ss) { coef[0][c] = a.bn.ss[c]; coef[1][c] = a.bn.ss[a.C + c]; }
+    else bn_scale_shift(a.bn, c, coef[0][c], coef[1][c], m, inv, var);
+  }
+  __syncthreads();
+  float sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { sc[k] = coef[0][c8 + k]; sh[k] = coef[1][c8 + k]; }
+  for (int rr = 0; rr < rpb; ++rr) {
+    const int orow = blockIdx.x * rpb + rr;
+    if (orow >= nrows) break;
+    const int n = orow / a.P, p = orow - n * a.P;
+    const bf16_t* xrow[3];
+    bf16_t* arow[3];
+    bool rok[3];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = 2 * p - 1 + kh;
+      rok[kh] = ih >= 0 && ih < a.H;
+      const size_t base = (size_t)(n * a.H + (rok[kh] ? ih : 0)) * a.W;
+      xrow[kh] = a.x + base * a.ldx + c8;
+      arow[kh] = a.act + base * a.ldact + c8;
+    }
+    for (int e = threadIdx.x; e < per_row; e += blockDim.x) {
+      const int q = e / CC;
+      uint4 u[9];
+      bool ok[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int kh = t / 3, kw = t % 3;
+        const int iw = 2 * q - 1 + kw;
+        ok[t] = rok[kh] && iw >= 0 && iw < a.W;
+        u[t] = ok[t] ? *reinterpret_cast<const uint4*>(xrow[kh] + (size_t)iw * a.ldx) : make_uint4(0, 0, 0, 0);
+      }
+      float best[8];
+      int bi[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; bi[k] = -1; }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        if (!ok[t]) continue;
+        float v[8];
+        unpack8(u[t], v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float z = v[k] * sc[k] + sh[k];
+          v[k] = z > 0.f ? z : 0.f;
+        }
+        const uint4 r = pack8(v);  // the stored act value
+        unpack8(r, v);
+        const int kh = t / 3, kw = t % 3;
+        if (kh >= 1 && kw >= 1) *reinterpret_cast<uint4*>(arow[kh] + (size_t)(2 * q - 1 + kw) * a.ldact) = r;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const bool take = bi[k] < 0 || v[k] > best[k] || (v[k] != v[k] && best[k] == best[k]);
+          best[k] = take ? v[k] : best[k];
+          bi[k] = take ? t : bi[k];
+        }
+      }
+      const size_t opix = (size_t)orow * a.Q + q;
+      *reinterpret_cast<uint4*>(a.y + opix * a.ldy + c8) = pack8(best);
+      uint2 ix;
+      ix.x = (unsigned)bi[0] | ((unsigned)bi[1] << 8) | ((unsigned)bi[2] << 16) | ((unsigned)bi[3] << 24);
+      ix.y = (unsigned)bi[4] | ((unsigned)bi[5] << 8) | ((unsigned)bi[6] << 16) | ((unsigned)bi[7] << 24);
+      *reinterpret_cast<uint2*>(a.idx + opix * a.C + c8) = ix;
+    }
+  }
+  // batch statistics of the BN (save_mean/invstd, running stats): block 0
+  if (blockIdx.x == 0 && !a.bn.ss) bn_finalize_block0(a.bn, threadIdx.x, blockDim.x, 0, a.C);
+}
+
 static inline int rows_per_block(int nrows, int target_blocks) {
   return (nrows + target_blocks - 1) / target_blocks;
 }
@@ -579,6 +664,14 @@ hipError_t launch_maxpool_fwd(const MaxPoolArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3((nrows + rpb - 1) / rpb), dim3(256), 0, st, a, rpb);
   return hipGetLastError();
 }
+hipError_t launch_bn_relu_maxpool_fwd(const MaxPoolArgs& a, hipStream_t st) {
+  if (a.C % 8 || 256 % (a.C / 8) || a.C > 256 || a.H != 2 * a.P || a.W != 2 * a.Q) return hipErrorInvalidValue;
+  const int nrows = a.N * a.P;
+  const int rpb = rows_per_block(nrows, 2048);
+  hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel, dim3((nrows + rpb - 1) / rpb), dim3(256), 0, st, a, rpb);
+  return hipGetLastError();
+}
+
 hipError_t launch_maxpool_bwd(const MaxPoolArgs& a, hipStream_t st) {
   if (a.C % 8 || 256 % (a.C / 8)) return hipErrorInvalidValue;
   if (a.bb.sums && a.bb.y2) return hipErrorInvalidValue;
@@ -852,11 +945,11 @@ __global__ void __launch_bounds__(256) pack_kernel(PackTable t) {
   // one LDS buffer for either path: [kPkTB*T][kPkTA+1] tile or a [B*T] row
   __shared__ float lds[kPkTB * kPkTmax * (kPkTA + 1)];
   static_assert(512 * kPkTmax <= kPkTB * kPkTmax * (kPkTA + 1), "row fits");
-  if (e.kind == PK_STEM) {  // dst[co][k], k < 49 -> W[co][0][k/7][k%7]
+  if (e.kind == PK_STEM) {  // dst[co][k], k = kr*8 + ks -> W[co][0][kr][ks] (kr, ks < 7; else 0)
     const int total = e.Co * 64;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-      const int k = i & 63, co = i >> 6;
-      e.dst[i] = f2bf(k < 49 ? e.src[co * 49 + k] : 0.f);
+      const int kr = (i >> 3) & 7, ks = i & 7, co = i >> 6;
+      e.dst[i] = f2bf(kr < 7 && ks < 7 ? e.src[co * 49 + kr * 7 + ks] : 0.f);
     }
     return;
   }
@@ -953,9 +1046,10 @@ __global__ void __launch_bounds__(256) unpack_kernel(UnpackTable t) {
       const int aa = (int)(q % R); q /= R;
       const int co = (int)(q % Co); const int ci = (int)(q / Co);
       v = e.acc[(((int)ci * R + aa) * S + b) * Co + co];
-    } else {  // UP_STEM: dst[co][0][r][s] <- acc[co][r*7+s] (row length 64)
+    } else {  // UP_STEM: dst[co][0][r][s] <- acc[co][r*8+s] (row length 64)
       const int k = (int)(i % 49), co = (int)(i / 49);
-      v = e.acc[(int)co * 64 + k];
+      const int r = k / 7, ss = k - r * 7;
+      v = e.acc[(int)co * 64 + r * 8 + ss];
     }
     e.dst[i] = v;
   }

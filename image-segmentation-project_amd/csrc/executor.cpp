@@ -795,13 +795,16 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
       ProfScope ps(p, st, "fwd input_conv.weight", 2.0 * N * p->y0.H * p->y0.W * cv.Co * 49);
       CK(launch_conv_fwd(a, MODE_STEM, st));
     }
-    RUN(bn_apply(x, p->stem_bn, p->y0, p->x1, 0, nullptr, -1, true));
+    // bn1 + relu + maxpool in one pass: x1 (the decoder1 skip, inside the
+    // concat buffer) and the pooled p0 + argmax index
     MaxPoolArgs m = {};
-    m.x = x.A(p->x1); m.ldx = p->x1.ld; m.y = x.A(p->p0); m.ldy = p->p0.ld; m.idx = x.W<uint8_t>(p->pidx);
+    m.x = x.A(p->y0); m.ldx = p->y0.ld; m.y = x.A(p->p0); m.ldy = p->p0.ld; m.idx = x.W<uint8_t>(p->pidx);
+    m.act = x.A(p->x1); m.ldact = p->x1.ld;
+    m.bn = bn_launch(x, p->stem_bn, (int64_t)N * p->y0.H * p->y0.W);
     m.N = N; m.H = p->x1.H; m.W = p->x1.W; m.C = p->x1.C; m.P = p->p0.H; m.Q = p->p0.W;
     {
-      ProfScope ps(p, st, "maxpool_fwd", 0);
-      CK(launch_maxpool_fwd(m, st));
+      ProfScope ps(p, st, "bn_relu_maxpool_fwd", 0);
+      CK(launch_bn_relu_maxpool_fwd(m, st));
     }
   }
   for (auto& b : p->blocks) {

@@ -131,8 +131,13 @@ struct MaxPoolArgs {
   // conv-dgrad epilogue, store dZ = dA * (act > 0) and run its BN-backward
   // reduction (bb.sums != null)
   BnBwdArgs bb;
+  // forward, fused (launch_bn_relu_maxpool_fwd): x is the RAW conv output of
+  // BN `bn`; act = relu(bn(x)) is written to act (every pixel once) and pooled
+  BnLaunch bn; bf16_t* act; int ldact;
 };
 hipError_t launch_maxpool_fwd(const MaxPoolArgs& a, hipStream_t st);
+// stem: BN apply + ReLU + MaxPool2d(3,2,1) in one pass over the raw conv output
+hipError_t launch_bn_relu_maxpool_fwd(const MaxPoolArgs& a, hipStream_t st);
 hipError_t launch_maxpool_bwd(const MaxPoolArgs& a, hipStream_t st);
 
 // fused ConvTranspose2d(k2,s2, Cin->16) + Conv1x1(16->1): logits[2i+a,2j+b] =

@@ -202,8 +202,9 @@ def test_convT_wgrad(L, cuda):
     close(out, w.grad, rel=2e-3)
 
 
-def test_stem_fwd_and_wgrad(L, cuda):
-    N, H, Co = 2, 64, 64
+@pytest.mark.parametrize("N,H", [(2, 64), (1, 1024)])
+def test_stem_fwd_and_wgrad(L, N, H, cuda):
+    Co = 64
     g = torch.Generator().manual_seed(6)
     img = torch.rand(N, 1, H, H, generator=g)
     w = torch.randn(Co, 1, 7, 7, generator=g) / 7.0
