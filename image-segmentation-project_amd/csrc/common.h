@@ -53,6 +53,14 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, char* lds_wave_
                                            0, 0);
 }
 
+// same, with a wave-uniform byte offset added to voff after the range check
+// (raw buffer: soffset is not part of the num_records test), so a kOOB lane
+// stays zero-filled whatever the stage offset
+__device__ __forceinline__ void glds16s(__amdgpu_buffer_rsrc_t r, char* lds_wave_base, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, soff,
+                                           0, 0);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -59,25 +59,6 @@ constexpr int kHW = 18;  // halo width: 16 output columns + 2
 // Halo of one output tile (TH x 16 at (n, oh0, ow0)): np 32-channel panels of
 // input channels c0 .. c0 + 32*np into LDS, HPR rows per panel.  DMA
 // instructions are dealt round-robin over the NW waves.
-template <int TH, int NW>
-__device__ __forceinline__ void issue_halo_dma(const ConvFwdArgs& a, __amdgpu_buffer_rsrc_t xr, char* dst, int n,
-                                               int oh0, int ow0, int c0, int np, int wave, int lane) {
-  constexpr int HP = (TH + 2) * kHW;
-  constexpr int HPR = (HP + 15) / 16 * 16;
-  const int nins = np * HPR / 16;
-  for (int ins = wave; ins < nins; ins += NW) {
-    const int rowg = ins * 16 + (lane >> 2);
-    const int p = rowg / HPR, hp = rowg - p * HPR;
-    const int lchunk = (lane & 3) ^ ((hp >> 1) & 2);
-    const int hr = hp / kHW, hc = hp - hr * kHW;
-    const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
-    unsigned off = kOOB;
-    if (hp < HP && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
-      off = (unsigned)((((n * a.H + ih) * a.W + iw) * a.ldx + c0 + p * 32 + lchunk * 8) * 2);
-    glds16(xr, dst + ins * 1024, off);
-  }
-}
-
 // 9 taps x COT output rows x np panels of 32 reduction channels from kc0,
 // LDS layout [tap][panel][co][32]; weights packed [Cout][9][K = a.C].
 template <int COT, int NW>
@@ -369,6 +350,31 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
 #pragma unroll
     for (int d = 0; d < 3; ++d) boff[h][d] = ws_off((wave * RW + h) * kHW + d + (lane & 15), lane >> 4);
 
+  // per-lane constant part of the halo DMA (pixel of the halo, channel
+  // offset); per tile only the image bounds test and the address remain
+  constexpr int H_NINS = NP * HPR / 16, H_PER = (H_NINS + NW - 1) / NW;
+  int hrow[H_PER], hcol[H_PER], hch[H_PER];
+#pragma unroll
+  for (int k = 0; k < H_PER; ++k) {
+    const int rowg = (wave + k * NW) * 16 + (lane >> 2);
+    const int p = rowg / HPR, hp = rowg - p * HPR;
+    const int lchunk = (lane & 3) ^ ((hp >> 1) & 2);
+    hrow[k] = hp < (TH + 2) * kHW ? hp / kHW - 1 : -(1 << 20);  // invalid rows fail the bounds test
+    hcol[k] = hp - (hp / kHW) * kHW - 1;
+    hch[k] = p * 32 + lchunk * 8;
+  }
+  auto issue_halo = [&](char* dst, int n, int oh0, int ow0) {
+#pragma unroll
+    for (int k = 0; k < H_PER; ++k) {
+      if (wave + k * NW >= H_NINS) break;
+      const int ih = oh0 + hrow[k], iw = ow0 + hcol[k];
+      unsigned off = kOOB;
+      if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+        off = (unsigned)((((n * a.H + ih) * a.W + iw) * a.ldx + hch[k]) * 2);
+      glds16(xr, dst + (wave + k * NW) * 1024, off);
+    }
+  };
+
   auto tile_origin = [&](int t, int& n, int& oh0, int& ow0) {
     n = t / (tp * tq);
     const int rem = t - n * (tp * tq);
@@ -380,7 +386,7 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
   if (t < ntiles) {
     int n, oh0, ow0;
     tile_origin(t, n, oh0, ow0);
-    issue_halo_dma<TH, NW>(a, xr, hl, n, oh0, ow0, 0, NP, wave, lane);
+    issue_halo(hl, n, oh0, ow0);
   }
   wait_vmcnt<0>();
   __syncthreads();
@@ -390,7 +396,7 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
     if (t + nslot < ntiles) {  // lands while this tile computes
       int n, oh0, ow0;
       tile_origin(t + nslot, n, oh0, ow0);
-      issue_halo_dma<TH, NW>(a, xr, hl + (b ^ 1) * HBUF, n, oh0, ow0, 0, NP, wave, lane);
+      issue_halo(hl + (b ^ 1) * HBUF, n, oh0, ow0);
     }
     int n, oh0, ow0;
     tile_origin(t, n, oh0, ow0);
@@ -447,10 +453,40 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_hs_kernel(ConvFwdArgs a, int 
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
   const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (unsigned)((size_t)a.Cout * 9 * a.C * 2));
 
+  // Per-lane DMA offsets of channel chunk 0, computed once: chunk kc only
+  // adds kc * 64 B, passed as the instruction's scalar offset (the address
+  // arithmetic would otherwise sit between the barrier and the MFMAs of every
+  // stage, on both waves of a SIMD at once).
+  constexpr int H_NINS = HPR / 16, H_PER = (H_NINS + NW - 1) / NW;
+  constexpr int W_NINS = 9 * COT / 16, W_PER = (W_NINS + NW - 1) / NW;
+  unsigned hoff[H_PER], woff[W_PER];
+#pragma unroll
+  for (int k = 0; k < H_PER; ++k) {
+    const int rowg = (wave + k * NW) * 16 + (lane >> 2);
+    const int hp = rowg;  // one panel per stage
+    const int lchunk = (lane & 3) ^ ((hp >> 1) & 2);
+    const int hr = hp / kHW, hc = hp - hr * kHW;
+    const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
+    hoff[k] = kOOB;
+    if (hp < (TH + 2) * kHW && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+      hoff[k] = (unsigned)((((n * a.H + ih) * a.W + iw) * a.ldx + lchunk * 8) * 2);
+  }
+#pragma unroll
+  for (int k = 0; k < W_PER; ++k) {
+    const int rowg = (wave + k * NW) * 16 + (lane >> 2);
+    const int co = rowg % COT, tap = rowg / COT;
+    const int lchunk = (lane & 3) ^ ((co >> 1) & 2);
+    woff[k] = (unsigned)(((co0 + co) * 9 * a.C + tap * a.C + lchunk * 8) * 2);
+  }
   auto issue = [&](int kc, int b) {
     char* S = smem + b * STAGE;
-    issue_halo_dma<TH, NW>(a, xr, S, n, oh0, ow0, kc * 32, 1, wave, lane);
-    issue_weight_dma<COT, NW>(a, wr, S + HBYTES, co0, kc * 32, 1, wave, lane);
+    const unsigned so = (unsigned)kc * 64u;
+#pragma unroll
+    for (int k = 0; k < H_PER; ++k)
+      if (wave + k * NW < H_NINS) glds16s(xr, S + (wave + k * NW) * 1024, hoff[k], so);
+#pragma unroll
+    for (int k = 0; k < W_PER; ++k)
+      if (wave + k * NW < W_NINS) glds16s(wr, S + HBYTES + (wave + k * NW) * 1024, woff[k], so);
   };
   issue(0, 0);
   load_epi_constants<COT>(a, cst, co0, tid, NW * 64);

@@ -900,6 +900,33 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
   const int arow = lane >> 3, aslot = lane & 7;                // dY: 8 rows of 128 B per instruction
   const int hrow = lane / HCPR, hslot = lane % HCPR;           // halo: HRPI rows per instruction
 
+  // Per-lane constant parts of the loads, computed once: the dY tile is
+  // contiguous rows of one image, so its offset is a per-lane part plus the
+  // tile's (wave-uniform, non-negative) origin passed as the scalar offset;
+  // the halo keeps a per-stage bounds test on precomputed (row, col).
+  unsigned arel[A_INS];
+#pragma unroll
+  for (int j = 0; j < A_INS; ++j) {
+    const int row = (wave * A_INS + j) * 8 + arow;  // pixel in tile
+    const int f = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+    const int lchunk = ((((aslot >> 1) ^ f)) << 1) | (aslot & 1);
+    arel[j] = (unsigned)((((row / TW) * a.Q + row % TW) * a.lddy) + co0 + lchunk * 8) * 2u;
+  }
+  int hrr[H_INS], hcc[H_INS], hch[H_INS];
+#pragma unroll
+  for (int j = 0; j < H_INS; ++j) {
+    const int row = (wave * H_INS + j) * HRPI + hrow;  // halo row
+    int lchunk;
+    if constexpr (CI == 32) {
+      lchunk = ((((hslot >> 1) ^ ((row >> 3) & 1))) << 1) | (hslot & 1);
+    } else {
+      const int f = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+      lchunk = ((((hslot >> 1) ^ f)) << 1) | (hslot & 1);
+    }
+    hrr[j] = row < HROWS ? row / HW2 - 1 : -(1 << 20);  // rows past the halo fail the bounds test
+    hcc[j] = row % HW2 - 1;
+    hch[j] = c0 + lchunk * 8;
+  }
   auto issue = [&](int kt, int buf) {
     const int t = t0 + kt;
     const int n = t / (tp * tq);
@@ -907,29 +934,15 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
     const int oh0 = (rem / tq) * TH, ow0 = (rem % tq) * TW;
     char* As = smem + buf * STAGE;
     char* Bs = As + A_BYTES;
+    const unsigned abase = (unsigned)(((n * a.P + oh0) * a.Q + ow0) * a.lddy) * 2u;
 #pragma unroll
-    for (int j = 0; j < A_INS; ++j) {
-      const int row = (wave * A_INS + j) * 8 + arow;  // pixel in tile
-      const int f = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
-      const int lchunk = ((((aslot >> 1) ^ f)) << 1) | (aslot & 1);
-      const int oh = oh0 + row / TW, ow = ow0 + row % TW;
-      const unsigned off = (unsigned)((((n * a.P + oh) * a.Q + ow) * a.lddy) + co0 + lchunk * 8) * 2u;
-      glds16(dyr, As + (wave * A_INS + j) * 1024, off);
-    }
+    for (int j = 0; j < A_INS; ++j) glds16s(dyr, As + (wave * A_INS + j) * 1024, arel[j], abase);
 #pragma unroll
     for (int j = 0; j < H_INS; ++j) {
-      const int row = (wave * H_INS + j) * HRPI + hrow;  // halo row
-      int lchunk;
-      if constexpr (CI == 32) {
-        lchunk = ((((hslot >> 1) ^ ((row >> 3) & 1))) << 1) | (hslot & 1);
-      } else {
-        const int f = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
-        lchunk = ((((hslot >> 1) ^ f)) << 1) | (hslot & 1);
-      }
-      const int ih = oh0 - 1 + row / HW2, iw = ow0 - 1 + row % HW2;
+      const int ih = oh0 + hrr[j], iw = ow0 + hcc[j];
       unsigned off = kOOB;
-      if (row < HROWS && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
-        off = (unsigned)((((n * a.H + ih) * a.W + iw) * a.ldx) + c0 + lchunk * 8) * 2u;
+      if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+        off = (unsigned)((((n * a.H + ih) * a.W + iw) * a.ldx) + hch[j]) * 2u;
       glds16(xr, Bs + (wave * H_INS + j) * 1024, off);
     }
   };
