@@ -56,6 +56,24 @@ __device__ __forceinline__ int ws_off(int row, int chunk) {  // byte offset of (
 
 constexpr int kHW = 18;  // halo width: 16 output columns + 2
 
+// sum over the 16 lanes of a lane row, complete in lane 15 of the row
+// (DPP row_shr adds; bound_ctrl reads 0 past the row start)
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x111, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x112, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x114, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x118, 0xf, 0xf, true));
+  return v;
+}
+
+// workgroup barrier ordering LDS only: outstanding global stores stay in
+// flight (__syncthreads' fence would wait for them)
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // Halo of one output tile (TH x 16 at (n, oh0, ow0)): np 32-channel panels of
 // input channels c0 .. c0 + 32*np into LDS, HPR rows per panel.  DMA
 // instructions are dealt round-robin over the NW waves.
@@ -169,19 +187,28 @@ struct TileEpi {
     }
   }
 
+  // bias, addend, ReLU mask, BN sums as before; the bf16 quads of a row pair
+  // (channel fragments i, i+1) are exchanged between lane rows 0<->1 and
+  // 2<->3 (v_permlane16_swap) so every lane stores 16 contiguous bytes and a
+  // wave instruction writes 64 B per pixel instead of 8-B pieces.  vec16:
+  // ld / channel split multiples of 8 (else the 8-B stores).
   __device__ __forceinline__ void store(const ConvFwdArgs& a, const f32x4 (&acc)[RW][FN], const size_t (&pix)[RW],
                                         int co0, int lane, const float* cst, float (&q0)[FN][4],
                                         float (&q1)[FN][4], float (&q2)[FN][4]) {
     constexpr int COT = FN * 16;
+    static_assert(FN % 2 == 0, "fragment pairs");
     const bool fbwd = a.bb.sums != nullptr;
     const bool stats = a.stats != nullptr || fbwd;
+    const bool vec16 = (a.ldy % 8 == 0) && (!a.ysplit || (a.ldysplit % 8 == 0 && a.csplit % 8 == 0));
+    const int g = lane >> 4;
 #pragma unroll
     for (int j = 0; j < RW; ++j) {
+      uint2 oq[FN];
 #pragma unroll
       for (int i = 0; i < FN; ++i) {
-        const int cl = i * 16 + ((lane >> 4) << 2);
+        const int cl = i * 16 + (g << 2);
         const int co = co0 + cl;
-        if (co >= a.Cout) continue;
+        const bool live = co < a.Cout;
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = acc[j][i][e] + cst[cl + e];
@@ -199,8 +226,12 @@ struct TileEpi {
         uint2 o;
         o.x = pack_bf2(v[0], v[1]);
         o.y = pack_bf2(v[2], v[3]);
-        if (a.ysplit && co >= a.csplit) *reinterpret_cast<uint2*>(a.ysplit + pix[j] * a.ldysplit + co - a.csplit) = o;
-        else *reinterpret_cast<uint2*>(a.y + pix[j] * a.ldy + co) = o;
+        oq[i] = o;
+        if (!live) continue;
+        if (!vec16) {
+          if (a.ysplit && co >= a.csplit) *reinterpret_cast<uint2*>(a.ysplit + pix[j] * a.ldysplit + co - a.csplit) = o;
+          else *reinterpret_cast<uint2*>(a.y + pix[j] * a.ldy + co) = o;
+        }
         if (FLIP && fbwd) {  // sums of the stored bf16 dZ, as bn_bwd_reduce_kernel would read them
           const float dz[4] = {__uint_as_float(o.x << 16), __uint_as_float(o.x & 0xffff0000u),
                                __uint_as_float(o.y << 16), __uint_as_float(o.y & 0xffff0000u)};
@@ -222,6 +253,21 @@ struct TileEpi {
         } else if (stats) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) { q0[i][e] += v[e]; q1[i][e] += v[e] * v[e]; }
+        }
+      }
+      if (vec16) {
+#pragma unroll
+        for (int ip = 0; ip < FN / 2; ++ip) {
+          // rows (0,1,2,3) end up holding channels (0-7, 16-23, 8-15, 24-31) of the pair
+          const auto sx = __builtin_amdgcn_permlane16_swap(oq[2 * ip].x, oq[2 * ip + 1].x, false, false);
+          const auto sy = __builtin_amdgcn_permlane16_swap(oq[2 * ip].y, oq[2 * ip + 1].y, false, false);
+          const uint4 chunk = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+          const int co = co0 + ip * 32 + ((g & 1) << 4) + ((g >> 1) << 3);
+          if (co < a.Cout) {
+            if (a.ysplit && co >= a.csplit)
+              *reinterpret_cast<uint4*>(a.ysplit + pix[j] * a.ldysplit + co - a.csplit) = chunk;
+            else *reinterpret_cast<uint4*>(a.y + pix[j] * a.ldy + co) = chunk;
+          }
         }
       }
     }
@@ -258,16 +304,14 @@ __device__ __forceinline__ void commit_stats(const ConvFwdArgs& a, float (&q0)[F
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        q0[i][e] += __shfl_xor(q0[i][e], o, 64);
-        q1[i][e] += __shfl_xor(q1[i][e], o, 64);
-        if (TWO) q2[i][e] += __shfl_xor(q2[i][e], o, 64);
-      }
+    for (int e = 0; e < 4; ++e) {
+      q0[i][e] = row16_sum(q0[i][e]);
+      q1[i][e] = row16_sum(q1[i][e]);
+      if (TWO) q2[i][e] = row16_sum(q2[i][e]);
+    }
   float* red = reinterpret_cast<float*>(scratch);  // [NW][COT][3]
-  __syncthreads();
-  if ((lane & 15) == 0) {
+  lds_barrier();  // every wave is done reading the staging LDS (no wait for the tile stores)
+  if ((lane & 15) == 15) {
 #pragma unroll
     for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -278,7 +322,7 @@ __device__ __forceinline__ void commit_stats(const ConvFwdArgs& a, float (&q0)[F
         red[(wave * COT + cl) * 3 + 2] = TWO ? q2[i][e] : 0.f;
       }
   }
-  __syncthreads();
+  lds_barrier();
   for (int cl = tid; cl < COT; cl += NW * 64) {
     const int co = co0 + cl;
     if (co < a.Cout) {

@@ -42,8 +42,15 @@ SHAPES = [
 
 
 def run(mode, C, Co, H, R, st, pad):
-    """mode 0: forward conv; mode 1: dgrad (transposed gather) of that conv."""
+    """mode 0: forward conv; mode 1: dgrad (transposed gather) of that conv;
+    mode 2: weight gradient (fp32 atomics into dW, no split-K slab)."""
     P = (H + 2 * pad - R) // st + 1
+    if mode == 2:
+        dy = torch.randn(N, P, P, Co, device="cuda").to(torch.bfloat16)
+        x = torch.randn(N, H, H, C, device="cuda").to(torch.bfloat16)
+        dw = torch.zeros(Co * R * R * C, device="cuda")
+        args_ = (dy.data_ptr(), Co, x.data_ptr(), C, dw.data_ptr(), N, H, H, C, P, P, Co, R, R, st, pad, 0)
+        return args_, 2.0 * N * P * P * Co * C * R * R, (dy, dw, x)
     if mode == 0:
         x = torch.randn(N, H, H, C, device="cuda").to(torch.bfloat16)
         y = torch.empty(N, P, P, Co, device="cuda", dtype=torch.bfloat16)
@@ -72,30 +79,31 @@ for name, C, Co, H, R, st, pad in SHAPES:
         continue
     for mode in [int(m) for m in args.modes.split(",")]:
         a, flops, keep = run(mode, C, Co, H, R, st, pad)
+        fn = L.unet_conv_wgrad if mode == 2 else L.unet_conv_fwd
         times = {c: [] for c in CFGS}
         y = keep[1]
         L.unet_set_conv_config(0)
-        L.unet_conv_fwd(*a, S())
+        fn(*a, S())
         y_ref = y.clone()
         bad = []
         for c in CFGS:
             y.zero_()
             L.unet_set_conv_config(c)
-            if L.unet_conv_fwd(*a, S()) == 0 and not torch.equal(y, y_ref):
+            if fn(*a, S()) == 0 and not torch.equal(y, y_ref):
                 bad.append((c, (y.float() - y_ref.float()).abs().max().item()))
         if bad:
             print(f"{name} mode {mode}: configs differ from auto: {bad}", flush=True)
         for rep in range(args.reps):
             for c in CFGS:
                 L.unet_set_conv_config(c)
-                if L.unet_conv_fwd(*a, S()) != 0:
+                if fn(*a, S()) != 0:
                     times[c] = None
                     continue
                 if times[c] is None:
                     continue
                 e0.record()
                 for _ in range(5):
-                    L.unet_conv_fwd(*a, S())
+                    fn(*a, S())
                 e1.record()
                 torch.cuda.synchronize()
                 times[c].append(e0.elapsed_time(e1) / 5 * 1e3)
@@ -103,5 +111,5 @@ for name, C, Co, H, R, st, pad in SHAPES:
         res = {c: sorted(t)[len(t) // 2] for c, t in times.items() if t}
         best = min(res, key=res.get)
         line = " ".join(f"{c}:{res[c]:.0f}" for c in sorted(res))
-        print(f"{name:10s} {'fwd' if mode == 0 else 'dgrad':5s} best cfg {best:2d} {res[best]:7.1f}us "
+        print(f"{name:10s} {['fwd', 'dgrad', 'wgrad'][mode]:5s} best cfg {best:2d} {res[best]:7.1f}us "
               f"{flops / res[best] / 1e6:6.0f} TF | auto {res.get(0, 0):.0f}us | {line}", flush=True)
