@@ -37,8 +37,18 @@ def pmc_traffic(kernel: str):
     path = found[-1]  # newest profiling session of the newest round
     with open(path) as f:
         table = json.load(f)
-    ent = table.get(kernel)
-    return None if ent is None else ent["bytes_per_launch"]
+    # rocprof names spell out defaulted template arguments ("..., false>")
+    # that the executor's kernel tag leaves off
+    def canon(name: str) -> str:
+        name = name.replace(" ", "")
+        while name.endswith(",false>"):
+            name = name[: -len(",false>")] + ">"
+        return name
+    want = canon(kernel)
+    for key, ent in table.items():
+        if canon(key) == want:
+            return ent["bytes_per_launch"]
+    return None
 
 
 def cpu_baseline(batch: int, h: int, steps: int, threads: int):
