@@ -16,8 +16,10 @@ namespace unet {
 constexpr float kMaskThreshold = 8.94069742685133e-08f;  // 0x33C00001, SURVEY.md §0
 
 // grid cap of the BN apply kernels (each block recomputes the per-channel
-// coefficients in its prologue; fewer, longer blocks amortise that)
-static int g_apply_cap = std::getenv("UNET_APPLY_CAP") ? std::atoi(std::getenv("UNET_APPLY_CAP")) : 4096;
+// coefficients in its prologue; fewer, longer blocks amortise that and keep
+// the next pass's loads in flight: 512 = 2 blocks per CU, measured best of
+// 256..4096 for both directions on the Base config)
+static int g_apply_cap = std::getenv("UNET_APPLY_CAP") ? std::atoi(std::getenv("UNET_APPLY_CAP")) : 512;
 
 static inline int grid_for(int64_t work, int per_block, int cap = 2048) {
   int64_t g = (work + per_block - 1) / per_block;
@@ -57,6 +59,7 @@ constexpr int kBnCG = 64;
 constexpr int kBnPPT = 4;
 __host__ __device__ __forceinline__ int bn_group(int C) { return C % kBnCG == 0 ? kBnCG : C; }
 
+template <int RES, bool RELU>
 __global__ void __launch_bounds__(256) bn_apply_kernel(BnApplyArgs a) {
   const int CG = bn_group(a.C);
   const int CC = CG >> 3;
@@ -72,8 +75,8 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(BnApplyArgs a) {
     for (int u = 0; u < PPT; ++u) {
       const int64_t pix = base + u * stride;
       uy[u] = pix < a.npix ? *reinterpret_cast<const uint4*>(a.y + pix * a.ldy + c8) : make_uint4(0, 0, 0, 0);
-      ur[u] = (a.res_mode && pix < a.npix) ? *reinterpret_cast<const uint4*>(a.res + pix * a.ldr + c8)
-                                           : make_uint4(0, 0, 0, 0);
+      if constexpr (RES != 0)
+        ur[u] = pix < a.npix ? *reinterpret_cast<const uint4*>(a.res + pix * a.ldr + c8) : make_uint4(0, 0, 0, 0);
     }
   };
   int64_t base = (int64_t)blockIdx.x * rows + row;
@@ -90,7 +93,7 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(BnApplyArgs a) {
     } else {
       bn_scale_shift(a.bn, ch, coef[c], coef[CG + c], m, inv, var);
     }
-    if (a.res_mode == 2) {
+    if (RES == 2) {
       if (a.bn2.training && a.bn2.ss) {
         coef[2 * CG + c] = a.bn2.ss[ch];
         coef[3 * CG + c] = a.bn2.ss[a.C + ch];
@@ -100,21 +103,26 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(BnApplyArgs a) {
     }
   }
   __syncthreads();
-  float sc1[8], sh1[8], sc2[8], sh2[8];
+  float sc1[8], sh1[8], sc2[RES == 2 ? 8 : 1], sh2[RES == 2 ? 8 : 1];
   const int l8 = chunk << 3;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     sc1[k] = coef[l8 + k];
     sh1[k] = coef[CG + l8 + k];
-    sc2[k] = a.res_mode == 2 ? coef[2 * CG + l8 + k] : 0.f;
-    sh2[k] = a.res_mode == 2 ? coef[3 * CG + l8 + k] : 0.f;
+    if constexpr (RES == 2) {
+      sc2[k] = coef[2 * CG + l8 + k];
+      sh2[k] = coef[3 * CG + l8 + k];
+    }
   }
   if (row < rows) {
     for (; base < a.npix; base += PPT * stride) {
       // this pass's operands; the next pass's loads go out before the math
       uint4 cy[PPT], cr[PPT];
 #pragma unroll
-      for (int u = 0; u < PPT; ++u) { cy[u] = uy[u]; cr[u] = ur[u]; }
+      for (int u = 0; u < PPT; ++u) {
+        cy[u] = uy[u];
+        if constexpr (RES != 0) cr[u] = ur[u];
+      }
       if (base + PPT * stride < a.npix) load(base + PPT * stride);
 #pragma unroll
       for (int u = 0; u < PPT; ++u) {
@@ -124,17 +132,17 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(BnApplyArgs a) {
         unpack8(cy[u], v);
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = v[k] * sc1[k] + sh1[k];
-        if (a.res_mode) {
+        if constexpr (RES != 0) {
           float r[8];
           unpack8(cr[u], r);
-          if (a.res_mode == 2) {
+          if constexpr (RES == 2) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) r[k] = r[k] * sc2[k] + sh2[k];
           }
 #pragma unroll
           for (int k = 0; k < 8; ++k) v[k] += r[k];
         }
-        if (a.relu) {
+        if constexpr (RELU) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
         }
@@ -146,7 +154,7 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(BnApplyArgs a) {
   // its channel group
   if (blockIdx.x == 0) {
     if (!a.bn.ss) bn_finalize_block0(a.bn, threadIdx.x, blockDim.x, cg0, cg0 + CG);
-    if (a.res_mode == 2 && !a.bn2.ss) bn_finalize_block0(a.bn2, threadIdx.x, blockDim.x, cg0, cg0 + CG);
+    if (RES == 2 && !a.bn2.ss) bn_finalize_block0(a.bn2, threadIdx.x, blockDim.x, cg0, cg0 + CG);
   }
 }
 
@@ -170,8 +178,17 @@ static inline bool bn_group_ok(int C) {
 
 hipError_t launch_bn_apply(const BnApplyArgs& a, hipStream_t st) {
   if (!bn_group_ok(a.C)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(bn_apply_kernel, bn_grid(a.npix, a.C), chunk_block(bn_group(a.C)),
-                     4 * bn_group(a.C) * sizeof(float), st, a);
+  const dim3 g = bn_grid(a.npix, a.C), b = chunk_block(bn_group(a.C));
+  const size_t lds = 4 * bn_group(a.C) * sizeof(float);
+  switch (a.res_mode * 2 + (a.relu ? 1 : 0)) {
+    case 0: hipLaunchKernelGGL((bn_apply_kernel<0, false>), g, b, lds, st, a); break;
+    case 1: hipLaunchKernelGGL((bn_apply_kernel<0, true>), g, b, lds, st, a); break;
+    case 2: hipLaunchKernelGGL((bn_apply_kernel<1, false>), g, b, lds, st, a); break;
+    case 3: hipLaunchKernelGGL((bn_apply_kernel<1, true>), g, b, lds, st, a); break;
+    case 4: hipLaunchKernelGGL((bn_apply_kernel<2, false>), g, b, lds, st, a); break;
+    case 5: hipLaunchKernelGGL((bn_apply_kernel<2, true>), g, b, lds, st, a); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
@@ -272,6 +289,13 @@ hipError_t launch_bn_bwd_reduce(const BnBwdArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// dY = k1 (dZ - mean dZ - xhat mean(dZ xhat)), xhat = (y - mu) invstd, folded
+// per channel into dY = A dZ + B y + Cc (A = k1, B = -k1 invstd m2,
+// Cc = k1 (invstd m2 mu - m1)): 3 coefficients (6 with TWO) per channel in
+// registers.  RELU: dZ = dA * (act > 0) (unfused path; the fused producers
+// store dZ itself).  Blocks grid-stride over passes of kBnPPT pixels per
+// thread with the next pass's loads issued before the current pass's math.
+template <bool TWO, bool RELU>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, double inv_n) {
   const int CG = bn_group(a.C);
   const int CC = CG >> 3;
@@ -279,7 +303,6 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, double i
   const int chunk = threadIdx.x % CC, row = threadIdx.x / CC;
   const int cg0 = blockIdx.y * CG;
   const int c8 = cg0 + (chunk << 3);
-  const bool two = a.y2 != nullptr;
   constexpr int PPT = kBnPPT;
   const int64_t stride = (int64_t)gridDim.x * rows;
   uint4 uda[PPT], uact[PPT], uy[PPT], uy2[PPT];
@@ -290,109 +313,116 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, double i
       const bool in = pix < a.npix;
       const uint4 z = make_uint4(0, 0, 0, 0);
       uda[u] = in ? *reinterpret_cast<const uint4*>(a.da + pix * a.ldda + c8) : z;
-      uact[u] = (in && a.relu) ? *reinterpret_cast<const uint4*>(a.act + pix * a.ldact + c8) : z;
+      if constexpr (RELU) uact[u] = in ? *reinterpret_cast<const uint4*>(a.act + pix * a.ldact + c8) : z;
       uy[u] = in ? *reinterpret_cast<const uint4*>(a.y + pix * a.ldy + c8) : z;
-      uy2[u] = (in && two) ? *reinterpret_cast<const uint4*>(a.y2 + pix * a.ldy2 + c8) : z;
+      if constexpr (TWO) uy2[u] = in ? *reinterpret_cast<const uint4*>(a.y2 + pix * a.ldy2 + c8) : z;
     }
   };
   int64_t base = (int64_t)blockIdx.x * rows + row;
   if (row < rows) load(base);  // first pass in flight during the prologue
-  // per channel of the group: k1 = gamma*invstd, m1 = mean(dZ), m2 =
-  // mean(dZ*xhat) (x2 for bn2) into LDS, then 8 per thread into registers
-  extern __shared__ __attribute__((aligned(16))) float coef[];  // [9][CG]
+  extern __shared__ __attribute__((aligned(16))) float coef[];  // [6][CG]
   for (int c = threadIdx.x; c < CG; c += blockDim.x) {
     const int ch = cg0 + c;
-    if (a.coef) {  // finalised by the reduce kernel's last block
-      coef[c] = a.coef[ch];
-      coef[CG + c] = a.coef[a.C + ch];
-      coef[2 * CG + c] = a.coef[2 * a.C + ch];
-      coef[3 * CG + c] = a.mean[ch];
-      coef[4 * CG + c] = a.invstd[ch];
-      if (two) {
-        coef[5 * CG + c] = a.coef[3 * a.C + ch];
-        coef[6 * CG + c] = a.coef[4 * a.C + ch];
-        coef[7 * CG + c] = a.mean2[ch];
-        coef[8 * CG + c] = a.invstd2[ch];
+    float k1, m1, m2, k1b = 0.f, m2b = 0.f;
+    if (a.coef) {  // finalised by the reduce's (or fused producer's) last block
+      k1 = a.coef[ch];
+      m1 = a.coef[a.C + ch];
+      m2 = a.coef[2 * a.C + ch];
+      if (TWO) { k1b = a.coef[3 * a.C + ch]; m2b = a.coef[4 * a.C + ch]; }
+    } else {
+      double s1 = 0.0, s2 = 0.0, t2 = 0.0;
+      for (int r = 0; r < kStatRep; ++r) {
+        const size_t rep = (size_t)r * 2 * a.C;
+        s1 += a.sums[rep + ch];
+        s2 += a.sums[rep + a.C + ch];
+        if (TWO) t2 += a.sums2[rep + a.C + ch];
       }
-      continue;
-    }
-    double s1 = 0.0, s2 = 0.0, t2 = 0.0;
-    for (int r = 0; r < kStatRep; ++r) {
-      const size_t rep = (size_t)r * 2 * a.C;
-      s1 += a.sums[rep + ch];
-      s2 += a.sums[rep + a.C + ch];
-      if (two) t2 += a.sums2[rep + a.C + ch];
-    }
-    coef[c] = a.gamma[ch] * a.invstd[ch];
-    coef[CG + c] = (float)(s1 * inv_n);
-    coef[2 * CG + c] = (float)(s2 * inv_n);
-    coef[3 * CG + c] = a.mean[ch];
-    coef[4 * CG + c] = a.invstd[ch];
-    if (two) {
-      coef[5 * CG + c] = a.gamma2[ch] * a.invstd2[ch];
-      coef[6 * CG + c] = (float)(t2 * inv_n);
-      coef[7 * CG + c] = a.mean2[ch];
-      coef[8 * CG + c] = a.invstd2[ch];
-    }
-    if (blockIdx.x == 0) {
-      a.dgamma[ch] = (float)s2;
-      a.dbeta[ch] = (float)s1;
-      if (two) {
-        a.dgamma2[ch] = (float)t2;
-        a.dbeta2[ch] = (float)s1;  // same dZ feeds both BNs
+      k1 = a.gamma[ch] * a.invstd[ch];
+      m1 = (float)(s1 * inv_n);
+      m2 = (float)(s2 * inv_n);
+      if (TWO) { k1b = a.gamma2[ch] * a.invstd2[ch]; m2b = (float)(t2 * inv_n); }
+      if (blockIdx.x == 0) {
+        a.dgamma[ch] = (float)s2;
+        a.dbeta[ch] = (float)s1;
+        if (TWO) {
+          a.dgamma2[ch] = (float)t2;
+          a.dbeta2[ch] = (float)s1;  // same dZ feeds both BNs
+        }
       }
+    }
+    const float is = a.invstd[ch], mu = a.mean[ch];
+    coef[c] = k1;
+    coef[CG + c] = -k1 * is * m2;
+    coef[2 * CG + c] = k1 * (is * m2 * mu - m1);
+    if (TWO) {
+      const float isb = a.invstd2[ch], mub = a.mean2[ch];
+      coef[3 * CG + c] = k1b;
+      coef[4 * CG + c] = -k1b * isb * m2b;
+      coef[5 * CG + c] = k1b * (isb * m2b * mub - m1);
     }
   }
   __syncthreads();
-  float k1[8], m1[8], m2[8], mu[8], is[8], k1b[8], m2b[8], mub[8], isb[8];
+  float cA[8], cB[8], cC[8], dA[TWO ? 8 : 1], dB[TWO ? 8 : 1], dC[TWO ? 8 : 1];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const int c = (chunk << 3) + k;
-    k1[k] = coef[c];
-    m1[k] = coef[CG + c];
-    m2[k] = coef[2 * CG + c];
-    mu[k] = coef[3 * CG + c];
-    is[k] = coef[4 * CG + c];
-    k1b[k] = two ? coef[5 * CG + c] : 0.f;
-    m2b[k] = two ? coef[6 * CG + c] : 0.f;
-    mub[k] = two ? coef[7 * CG + c] : 0.f;
-    isb[k] = two ? coef[8 * CG + c] : 0.f;
+    cA[k] = coef[c];
+    cB[k] = coef[CG + c];
+    cC[k] = coef[2 * CG + c];
+    if constexpr (TWO) {
+      dA[k] = coef[3 * CG + c];
+      dB[k] = coef[4 * CG + c];
+      dC[k] = coef[5 * CG + c];
+    }
   }
-  if (row < rows) {
-    for (bool first = true; base < a.npix; base += PPT * stride, first = false) {
-      if (!first) load(base);
+  if (row >= rows) return;
+  for (; base < a.npix; base += PPT * stride) {
+    uint4 cda[PPT], cact[PPT], cy[PPT], cy2[PPT];
 #pragma unroll
-      for (int u = 0; u < PPT; ++u) {
-        const int64_t pix = base + u * stride;
-        if (pix >= a.npix) break;
-        float dz[8], y[8], o[8];
-        unpack8(uda[u], dz);
-        if (a.relu) {
-          float av[8];
-          unpack8(uact[u], av);
+    for (int u = 0; u < PPT; ++u) {
+      cda[u] = uda[u]; cy[u] = uy[u];
+      if constexpr (RELU) cact[u] = uact[u];
+      if constexpr (TWO) cy2[u] = uy2[u];
+    }
+    if (base + PPT * stride < a.npix) load(base + PPT * stride);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) dz[k] = av[k] > 0.f ? dz[k] : 0.f;
-        }
-        unpack8(uy[u], y);
+    for (int u = 0; u < PPT; ++u) {
+      const int64_t pix = base + u * stride;
+      if (pix >= a.npix) break;
+      float dz[8], y[8], o[8];
+      unpack8(cda[u], dz);
+      if constexpr (RELU) {
+        float av[8];
+        unpack8(cact[u], av);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] = k1[k] * (dz[k] - m1[k] - (y[k] - mu[k]) * is[k] * m2[k]);
-        *reinterpret_cast<uint4*>(a.dy + pix * a.lddy + c8) = pack8(o);
-        if (two) {
-          unpack8(uy2[u], y);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) o[k] = k1b[k] * (dz[k] - m1[k] - (y[k] - mub[k]) * isb[k] * m2b[k]);
-          *reinterpret_cast<uint4*>(a.dy2 + pix * a.lddy2 + c8) = pack8(o);
-        }
-        if (a.dres) *reinterpret_cast<uint4*>(a.dres + pix * a.lddres + c8) = pack8(dz);
+        for (int k = 0; k < 8; ++k) dz[k] = av[k] > 0.f ? dz[k] : 0.f;
       }
+      unpack8(cy[u], y);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = fmaf(cA[k], dz[k], fmaf(cB[k], y[k], cC[k]));
+      *reinterpret_cast<uint4*>(a.dy + pix * a.lddy + c8) = pack8(o);
+      if constexpr (TWO) {
+        unpack8(cy2[u], y);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = fmaf(dA[k], dz[k], fmaf(dB[k], y[k], dC[k]));
+        *reinterpret_cast<uint4*>(a.dy2 + pix * a.lddy2 + c8) = pack8(o);
+      }
+      if (RELU && a.dres) *reinterpret_cast<uint4*>(a.dres + pix * a.lddres + c8) = pack8(dz);
     }
   }
 }
 
 hipError_t launch_bn_bwd_apply(const BnBwdArgs& a, hipStream_t st) {
   if (!bn_group_ok(a.C)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, bn_grid(a.npix, a.C), chunk_block(bn_group(a.C)),
-                     9 * bn_group(a.C) * sizeof(float), st, a, 1.0 / (double)a.npix);
+  if (!a.relu && a.dres) return hipErrorInvalidValue;  // dZ is dA itself: nothing to store
+  const dim3 g = bn_grid(a.npix, a.C), b = chunk_block(bn_group(a.C));
+  const size_t lds = 6 * bn_group(a.C) * sizeof(float);
+  const double inv_n = 1.0 / (double)a.npix;
+  const bool two = a.y2 != nullptr;
+  if (two && a.relu) hipLaunchKernelGGL((bn_bwd_apply_kernel<true, true>), g, b, lds, st, a, inv_n);
+  else if (two) hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false>), g, b, lds, st, a, inv_n);
+  else if (a.relu) hipLaunchKernelGGL((bn_bwd_apply_kernel<false, true>), g, b, lds, st, a, inv_n);
+  else hipLaunchKernelGGL((bn_bwd_apply_kernel<false, false>), g, b, lds, st, a, inv_n);
   return hipGetLastError();
 }
 
