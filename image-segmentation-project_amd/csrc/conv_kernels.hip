@@ -1462,7 +1462,9 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a0, int mode, hipStream_t st) {
   if (a0.ysplit && (!g_use_glds || mode == MODE_STEM || mode == MODE_SHUF || a0.csplit % 4 || a0.ldysplit % 4 ||
                     a0.bb.sums || a0.add))
     return hipErrorInvalidValue;
-  if (g_use_glds && mode == MODE_STEM) return launch_stem_fwd(a0, st);
+  // dedicated stem kernel: 64 output channels (Base); the Wide stem (128) takes
+  // the generic implicit-GEMM path below
+  if (g_use_glds && mode == MODE_STEM && a0.Cout == 64) return launch_stem_fwd(a0, st);
   if (mode == MODE_SHUF) {  // convT k2s2 forward: a0 holds the transposed-conv geometry
     if (!g_use_glds || a0.R != 2 || a0.S != 2 || a0.stride != 2 || a0.pad != 0 || a0.Cout % 4 || a0.C % 32 ||
         a0.P != 2 * a0.H || a0.Q != 2 * a0.W || a0.stats || a0.add || a0.bb.sums)
@@ -1611,7 +1613,8 @@ hipError_t launch_convt_wgrad(const ConvWgradArgs& a0, hipStream_t st) {
 }
 
 hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st) {
-  if (stem) return g_use_glds ? launch_stem_wgrad(a, st) : launch_wgrad_cfg<XLOAD_STEM, 64, 64, 64, 2, 2>(a, st);
+  if (stem)
+    return g_use_glds && a.Cout == 64 ? launch_stem_wgrad(a, st) : launch_wgrad_cfg<XLOAD_STEM, 64, 64, 64, 2, 2>(a, st);
   if (g_use_glds && a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.C % 32 == 0 && a.P == a.H &&
       a.Q == a.W && (size_t)a.N * a.H * a.W * a.ldx * 2 < 0x80000000ull &&
       (size_t)a.N * a.P * a.Q * a.lddy * 2 < 0x80000000ull) {

@@ -988,27 +988,30 @@ __global__ void __launch_bounds__(256) pack_kernel(PackTable t) {
   const bool full = e.kind == PK_CONV_DGRAD || e.kind == PK_CONVT_FWD;
   // every load of a pass is issued before the first LDS store (no per-load
   // round trip to L2)
-  if (!full) {  // one a-row [B][T] -> [T][B] per block iteration
+  if (!full) {  // one a-row [B][T] -> [T][B] per block iteration, in b-chunks of <= 512
     constexpr int kMaxPer = 512 * kPkTmax / 256;
     const int n = B * T;
     for (int a = blockIdx.x; a < A; a += gridDim.x) {
-      const float* src = e.src + (size_t)a * n;
-      float v[kMaxPer];
+      for (int b0 = 0; b0 < B; b0 += 512) {  // rows wider than 512 b (Wide config, Ci = 1536)
+        const int nb = min(512, B - b0), m = nb * T;
+        const float* src = e.src + (size_t)a * n + (size_t)b0 * T;
+        float v[kMaxPer];
 #pragma unroll
-      for (int k = 0; k < kMaxPer; ++k) {
-        const int i = threadIdx.x + 256 * k;
-        v[k] = i < n ? src[i] : 0.f;
-      }
+        for (int k = 0; k < kMaxPer; ++k) {
+          const int i = threadIdx.x + 256 * k;
+          v[k] = i < m ? src[i] : 0.f;
+        }
 #pragma unroll
-      for (int k = 0; k < kMaxPer; ++k) {
-        const int i = threadIdx.x + 256 * k;
-        if (i < n) lds[i] = v[k];
+        for (int k = 0; k < kMaxPer; ++k) {
+          const int i = threadIdx.x + 256 * k;
+          if (i < m) lds[i] = v[k];
+        }
+        __syncthreads();
+        bf16_t* dst = e.dst + (size_t)a * n + b0;
+        for (int tt = 0; tt < T; ++tt)
+          for (int b = threadIdx.x; b < nb; b += blockDim.x) dst[tt * B + b] = f2bf(lds[b * T + tt]);
+        __syncthreads();
       }
-      __syncthreads();
-      bf16_t* dst = e.dst + (size_t)a * n;
-      for (int tt = 0; tt < T; ++tt)
-        for (int b = threadIdx.x; b < B; b += blockDim.x) dst[tt * B + b] = f2bf(lds[b * T + tt]);
-      __syncthreads();
     }
     return;
   }
@@ -1051,9 +1054,7 @@ hipError_t launch_pack(const PackTable& t, hipStream_t st) {
   if (t.n <= 0) return hipSuccess;
   for (int i = 0; i < t.n; ++i) {
     const PackEntry& e = t.e[i];
-    const bool convt = e.kind == PK_CONVT_FWD || e.kind == PK_CONVT_DGRAD;
-    const int B = convt ? e.Co : e.Ci;
-    if (e.kind != PK_STEM && (e.R * e.S > kPkTmax || B * e.R * e.S > 512 * kPkTmax)) return hipErrorInvalidValue;
+    if (e.kind != PK_STEM && e.R * e.S > kPkTmax) return hipErrorInvalidValue;
   }
   hipLaunchKernelGGL(pack_kernel, dim3(256, t.n), dim3(256), 0, st, t);
   return hipGetLastError();

@@ -44,13 +44,15 @@ def local_bn_bwd(y, dout, mod, out=None, extra=None):
     return yl.grad, g.grad, b.grad
 
 
-@pytest.fixture(scope="module")
-def run(pkg, golden, cuda):
+@pytest.fixture(scope="module", params=[1, 2], ids=["base", "wide"])
+def run(pkg, golden, cuda, request):
+    """width 1 = Base topology; width 2 = the Wide config (every channel x2)."""
+    width = request.param
     base = golden("base64.npz")
-    ref = oracle.ReferenceUNet()
+    ref = oracle.ReferenceUNet(width=width)
     sd = oracle.closed_form_state_dict(ref, seed=0)
     ref.load_state_dict(sd)
-    m = pkg.UNetWithBackbone(pretrained=False, use_attention=False)
+    m = pkg.UNetWithBackbone(pretrained=False, use_attention=False, width=width)
     m.load_state_dict(sd)
     m = m.cuda().train()
     x = torch.from_numpy(base["x"])
@@ -161,7 +163,7 @@ def test_backward_ops(run):
         rows.append((p + "d.cat", _rel(_dcat(v, p), dcat)))
         gw = torch.nn.grad.conv2d_weight(v[p + "cat"], dec[0].weight.shape, v[p + "d.y1"], padding=1)
         rows.append((f"g decoder{lvl}.0.weight", _rel(grads[f"decoder{lvl}.0.weight"], gw)))
-        sk = skips[lvl][1]
+        sk = v[skips[lvl][0]].shape[1]
         du = _dcat(v, p)[:, sk:]
         upin_name = "enc4.2.out" if lvl == 4 else f"dec{lvl + 1}.out"
         xin = v[upin_name].clone().requires_grad_(True)
@@ -225,7 +227,7 @@ def test_backward_ops(run):
     # maxpool + stem
     x1 = v["x1"].clone().requires_grad_(True)
     F.max_pool2d(x1, 3, 2, 1).backward(v["d.p0"])
-    rows.append(("d.x1", _masked(v["d.x1"], x1.grad + _dcat(v, "dec1.")[:, :64], v["x1"])))
+    rows.append(("d.x1", _masked(v["d.x1"], x1.grad + _dcat(v, "dec1.")[:, :v["x1"].shape[1]], v["x1"])))
     dy0, dg, db = local_bn_bwd(v["y0"], v["d.x1"], ref.bn1, out=v["x1"])
     rows += [("g bn1.weight", _rel(grads["bn1.weight"], dg)), ("g bn1.bias", _rel(grads["bn1.bias"], db))]
     if "d.y0" in v:  # unfused build only: the fused stem wgrad never stores the stem dY
