@@ -44,11 +44,16 @@ def local_bn_bwd(y, dout, mod, out=None, extra=None):
     return yl.grad, g.grad, b.grad
 
 
-@pytest.fixture(scope="module", params=[1, 2], ids=["base", "wide"])
+@pytest.fixture(scope="module", params=[(1, None), (2, None), (1, (1, 64, 96))], ids=["base", "wide", "n1_64x96"])
 def run(pkg, golden, cuda, request):
-    """width 1 = Base topology; width 2 = the Wide config (every channel x2)."""
-    width = request.param
+    """width 1 = Base topology; width 2 = the Wide config (every channel x2);
+    n1_64x96 = a ragged case: batch 1, non-square, a 2x3 deepest level (the
+    kernels' partial-tile and fallback paths)."""
+    width, shape = request.param
     base = golden("base64.npz")
+    if shape is not None:
+        xs, ms = pkg.synthetic_cells(*shape, seed=7)
+        base = {"x": xs, "masks": ms}
     ref = oracle.ReferenceUNet(width=width)
     sd = oracle.closed_form_state_dict(ref, seed=0)
     ref.load_state_dict(sd)
