@@ -1442,6 +1442,14 @@ static hipError_t launch_glds(const ConvFwdArgs& a, int classes, hipStream_t st)
   }
   if (bk64 && a.Cout >= 256 && nblk(256, 256) >= 256)
     return launch_glds_cfg<MODE, 256, 256, 64, 2, 2, 4>(a, classes, st);
+  // per-layer sweep (scripts/sweep_glds_cfg.sh): the 256-channel stride-2
+  // layers (enc3.0 conv1 forward, enc4.0 conv1+downsample dgrad) keep a third
+  // stage in flight (-18 %); upconv1's dgrad (k2s2, 32 -> 64 channels, K = 128)
+  // prefers 256-pixel tiles (-14 %)
+  if (bk64 && a.stride == 2 && a.Cout == 256 && nblk(128, 128) >= 240)
+    return launch_glds_cfg<MODE, 128, 128, 64, 3, 2, 4>(a, classes, st);
+  if (!bk64 && a.R == 2 && a.stride == 2 && a.Cout == 64)
+    return launch_glds_cfg<MODE, 256, 64, 32, 3, 4, 2>(a, classes, st);
   if (a.Cout > 64 && nblk(128, 128) >= 240) {
     return bk64 ? launch_glds_cfg<MODE, 128, 128, 64, 2, 2, 4>(a, classes, st)
                 : launch_glds_cfg<MODE, 128, 128, 32, 3, 2, 2>(a, classes, st);
