@@ -3,8 +3,9 @@
 Never imported by the product package.  Every function cites the reference
 file:line (under ``/root/reference``) whose behaviour it restates:
 
-* ``ReferenceUNet`` — ``advanced_models.py:64-100,157-160,197-205,264-357``
-  (``UNetWithBackbone(backbone='resnet34', use_attention=False)``) with the
+* ``ReferenceUNet`` — ``advanced_models.py:64-100,157-172,197-205,264-357``
+  (``UNetWithBackbone(backbone='resnet34', use_attention=False|True)``;
+  ``AttentionGate`` :7-40, ``ChannelAttention`` :43-61) with the
   torchvision ResNet34 encoder (``advanced_models.py:73,81-87``; torchvision's
   ``BasicBlock`` layout: conv1/bn1/conv2/bn2/downsample.{0,1}).
 * ``bce_with_logits``/``dice_loss``/``combo_loss``/``get_loss_function`` —
@@ -121,17 +122,47 @@ def decoder_block(cin: int, cout: int) -> nn.Sequential:
         nn.Conv2d(cout, cout, 3, padding=1), nn.BatchNorm2d(cout), nn.ReLU(inplace=True))
 
 
+class AttentionGate(nn.Module):
+    """advanced_models.py:7-40: psi = sigmoid(BN(conv1x1(relu(BN(W_g g) + BN(W_x x))))); x * psi."""
+
+    def __init__(self, f_g: int, f_l: int, f_int: int):
+        super().__init__()
+        self.W_g = nn.Sequential(nn.Conv2d(f_g, f_int, 1, 1, 0, bias=True), nn.BatchNorm2d(f_int))
+        self.W_x = nn.Sequential(nn.Conv2d(f_l, f_int, 1, 1, 0, bias=True), nn.BatchNorm2d(f_int))
+        self.psi = nn.Sequential(nn.Conv2d(f_int, 1, 1, 1, 0, bias=True), nn.BatchNorm2d(1), nn.Sigmoid())
+        self.relu = nn.ReLU(inplace=True)
+
+    def forward(self, g, x):
+        return x * self.psi(self.relu(self.W_g(g) + self.W_x(x)))   # :28-40
+
+
+class ChannelAttention(nn.Module):
+    """advanced_models.py:43-61 (squeeze-and-excitation with avg + max pooling, ratio 16)."""
+
+    def __init__(self, c: int, reduction_ratio: int = 16):
+        super().__init__()
+        self.avg_pool = nn.AdaptiveAvgPool2d(1)
+        self.max_pool = nn.AdaptiveMaxPool2d(1)
+        self.fc = nn.Sequential(nn.Conv2d(c, c // reduction_ratio, 1, bias=False), nn.ReLU(inplace=True),
+                                nn.Conv2d(c // reduction_ratio, c, 1, bias=False))
+        self.sigmoid = nn.Sigmoid()
+
+    def forward(self, x):
+        return x * self.sigmoid(self.fc(self.avg_pool(x)) + self.fc(self.max_pool(x)))   # :56-61
+
+
 class ReferenceUNet(nn.Module):
-    """UNetWithBackbone(n_classes, 'resnet34', pretrained=False, use_attention=False).
+    """UNetWithBackbone(n_classes, 'resnet34', pretrained=False, use_attention).
 
     Registration order (hence state_dict order) follows advanced_models.py:76-100,
     157-160.  ``width`` multiplies every channel count (1 = reference; 2 =
     the build-defined "wide" config of SURVEY.md §0).
     """
 
-    def __init__(self, n_classes: int = 1, width: int = 1):
+    def __init__(self, n_classes: int = 1, width: int = 1, use_attention: bool = False):
         super().__init__()
         c = [64 * width, 128 * width, 256 * width, 512 * width]
+        self.use_attention = use_attention
         self.input_conv = nn.Conv2d(1, c[0], 7, 2, 3, bias=False)
         self.bn1 = nn.BatchNorm2d(c[0])
         self.relu = nn.ReLU(inplace=True)
@@ -150,6 +181,23 @@ class ReferenceUNet(nn.Module):
         self.decoder1 = decoder_block(c[0] + c[0] // 2, c[0] // 2)
         self.upconv0 = nn.ConvTranspose2d(c[0] // 2, c[0] // 4, 2, 2)
         self.conv_final = nn.Conv2d(c[0] // 4, n_classes, 1)
+        if use_attention:   # advanced_models.py:163-172 (resnet34 branch), registered after conv_final
+            self.attention4 = AttentionGate(c[2], c[2], c[1])
+            self.attention3 = AttentionGate(c[1], c[1], c[0])
+            self.attention2 = AttentionGate(c[0], c[0], c[0] // 2)
+            self.attention1 = AttentionGate(c[0] // 2, c[0], c[0] // 2)
+            self.ch_attention4 = ChannelAttention(c[2])
+            self.ch_attention3 = ChannelAttention(c[1])
+            self.ch_attention2 = ChannelAttention(c[0])
+            self.ch_attention1 = ChannelAttention(c[0] // 2)
+
+    def _level(self, lvl: int, skip, up):
+        """One decoder level: skip-first concat (+ attention gate / channel attention, :286-334)."""
+        dec = getattr(self, f"decoder{lvl}")
+        if not self.use_attention:
+            return dec(torch.cat((skip, up), 1))
+        skip = getattr(self, f"attention{lvl}")(g=up, x=skip)
+        return getattr(self, f"ch_attention{lvl}")(dec(torch.cat((skip, up), 1)))
 
     def forward(self, x):
         x1 = self.relu(self.bn1(self.input_conv(x)))          # :268-270
@@ -157,15 +205,15 @@ class ReferenceUNet(nn.Module):
         x3 = self.enc2(x2)
         x4 = self.enc3(x3)
         x5 = self.enc4(x4)                                    # :276
-        d = self.decoder4(torch.cat((x4, self.upconv4(x5)), 1))   # :284,292-293
-        d = self.decoder3(torch.cat((x3, self.upconv3(d)), 1))    # :295-303
-        d = self.decoder2(torch.cat((x2, self.upconv2(d)), 1))    # :305-313
+        d = self._level(4, x4, self.upconv4(x5))             # :284-293
+        d = self._level(3, x3, self.upconv3(d))              # :295-303
+        d = self._level(2, x2, self.upconv2(d))              # :305-313
         u = self.upconv1(d)                                   # :315
         if u.shape != x1.shape:                               # :318-325 crop
             dh, dw = x1.shape[2] - u.shape[2], x1.shape[3] - u.shape[3]
             if dh > 0 and dw > 0:
                 x1 = x1[:, :, dh // 2:dh // 2 + u.shape[2], dw // 2:dw // 2 + u.shape[3]]
-        d = self.decoder1(torch.cat((x1, u), 1))              # :333-334
+        d = self._level(1, x1, u)                             # :327-334
         d0 = self.upconv0(d)                                  # :337
         if d0.shape[2] != x.shape[2] or d0.shape[3] != x.shape[3]:   # :340-347
             dh, dw = d0.shape[2] - x.shape[2], d0.shape[3] - x.shape[3]

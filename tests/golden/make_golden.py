@@ -313,6 +313,43 @@ def main():
     for k, p in tiny.named_parameters():
         tout["grad/" + k] = p.grad.numpy()
     np.savez_compressed(os.path.join(HERE, "tiny64.npz"), **tout)
+
+    # ---------------- attention decoder (use_attention=True, the reference default) ----------------
+    torch.manual_seed(0)
+    ref = am.UNetWithBackbone(n_classes=1, backbone="resnet34", pretrained=False, use_attention=True)
+    orc = oracle.ReferenceUNet(use_attention=True)
+    rk = [(k, tuple(v.shape)) for k, v in ref.state_dict().items()]
+    ok = [(k, tuple(v.shape)) for k, v in orc.state_dict().items()]
+    assert rk == ok, "attention state_dict layout differs from the reference"
+    sd = oracle.closed_form_state_dict(orc, seed=0)
+    ref.load_state_dict(sd); orc.load_state_dict(sd)
+    ref.train(); orc.train()
+    lr_ = ref(x); lo_ = orc(x)
+    assert torch.equal(lr_, lo_), "attention: oracle logits != reference logits"
+    loss_r = ref_losses.get_loss_function({"loss_fn": "bce"})(lr_, m)
+    loss_o = oracle.get_loss_function({"loss_fn": "bce"})(lo_, m)
+    assert torch.equal(loss_r, loss_o)
+    loss_r.backward(); loss_o.backward()
+    gr = dict(ref.named_parameters()); go = dict(orc.named_parameters())
+    for k in gr:
+        assert torch.equal(gr[k].grad, go[k].grad), k
+    aout = {"x": x_np, "masks": m_np, "n_params": np.int64(sum(p.numel() for p in ref.parameters())),
+            "logits_train": lr_.detach().numpy(), "loss_bce": np.float32(loss_r.item())}
+    for k in gr:
+        if k.startswith(("attention", "ch_attention", "conv_final", "upconv0")):
+            aout["grad/" + k] = gr[k].grad.numpy().copy()
+    bref = dict(ref.named_buffers())
+    for k in bref:
+        if k.startswith("attention") and not k.endswith("num_batches_tracked"):
+            aout["buf/" + k] = bref[k].numpy().copy()
+    ref.load_state_dict(sd); orc.load_state_dict(sd)
+    ref.eval(); orc.eval()
+    with torch.no_grad():
+        le = ref(x); lo = orc(x)
+    assert torch.equal(le, lo)
+    aout["logits_eval"] = le.numpy()
+    np.savez_compressed(os.path.join(HERE, "attn64.npz"), **aout)
+    print("attn64.npz: params", int(aout["n_params"]), "bce", aout["loss_bce"])
     print("fixtures written; oracle == reference on every case")
 
 

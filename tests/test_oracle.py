@@ -123,3 +123,33 @@ def test_tiny_config(golden):
     assert loss.item() == float(g["loss_bce"])
     for k, p in t.named_parameters():
         np.testing.assert_array_equal(p.grad.numpy(), g["grad/" + k])
+
+
+def test_attention_decoder_matches_reference(golden):
+    """use_attention=True (advanced_models.py:7-61,163-172,286-334): the oracle's
+    AttentionGate / ChannelAttention restatement is bit-identical to the
+    reference on train logits, loss, every attention / head gradient, the
+    attention BN running statistics and eval logits (fixture attn64.npz)."""
+    a = golden("attn64.npz")
+    m = oracle.ReferenceUNet(use_attention=True)
+    m.load_state_dict(oracle.closed_form_state_dict(m, seed=0))
+    assert sum(p.numel() for p in m.parameters()) == int(a["n_params"]) == 24441229
+    x, y = torch.from_numpy(a["x"]), torch.from_numpy(a["masks"])
+    m.train()
+    out = m(x)
+    assert torch.equal(out, torch.from_numpy(a["logits_train"]))
+    loss = oracle.get_loss_function({"loss_fn": "bce"})(out, y)
+    assert loss.item() == float(a["loss_bce"])
+    loss.backward()
+    params = dict(m.named_parameters())
+    keys = [k[5:] for k in a.files if k.startswith("grad/")]
+    assert any(k.startswith("ch_attention1.") for k in keys) and any(k.startswith("attention4.psi") for k in keys)
+    for k in keys:
+        assert torch.equal(params[k].grad, torch.from_numpy(a["grad/" + k])), k
+    bufs = dict(m.named_buffers())
+    for k in [f[4:] for f in a.files if f.startswith("buf/")]:
+        assert torch.equal(bufs[k], torch.from_numpy(a["buf/" + k])), k
+    m.load_state_dict(oracle.closed_form_state_dict(m, seed=0))
+    m.eval()
+    with torch.no_grad():
+        assert torch.equal(m(x), torch.from_numpy(a["logits_eval"]))
