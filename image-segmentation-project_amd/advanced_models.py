@@ -48,12 +48,35 @@ def _decoder_block(cin, cout):
                          nn.Conv2d(cout, cout, 3, padding=1), nn.BatchNorm2d(cout), nn.ReLU(inplace=True))
 
 
+class _AttentionGate(nn.Module):
+    """Parameter container of ``AttentionGate`` (advanced_models.py:7-40); computed natively."""
+
+    def __init__(self, f_g, f_l, f_int):
+        super().__init__()
+        self.W_g = nn.Sequential(nn.Conv2d(f_g, f_int, 1, bias=True), nn.BatchNorm2d(f_int))
+        self.W_x = nn.Sequential(nn.Conv2d(f_l, f_int, 1, bias=True), nn.BatchNorm2d(f_int))
+        self.psi = nn.Sequential(nn.Conv2d(f_int, 1, 1, bias=True), nn.BatchNorm2d(1), nn.Sigmoid())
+        self.relu = nn.ReLU(inplace=True)
+
+
+class _ChannelAttention(nn.Module):
+    """Parameter container of ``ChannelAttention`` (advanced_models.py:43-61); computed natively."""
+
+    def __init__(self, c, reduction_ratio=16):
+        super().__init__()
+        self.avg_pool = nn.AdaptiveAvgPool2d(1)
+        self.max_pool = nn.AdaptiveMaxPool2d(1)
+        self.fc = nn.Sequential(nn.Conv2d(c, c // reduction_ratio, 1, bias=False), nn.ReLU(inplace=True),
+                                nn.Conv2d(c // reduction_ratio, c, 1, bias=False))
+        self.sigmoid = nn.Sigmoid()
+
+
 class _Plan:
     """Owns one native plan (per input shape) and its persistent workspace."""
 
-    def __init__(self, n, h, w, width, n_classes, device):
+    def __init__(self, n, h, w, width, n_classes, device, attention=False):
         lib = _lib.load()
-        cfg = _lib.UnetConfig(n, h, w, width, n_classes, 1e-5, 0.1)
+        cfg = _lib.UnetConfig(n, h, w, width, n_classes, 1e-5, 0.1, 1 if attention else 0)
         handle = ctypes.c_void_p()
         _lib.check(lib.unet_plan_create(ctypes.byref(cfg), ctypes.byref(handle)), "unet_plan_create")
         self.lib, self.handle = lib, handle
@@ -149,20 +172,18 @@ class _UNetFunction(torch.autograd.Function):
 
 
 class UNetWithBackbone(nn.Module):
-    """Drop-in for ``advanced_models.UNetWithBackbone`` (resnet34, use_attention=False).
+    """Drop-in for ``advanced_models.UNetWithBackbone`` (resnet34, with or without attention).
 
     ``width`` is a build extension (1 = reference channels); ``backbone`` other
-    than 'resnet34' and ``use_attention=True`` are the SURVEY.md §8(f) "next"
-    rows and raise ``NotImplementedError``.
+    than 'resnet34' is a SURVEY.md §8(f) "next" row and raises
+    ``NotImplementedError``.  ``use_attention=True`` (the reference default)
+    adds the AttentionGate / ChannelAttention decoder (advanced_models.py:7-61).
     """
 
     def __init__(self, n_classes=1, backbone="resnet34", pretrained=True, use_attention=True, width=1):
         super().__init__()
         if backbone != "resnet34":
             raise NotImplementedError(f"backbone={backbone!r}: only 'resnet34' is built for MI355X (SURVEY.md §8)")
-        if use_attention:
-            raise NotImplementedError("use_attention=True (AttentionGate/ChannelAttention) is not built yet; "
-                                      "pass use_attention=False (the configuration every experiment trains)")
         if n_classes != 1:
             raise NotImplementedError("n_classes must be 1 (binary segmentation, advanced_models.py:160)")
         if pretrained:
@@ -190,6 +211,15 @@ class UNetWithBackbone(nn.Module):
         self.decoder1 = _decoder_block(c0 + c0 // 2, c0 // 2)
         self.upconv0 = nn.ConvTranspose2d(c0 // 2, c0 // 4, kernel_size=2, stride=2)
         self.conv_final = nn.Conv2d(c0 // 4, n_classes, kernel_size=1)
+        if use_attention:  # advanced_models.py:163-172 (resnet34), registered after conv_final
+            self.attention4 = _AttentionGate(c2, c2, c1)
+            self.attention3 = _AttentionGate(c1, c1, c0)
+            self.attention2 = _AttentionGate(c0, c0, c0 // 2)
+            self.attention1 = _AttentionGate(c0 // 2, c0, c0 // 2)
+            self.ch_attention4 = _ChannelAttention(c2)
+            self.ch_attention3 = _ChannelAttention(c1)
+            self.ch_attention2 = _ChannelAttention(c0)
+            self.ch_attention1 = _ChannelAttention(c0 // 2)
         self._plans = {}
         self._ddp = None  # set by ddp.enable_data_parallel
 
@@ -210,7 +240,7 @@ class UNetWithBackbone(nn.Module):
         key = (n, h, w, x.device)
         plan = self._plans.get(key)
         if plan is None:
-            plan = _Plan(n, h, w, self.width, 1, x.device)
+            plan = _Plan(n, h, w, self.width, 1, x.device, self.use_attention)
             names = [k for k, _ in self.named_parameters()]
             if names != plan.param_names:
                 raise RuntimeError("native parameter table does not match the module's named_parameters()")
@@ -273,7 +303,7 @@ class UNetWithBackbone(nn.Module):
         """Algorithmic FLOPs of one step at input shape [N,1,H,W]."""
         n, _, h, w = x_shape
         lib = _lib.load()
-        cfg = _lib.UnetConfig(n, h, w, self.width, 1, 1e-5, 0.1)
+        cfg = _lib.UnetConfig(n, h, w, self.width, 1, 1e-5, 0.1, 1 if self.use_attention else 0)
         handle = ctypes.c_void_p()
         _lib.check(lib.unet_plan_create(ctypes.byref(cfg), ctypes.byref(handle)), "unet_plan_create")
         try:

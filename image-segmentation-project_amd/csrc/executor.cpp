@@ -81,6 +81,22 @@ struct Dec {
   bool split = false;
 };
 
+// use_attention=True: AttentionGate on the skip (advanced_models.py:7-40,286-331)
+// and ChannelAttention on the decoder output (:43-61,294,...) of one level
+struct Att {
+  int wg, bng, wx, bnx, psi_w, psi_b, psibn, fc1, fc2;  // conv / BN / param indices
+  int Fg, Fl, Fi, C, Cr;
+  Act x;               // the skip activation (own buffer; the concat slice holds x * psi)
+  Act g1, xa, s;       // W_g g, W_x x, relu(BN_g + BN_x)
+  size_t p = 0, psi = 0, dbnp = 0;     // fp32 [npix]: psi logits, sigmoid(BN(p)), dL/dBN(p)
+  size_t pst = 0, pbs = 0, psave = 0;  // fp64 [2] fwd sums, fp64 [2] bwd sums, fp32 mean|invstd
+  Act dS, dg1, dxa, dxpsi, dskip, du;  // gradients (du = up-conv output grad incl. the W_g path)
+  Act out2, d_out2;                    // decoder output * channel gate, and its gradient
+  size_t psum = 0, pkey = 0;           // fp32 [N][C] pooled sums, u64 [N][C] (max, first index) keys
+  size_t ca = 0, ch = 0, cam = 0;      // fp32 gate [N][C], hidden [N][2][Cr], avg|max [N][2][C]
+  size_t cda = 0, cdam = 0;            // fp32 dL/dgate [N][C], dL/d(avg|max) [N][2][C]
+};
+
 }  // namespace unet
 
 using namespace unet;
@@ -92,6 +108,7 @@ struct unet_plan {
   std::vector<Conv> convs;
   std::vector<Block> blocks;  // 16 encoder blocks
   std::vector<Dec> decs;      // decoder4..decoder1 (index 0 = level 4)
+  std::vector<Att> atts;      // attention of decoder level (same index), when cfg.attention
   int stem_conv, stem_bn, up0_w, up0_b, fin_w, fin_b;
   Act x1, y0, p0, d_x1, d_y0, d_p0;
   size_t pidx = 0;
@@ -292,6 +309,29 @@ static int build_plan(unet_plan* p) {
   p->up0_b = add_param(p, "upconv0.bias", {c0 / 4});
   p->fin_w = add_param(p, "conv_final.weight", {c.n_classes, c0 / 4, 1, 1});
   p->fin_b = add_param(p, "conv_final.bias", {c.n_classes});
+  if (c.attention) {  // advanced_models.py:163-172, registered after conv_final
+    const int fi[4] = {c1, c0, c0 / 2, c0 / 2};
+    for (int l = 0; l < 4; ++l) {
+      const std::string pre = "attention" + std::to_string(4 - l);
+      Att t;
+      t.Fg = dspecs[l].upout; t.Fl = dspecs[l].skipc; t.Fi = fi[l];
+      t.wg = add_conv(p, pre + ".W_g.0", L_CONV, t.Fg, t.Fi, 1, 1, 0, true);
+      t.bng = add_bn(p, pre + ".W_g.1", t.Fi);
+      t.wx = add_conv(p, pre + ".W_x.0", L_CONV, t.Fl, t.Fi, 1, 1, 0, true);
+      t.bnx = add_bn(p, pre + ".W_x.1", t.Fi);
+      t.psi_w = add_param(p, pre + ".psi.0.weight", {1, t.Fi, 1, 1});
+      t.psi_b = add_param(p, pre + ".psi.0.bias", {1});
+      t.psibn = add_bn(p, pre + ".psi.1", 1);
+      p->atts.push_back(t);
+    }
+    for (int l = 0; l < 4; ++l) {
+      const std::string pre = "ch_attention" + std::to_string(4 - l);
+      Att& t = p->atts[l];
+      t.C = dspecs[l].outc; t.Cr = t.C / 16;
+      t.fc1 = add_param(p, pre + ".fc.0.weight", {t.Cr, t.C, 1, 1});
+      t.fc2 = add_param(p, pre + ".fc.2.weight", {t.C, t.Cr, 1, 1});
+    }
+  }
 
   // ---- DDP buckets in backward completion order ----
   auto stage_range = [&](int s) {
@@ -318,6 +358,12 @@ static int build_plan(unet_plan* p) {
     b.stats = A.take((size_t)kStatRep * 2 * b.C * sizeof(double));
     b.tfwd = A.take(sizeof(unsigned));
   }
+  for (int l = 0; l < (int)p->atts.size(); ++l) {
+    Att& t = p->atts[l];
+    t.pst = A.take(2 * sizeof(double));
+    t.psum = A.take((size_t)N * t.C * sizeof(float));
+    t.pkey = A.take((size_t)N * t.C * sizeof(unsigned long long));
+  }
   p->zero_fwd_bytes = A.top - p->zero_fwd_off;
   // zeroed at backward start: BN bwd sums, convT bias sums, head sums, wgrad accumulators
   p->zero_bwd_off = A.take(0);
@@ -333,6 +379,10 @@ static int build_plan(unet_plan* p) {
     if (cv.kind == L_STEM) n = (size_t)cv.Co * 64;
     else n = (size_t)cv.Co * cv.Ci * cv.R * cv.S;
     cv.wacc = A.take(n * sizeof(float));
+  }
+  for (auto& t : p->atts) {
+    t.pbs = A.take(2 * sizeof(double));
+    t.cda = A.take((size_t)N * t.C * sizeof(float));
   }
   p->zero_bwd_bytes = A.top - p->zero_bwd_off;
   for (auto& b : p->bns) {
@@ -353,7 +403,7 @@ static int build_plan(unet_plan* p) {
   // forward activations
   const int H2 = H / 2, W2 = W / 2, H4 = H / 4, W4 = W / 4;
   Act cat1 = act(A, N, H2, W2, c0 + c0 / 2);
-  p->x1 = slice(cat1, 0, c0);
+  p->x1 = c.attention ? act(A, N, H2, W2, c0) : slice(cat1, 0, c0);
   p->y0 = act(A, N, H2, W2, c0);
   p->p0 = act(A, N, H4, W4, c0);
   p->pidx = A.take((size_t)N * H4 * W4 * c0);
@@ -381,6 +431,7 @@ static int build_plan(unet_plan* p) {
     const bool last = (i + 1 == specs.size()) || specs[i + 1].stage != s.stage;
     if (last) {
       if (s.stage == 3) b.out = x5;
+      else if (c.attention) b.out = act(A, N, Hs, Ws, s.cout);  // gated copy goes into the concat
       else b.out = slice(cats[2 - s.stage], 0, s.cout);  // x2->cat2, x3->cat3, x4->cat4
     } else {
       b.out = act(A, N, Hs, Ws, s.cout);
@@ -403,6 +454,39 @@ static int build_plan(unet_plan* p) {
     d.out = act(A, N, Hl, Wl, s.outc);
     p->decs.push_back(d);
     dec_in = d.out;
+    if (c.attention) {
+      Att& t = p->atts[l];
+      const int64_t np = (int64_t)N * Hl * Wl;
+      t.g1 = act(A, N, Hl, Wl, t.Fi);
+      t.xa = act(A, N, Hl, Wl, t.Fi);
+      t.s = act(A, N, Hl, Wl, t.Fi);
+      t.p = A.take(np * sizeof(float));
+      t.psi = A.take(np * sizeof(float));
+      t.dbnp = A.take(np * sizeof(float));
+      t.psave = A.take(2 * sizeof(float));
+      t.ca = A.take((size_t)N * t.C * sizeof(float));
+      t.ch = A.take((size_t)N * 2 * t.Cr * sizeof(float));
+      t.cam = A.take((size_t)N * 2 * t.C * sizeof(float));
+      t.cdam = A.take((size_t)N * 2 * t.C * sizeof(float));
+      t.out2 = act(A, N, Hl, Wl, t.C);
+      t.d_out2 = act(A, N, Hl, Wl, t.C);
+      t.dS = act(A, N, Hl, Wl, t.Fi);
+      t.dg1 = act(A, N, Hl, Wl, t.Fi);
+      t.dxa = act(A, N, Hl, Wl, t.Fi);
+      t.dxpsi = act(A, N, Hl, Wl, t.Fl);
+      t.dskip = act(A, N, Hl, Wl, t.Fl);
+      t.du = act(A, N, Hl, Wl, t.Fg);
+      dec_in = t.out2;
+    }
+  }
+  if (c.attention) {  // skips: x4 = enc3 out, x3 = enc2 out, x2 = enc1 out, x1 = stem
+    int last[3] = {-1, -1, -1};
+    for (size_t i = 0; i < specs.size(); ++i)
+      if (specs[i].stage < 3) last[specs[i].stage] = (int)i;
+    p->atts[0].x = p->blocks[last[2]].out;
+    p->atts[1].x = p->blocks[last[1]].out;
+    p->atts[2].x = p->blocks[last[0]].out;
+    p->atts[3].x = p->x1;
   }
 
   // backward gradient tensors
@@ -425,7 +509,8 @@ static int build_plan(unet_plan* p) {
   }
   for (int l = 0; l < 4; ++l) {
     Dec& d = p->decs[l];
-    d.d_up_in = (l == 0) ? act(A, N, H / 32, W / 32, c3) : p->decs[l - 1].d_out;
+    d.d_up_in = (l == 0) ? act(A, N, H / 32, W / 32, c3)
+                         : (c.attention ? p->atts[l - 1].d_out2 : p->decs[l - 1].d_out);
   }
   for (auto& b : p->blocks) {
     const int Hs = b.y1.H, Ws = b.y1.W, C = b.y1.C;
@@ -451,7 +536,7 @@ static int build_plan(unet_plan* p) {
       // input x_{s+1} also fed cat_{s+1} slice 0: add that slice's gradient
       const int s = specs[i].stage;            // 1..3
       const int l = 3 - s;                     // x2 (s=1) -> cats[2], x3 -> cats[1], x4 -> cats[0]
-      b.skip_add = slice(p->decs[l].dcat, 0, specs[i].cin);
+      b.skip_add = c.attention ? p->atts[l].dskip : slice(p->decs[l].dcat, 0, specs[i].cin);
     }
   }
   p->d_x1 = act(A, N, H2, W2, c0);
@@ -483,6 +568,14 @@ static int build_plan(unet_plan* p) {
     nm.push_back({pre + "out", d.out});
     nm.push_back({pre + "d.out", d.d_out}); nm.push_back({pre + "d.y2", d.dy2}); nm.push_back({pre + "d.h", d.dh});
     nm.push_back({pre + "d.y1", d.dy1});
+    if (!p->atts.empty()) {
+      const Att& t = p->atts[l];
+      const std::string ap = "att" + std::to_string(4 - l) + ".";
+      nm.push_back({ap + "x", t.x}); nm.push_back({ap + "g1", t.g1}); nm.push_back({ap + "xa", t.xa});
+      nm.push_back({ap + "s", t.s}); nm.push_back({ap + "out2", t.out2}); nm.push_back({ap + "d.out2", t.d_out2});
+      nm.push_back({ap + "d.S", t.dS}); nm.push_back({ap + "d.g1", t.dg1}); nm.push_back({ap + "d.xa", t.dxa});
+      nm.push_back({ap + "d.skip", t.dskip}); nm.push_back({ap + "d.u", t.du});
+    }
     if (d.split) { nm.push_back({pre + "d.cat.skip", d.dcat}); nm.push_back({pre + "d.cat.up", d.dcat_up}); }
     else nm.push_back({pre + "d.cat", d.dcat});
   }
@@ -520,6 +613,11 @@ static int build_plan(unet_plan* p) {
     const double px = (double)N * d.y1.H * d.y1.W;
     fw += 2 * px * p->convs[d.conv1].Ci * p->convs[d.conv1].Co * 9;
     fw += 2 * px * p->convs[d.conv2].Ci * p->convs[d.conv2].Co * 9;
+  }
+  for (int l = 0; l < (int)p->atts.size(); ++l) {  // attention 1x1 convs + psi + channel MLP
+    const Att& t = p->atts[l];
+    const double px = (double)N * p->decs[l].y1.H * p->decs[l].y1.W;
+    fw += 2 * px * t.Fi * (t.Fg + t.Fl + 1) + 2.0 * N * 2 * 2 * t.C * t.Cr;
   }
   fw += 2.0 * N * H2 * W2 * (c0 / 2) * (c0 / 4) * 4;  // upconv0
   fw += 2.0 * N * H * W * (c0 / 4);                    // conv_final
@@ -748,6 +846,82 @@ int unpack_bucket(const Ctx& x, int bk, float* grads) {
     if (r_) return r_;         \
   } while (0)
 
+// attention-gate / channel-attention argument blocks of decoder level l
+AttGateArgs gate_args(const Ctx& x, int l, float* grads) {
+  const unet_plan* p = x.p;
+  const Att& t = p->atts[l];
+  const Dec& d = p->decs[l];
+  const Bn& b = p->bns[t.psibn];
+  AttGateArgs a = {};
+  a.s = x.A(t.s); a.lds = t.s.ld;
+  a.psi_w = x.prm[t.psi_w]; a.psi_b = x.prm[t.psi_b];
+  a.p = x.W<float>(t.p); a.psi = x.W<float>(t.psi); a.dbnp = x.W<float>(t.dbnp);
+  a.pst = x.W<double>(t.pst); a.pbs = x.W<double>(t.pbs); a.save = x.W<float>(t.psave);
+  a.gamma = x.prm[b.gamma]; a.beta = x.prm[b.beta];
+  a.run_mean = x.buf ? x.buf[3 * b.idx + 0] : nullptr;
+  a.run_var = x.buf ? x.buf[3 * b.idx + 1] : nullptr;
+  a.npix = (int64_t)p->cfg.N * d.cat.H * d.cat.W;
+  a.count = (double)a.npix; a.eps = p->cfg.bn_eps; a.momentum = p->cfg.bn_momentum; a.training = x.training;
+  a.x = x.A(t.x); a.ldx = t.x.ld;
+  const Act xs = slice(d.cat, 0, t.Fl);
+  a.xatt = x.A(xs); a.ldxatt = xs.ld;
+  a.dxatt = x.A(d.dcat); a.lddxatt = d.dcat.ld;  // skip channels come first (split or not)
+  a.dxpsi = x.A(t.dxpsi); a.lddxpsi = t.dxpsi.ld;
+  a.dS = x.A(t.dS); a.lddS = t.dS.ld;
+  if (grads) {
+    a.gpsi_w = grads + p->params[t.psi_w].flat;
+    a.ggamma = grads + p->params[b.gamma].flat;
+    a.gbeta = grads + p->params[b.beta].flat;
+  }
+  a.Fi = t.Fi; a.Fl = t.Fl;
+  return a;
+}
+
+ChAttArgs ch_args(const Ctx& x, int l, float* grads) {
+  const unet_plan* p = x.p;
+  const Att& t = p->atts[l];
+  const Dec& d = p->decs[l];
+  ChAttArgs c = {};
+  c.y = x.A(d.out); c.ldy = d.out.ld;
+  c.out = x.A(t.out2); c.ldo = t.out2.ld;
+  c.psum = x.W<float>(t.psum); c.pkey = x.W<unsigned long long>(t.pkey);
+  c.w1 = x.prm[t.fc1]; c.w2 = x.prm[t.fc2];
+  c.am = x.W<float>(t.cam); c.h = x.W<float>(t.ch); c.gate = x.W<float>(t.ca);
+  c.dout2 = x.A(t.d_out2); c.lddo2 = t.d_out2.ld;
+  c.dgate = x.W<float>(t.cda); c.dam = x.W<float>(t.cdam);
+  if (grads) {
+    c.gw1 = grads + p->params[t.fc1].flat;
+    c.gw2 = grads + p->params[t.fc2].flat;
+  }
+  c.dout = x.A(d.d_out); c.lddo = d.d_out.ld;
+  c.HW = (int64_t)d.out.H * d.out.W;
+  c.inv_hw = 1.0f / (float)c.HW;
+  c.N = p->cfg.N; c.C = t.C; c.Cr = t.Cr;
+  return c;
+}
+
+// AttentionGate forward (advanced_models.py:28-40): x_att = x * sigmoid(BN(psi(relu(BN(W_g g) + BN(W_x x)))))
+int att_gate_forward(const Ctx& x, int l) {
+  const Att& t = x.p->atts[l];
+  const Dec& d = x.p->decs[l];
+  RUN(conv_forward(x, t.wg, d.up_out, t.g1, t.bng));
+  RUN(conv_forward(x, t.wx, t.x, t.xa, t.bnx));
+  RUN(bn_apply(x, t.bng, t.g1, t.s, 2, &t.xa, t.bnx, true));
+  const AttGateArgs a = gate_args(x, l, nullptr);
+  ProfScope ps(x.p, x.st, "att_gate_fwd", 0);
+  CK(launch_att_gate(a, 0, x.st));
+  CK(launch_att_gate(a, 1, x.st));
+  return 0;
+}
+
+// ChannelAttention forward (advanced_models.py:56-61)
+int ch_att_forward(const Ctx& x, int l) {
+  const ChAttArgs c = ch_args(x, l, nullptr);
+  ProfScope ps(x.p, x.st, "ch_att_fwd", 0);
+  for (int pass = 0; pass < 3; ++pass) CK(launch_ch_att(c, pass, x.st));
+  return 0;
+}
+
 static int run_forward(unet_plan* p, const float* image, const float* const* prm, float* const* buf, char* ws,
                        float* logits, int training, hipStream_t st) {
   Ctx x{p, ws, prm, buf, st, training};
@@ -818,15 +992,19 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
       RUN(bn_apply(x, b.bn2, b.y2, b.out, 1, &b.in, -1, true));
     }
   }
-  for (auto& d : p->decs) {
+  const bool att = !p->atts.empty();
+  for (int l = 0; l < (int)p->decs.size(); ++l) {
+    Dec& d = p->decs[l];
     RUN(conv_forward(x, d.up, d.up_in, d.up_out, -1));
+    if (att) RUN(att_gate_forward(x, l));
     RUN(conv_forward(x, d.conv1, d.cat, d.y1, d.bn1));
     RUN(bn_apply(x, d.bn1, d.y1, d.h, 0, nullptr, -1, true));
     RUN(conv_forward(x, d.conv2, d.h, d.y2, d.bn2));
     RUN(bn_apply(x, d.bn2, d.y2, d.out, 0, nullptr, -1, true));
+    if (att) RUN(ch_att_forward(x, l));
   }
   {
-    const Act& o = p->decs[3].out;
+    const Act& o = att ? p->atts[3].out2 : p->decs[3].out;
     HeadArgs h = {};
     h.x = x.A(o); h.ldx = o.ld;
     h.w0 = prm[p->up0_w]; h.b0 = prm[p->up0_b]; h.wf = prm[p->fin_w]; h.bf = prm[p->fin_b];
@@ -871,19 +1049,24 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
   // fork: the weight stream starts after the zeroing of the accumulators
   auto fork = [&]() { return stream_edge(p, st, x.wst); };
   CK(hipMemsetAsync(ws + p->zero_bwd_off, 0, p->zero_bwd_bytes, st));
+  const bool att = !p->atts.empty();
+  for (auto& t : p->atts)  // gradients accumulated with atomics
+    for (int pi : {t.psi_w, t.fc1, t.fc2})
+      CK(hipMemsetAsync(grads + p->params[pi].flat, 0, sizeof(float) * p->params[pi].numel, st));
   // head (upconv0 + conv_final)
   {
-    const Act& o = p->decs[3].out;
+    const Act& o = att ? p->atts[3].out2 : p->decs[3].out;
     HeadArgs h = {};
     h.x = x.A(o); h.ldx = o.ld;
     h.w0 = prm[p->up0_w]; h.b0 = prm[p->up0_b]; h.wf = prm[p->fin_w]; h.bf = prm[p->fin_b];
     h.dl = dlogits;
-    h.dx = x.A(p->decs[3].d_out); h.lddx = p->decs[3].d_out.ld;
+    const Act& hdx = att ? p->atts[3].d_out2 : p->decs[3].d_out;
+    h.dx = x.A(hdx); h.lddx = hdx.ld;
     h.usum = x.W<double>(p->head_usum);
     h.gw0 = grads + p->params[p->up0_w].flat; h.gb0 = grads + p->params[p->up0_b].flat;
     h.gwf = grads + p->params[p->fin_w].flat; h.gbf = grads + p->params[p->fin_b].flat;
     h.N = N; h.H = o.H; h.W = o.W; h.Cin = o.C; h.Co = (int)p->params[p->up0_b].numel;
-    if (p->fuse_bwd) {  // the head produces dA of decoder1's last BN: reduce it here
+    if (p->fuse_bwd && !att) {  // the head produces dA of decoder1's last BN: reduce it here
       const Dec& d = p->decs[3];
       h.bb = bwd_args(x, d.bn2, d.d_out, d.out, d.y2, d.dy2, -1, nullptr, nullptr, nullptr, grads);
     }
@@ -915,7 +1098,16 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
   // decoder1 .. decoder4 (+ their up-convs)
   for (int l = 3; l >= 0; --l) {
     Dec& d = p->decs[l];
-    RUN(bn_backward(x, d.bn2, dec_bn2(l), fz));
+    if (att) {  // ChannelAttention backward: dOut2 -> dOut, then the unfused BN backward
+      const ChAttArgs c = ch_args(x, l, grads);
+      {
+        ProfScope ps(p, st, "ch_att_bwd", 0);
+        for (int pass = 3; pass < 6; ++pass) CK(launch_ch_att(c, pass, st));
+      }
+      RUN(bn_backward(x, d.bn2, dec_bn2(l), false));
+    } else {
+      RUN(bn_backward(x, d.bn2, dec_bn2(l), fz));
+    }
     RUN(fork());
     RUN(conv_wgrad(x, d.conv2, d.dy2, d.h));
     const BnBwdArgs f1 = dec_bn1(l);
@@ -930,8 +1122,28 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     CK(hipMemsetAsync(grads + p->params[p->convs[d.conv2].b].flat, 0, sizeof(float) * p->convs[d.conv2].Co, st));
     // up-conv: dU = dcat[:, skip:]; its dgrad is dA of the previous decoder's
     // (or enc4's) last BN
+    if (att) {  // AttentionGate backward (skip gradient -> dskip, g-path gradient added into du)
+      Att& t = p->atts[l];
+      const AttGateArgs a = gate_args(x, l, grads);
+      {
+        ProfScope ps(p, st, "att_gate_bwd", 0);
+        CK(launch_att_gate(a, 2, st));
+        CK(launch_att_gate(a, 3, st));
+      }
+      RUN(bn_backward(x, t.bng, bwd_args(x, t.bng, t.dS, t.s, t.g1, t.dg1, t.bnx, &t.xa, &t.dxa, nullptr, grads),
+                      false));
+      RUN(fork());
+      RUN(conv_wgrad(x, t.wg, t.dg1, d.up_out));
+      RUN(conv_wgrad(x, t.wx, t.dxa, t.x));
+      RUN(conv_dgrad(x, t.wg, t.dg1, t.du, &d.dcat_up));
+      RUN(conv_dgrad(x, t.wx, t.dxa, t.dskip, &t.dxpsi));
+      // W_g / W_x / psi conv biases feed a training-mode BN: exact gradient 0
+      for (int ci : {t.wg, t.wx})
+        CK(hipMemsetAsync(grads + p->params[p->convs[ci].b].flat, 0, sizeof(float) * p->convs[ci].Co, st));
+      CK(hipMemsetAsync(grads + p->params[t.psi_b].flat, 0, sizeof(float), st));
+    }
     const Conv& up = p->convs[d.up];
-    const Act du = d.dcat_up;
+    const Act du = att ? p->atts[l].du : d.dcat_up;
     RUN(fork());
     RUN(conv_wgrad(x, d.up, du, d.up_in));
     {
@@ -940,7 +1152,10 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
       CK(launch_d2f(x.W<double>(up.bias_acc), grads + p->params[up.b].flat, up.Co, x.wst));
     }
     const BnBwdArgs fu = l > 0 ? dec_bn2(l - 1) : blk_bn2(nb - 1);
-    RUN(conv_dgrad(x, d.up, du, d.d_up_in, nullptr, fz ? &fu : nullptr));
+    // with attention the up-conv input of levels 3..1 is the channel-gated
+    // output: its gradient is not dA of a BN
+    const bool fuse_up = fz && (l == 0 || !att);
+    RUN(conv_dgrad(x, d.up, du, d.d_up_in, nullptr, fuse_up ? &fu : nullptr));
   }
   // bucket 0 also holds the head's and the decoder biases' gradients (main stream)
   RUN(stream_edge(p, st, x.wst));
@@ -982,7 +1197,7 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
   {
     MaxPoolArgs m = {};
     m.dy = x.A(p->d_p0); m.lddy = p->d_p0.ld; m.idx = x.W<uint8_t>(p->pidx);
-    const Act skip = slice(p->decs[3].dcat, 0, p->x1.C);
+    const Act skip = att ? p->atts[3].dskip : slice(p->decs[3].dcat, 0, p->x1.C);
     m.add = x.A(skip); m.ldadd = skip.ld;
     m.dx = x.A(p->d_x1); m.lddx = p->d_x1.ld;
     m.N = N; m.H = p->x1.H; m.W = p->x1.W; m.C = p->x1.C; m.P = p->p0.H; m.Q = p->p0.W;

@@ -194,4 +194,39 @@ hipError_t launch_loss_grad(const float* logits, const float* target, int64_t n,
 hipError_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float* coef, float lr,
                        float beta1, float beta2, float eps, float wd, int advance_step, hipStream_t st);
 
+// attention decoder (attention.hip; advanced_models.py:7-61)
+struct AttGateArgs {
+  const bf16_t* s; int lds;            // relu(BN_g + BN_x), F_int channels
+  const float* psi_w; const float* psi_b;
+  float* p; float* psi; float* dbnp;   // fp32 [npix]
+  double* pst; double* pbs;            // BN(1) fwd sums (sum, sumsq) / bwd sums (sum dZ, sum dZ phat)
+  float* save;                         // mean, invstd
+  const float* gamma; const float* beta; float* run_mean; float* run_var;
+  double count; float eps, momentum; int training;
+  const bf16_t* x; int ldx;            // skip activation (F_l channels)
+  bf16_t* xatt; int ldxatt;            // x * psi (concat slice)
+  const bf16_t* dxatt; int lddxatt;    // its gradient
+  bf16_t* dxpsi; int lddxpsi;          // gate-path skip gradient
+  bf16_t* dS; int lddS;                // dA of relu(BN_g + BN_x)
+  float* gpsi_w; float* ggamma; float* gbeta;
+  int64_t npix; int Fi, Fl;
+};
+struct ChAttArgs {
+  const bf16_t* y; int ldy;            // decoder output
+  bf16_t* out; int ldo;                // y * gate
+  float* psum; unsigned long long* pkey;
+  const float* w1; const float* w2;    // fc.0 [Cr][C], fc.2 [C][Cr]
+  float* am; float* h; float* gate;    // avg|max [N][2][C], hidden [N][2][Cr], gate [N][C]
+  const bf16_t* dout2; int lddo2;
+  float* dgate; float* dam;            // [N][C], [N][2][C]
+  float* gw1; float* gw2;
+  bf16_t* dout; int lddo;
+  float inv_hw;
+  int64_t HW; int N, C, Cr;
+};
+// pass 0 psi fwd, 1 gate fwd, 2 bwd reduce, 3 bwd apply
+hipError_t launch_att_gate(const AttGateArgs& a, int pass, hipStream_t st);
+// pass 0 pool, 1 MLP fwd, 2 scale, 3 bwd reduce, 4 MLP bwd, 5 bwd apply
+hipError_t launch_ch_att(const ChAttArgs& a, int pass, hipStream_t st);
+
 }  // namespace unet

@@ -42,6 +42,8 @@ typedef struct unet_config {
   int n_classes;     /* must be 1 (binary segmentation, advanced_models.py:160) */
   float bn_eps;      /* 1e-5  (torch.nn.BatchNorm2d default)                   */
   float bn_momentum; /* 0.1                                                    */
+  int attention;     /* 1: AttentionGate + ChannelAttention decoder            */
+                     /*    (use_attention=True, advanced_models.py:7-61,163-172) */
 } unet_config;
 
 const char* unet_last_error(void);
