@@ -51,14 +51,14 @@ def pmc_traffic(kernel: str):
     return None
 
 
-def cpu_baseline(batch: int, h: int, steps: int, threads: int, width: int = 1):
+def cpu_baseline(batch: int, h: int, steps: int, threads: int, width: int = 1, attention: bool = False):
     """Time the oracle (fp32 torch-CPU restatement of the reference path) on host cores."""
     import oracle
     torch.set_num_threads(threads)
     pkg = importlib.import_module("image-segmentation-project_amd")
     xs, ms = pkg.synthetic_cells(batch, h, h, seed=1234)
     x, y = torch.from_numpy(xs), torch.from_numpy(ms)
-    m = oracle.ReferenceUNet(width=width)
+    m = oracle.ReferenceUNet(width=width, use_attention=attention)
     m.load_state_dict(oracle.closed_form_state_dict(m))
     m.train()
     opt = oracle.make_adam(m)
@@ -80,6 +80,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=16, help="images per GPU")
     ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--attention", action="store_true",
+                    help="use_attention=True decoder (AttentionGate + ChannelAttention, the reference default)")
     ap.add_argument("--width", type=int, default=1,
                     help="channel multiplier: 1 = Base (configs[1]), 2 = Wide 128->1024 (configs[4], bf16 here)")
     ap.add_argument("--cpu-steps", type=int, default=2)
@@ -103,8 +105,8 @@ def main():
     ddp = importlib.import_module("image-segmentation-project_amd.ddp")
 
     torch.manual_seed(0)
-    model = pkg.UNetWithBackbone(n_classes=1, backbone="resnet34", pretrained=False, use_attention=False,
-                                  width=args.width).to(dev)
+    model = pkg.UNetWithBackbone(n_classes=1, backbone="resnet34", pretrained=False,
+                                  use_attention=args.attention, width=args.width).to(dev)
     if world > 1:
         ddp.enable_data_parallel(model)
     use_graph = args.graph if args.graph is not None else world == 1
@@ -192,7 +194,8 @@ def main():
         "data": "synthetic (Gaussian cells, seed 1234+rank), random-init weights",
         "miou": round(miou, 6),
         "config": {"workload": ("Base" if args.width == 1 else f"Wide (x{args.width} channels)")
-                   + " U-Net resnet34 no-attention train step (fwd+bce+bwd+Adam)",
+                   + " U-Net resnet34 " + ("attention" if args.attention else "no-attention")
+                   + " train step (fwd+bce+bwd+Adam)",
                    "global_batch": args.batch * world, "image": f"{args.size}x{args.size}",
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "achieved": round(achieved_tflops, 2), "peak": MFMA_BF16_PEAK_TFLOPS,
@@ -209,7 +212,8 @@ def main():
         "optimizer": "torch.optim.Adam (foreach)" if args.torch_adam else "fused HIP Adam (unet_adam_step)",
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.batch, args.size, args.cpu_steps, args.cpu_threads, args.width)
+        line["cpu_baseline"] = cpu_baseline(args.batch, args.size, args.cpu_steps, args.cpu_threads, args.width,
+                                            args.attention)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -71,23 +71,36 @@ __device__ void bn1_coef(const AttGateArgs& a, float& scale, float& shift, float
 
 }  // namespace
 
-// p[px] = psi.0(s[px]) = b + sum_c w[c] s[px][c]; BN(1) batch sums (training)
+// sum over the CC lanes of one pixel group (CC | 64, groups lane-aligned)
+__device__ __forceinline__ float group_sum(float v, int CC) {
+  for (int o = CC >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// p[px] = psi.0(s[px]) = b + sum_c w[c] s[px][c]; BN(1) batch sums (training).
+// CC = F_int/8 consecutive lanes share a pixel (one 16-B chunk each, so a
+// wave's loads are contiguous rows) and reduce the dot product by shuffles.
 __global__ void __launch_bounds__(256) att_psi_fwd_kernel(AttGateArgs a) {
   __shared__ double red[512];
   double ls = 0.0, lq = 0.0;
-  const int CC = a.Fi >> 3;
-  for (int64_t px = (int64_t)blockIdx.x * 256 + threadIdx.x; px < a.npix; px += (int64_t)gridDim.x * 256) {
-    float acc = a.psi_b[0];
-    const bf16_t* row = a.s + px * a.lds;
-    for (int c8 = 0; c8 < CC; ++c8) {
-      float v[8];
-      unpack8(*reinterpret_cast<const uint4*>(row + c8 * 8), v);
+  const int CC = a.Fi >> 3, ppb = 256 / CC;
+  const int chunk = threadIdx.x % CC, prow = threadIdx.x / CC;
+  float w[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc += v[k] * a.psi_w[c8 * 8 + k];
+  for (int k = 0; k < 8; ++k) w[k] = a.psi_w[chunk * 8 + k];
+  const float bias = a.psi_b[0];
+  for (int64_t px = (int64_t)blockIdx.x * ppb + prow; px < a.npix; px += (int64_t)gridDim.x * ppb) {
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4*>(a.s + px * a.lds + chunk * 8), v);
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += v[k] * w[k];
+    const float acc = group_sum(t, CC) + bias;
+    if (chunk == 0) {
+      a.p[px] = acc;
+      ls += acc;
+      lq += (double)acc * acc;
     }
-    a.p[px] = acc;
-    ls += acc;
-    lq += (double)acc * acc;
   }
   if (!a.training) return;
   block_sum2(ls, lq, red);
@@ -126,30 +139,33 @@ __global__ void __launch_bounds__(256) att_gate_fwd_kernel(AttGateArgs a) {
 }
 
 // backward, pass 1: d_psi = sum_c dXatt x; dZ = d_psi psi (1 - psi) (into
-// dbnp); dX (gate path) = dXatt psi; BN(1) sums (sum dZ, sum dZ phat)
+// dbnp); dX (gate path) = dXatt psi; BN(1) sums (sum dZ, sum dZ phat).
+// CC = F_l/8 lanes per pixel, as in att_psi_fwd_kernel.
 __global__ void __launch_bounds__(256) att_gate_bwd_reduce_kernel(AttGateArgs a) {
   __shared__ double red[512];
   const float mean = a.save[0], inv = a.save[1];
-  const int CC = a.Fl >> 3;
+  const int CC = a.Fl >> 3, ppb = 256 / CC;
+  const int chunk = threadIdx.x % CC, prow = threadIdx.x / CC;
   double s1 = 0.0, s2 = 0.0;
-  for (int64_t px = (int64_t)blockIdx.x * 256 + threadIdx.x; px < a.npix; px += (int64_t)gridDim.x * 256) {
+  for (int64_t px = (int64_t)blockIdx.x * ppb + prow; px < a.npix; px += (int64_t)gridDim.x * ppb) {
     const float ps = a.psi[px];
-    float dpsi = 0.f;
-    for (int c8 = 0; c8 < CC; ++c8) {
-      float d[8], v[8];
-      unpack8(*reinterpret_cast<const uint4*>(a.dxatt + px * a.lddxatt + c8 * 8), d);
-      unpack8(*reinterpret_cast<const uint4*>(a.x + px * a.ldx + c8 * 8), v);
+    float d[8], v[8];
+    unpack8(*reinterpret_cast<const uint4*>(a.dxatt + px * a.lddxatt + chunk * 8), d);
+    unpack8(*reinterpret_cast<const uint4*>(a.x + px * a.ldx + chunk * 8), v);
+    float t = 0.f;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        dpsi += d[k] * v[k];
-        d[k] *= ps;
-      }
-      *reinterpret_cast<uint4*>(a.dxpsi + px * a.lddxpsi + c8 * 8) = pack8(d);
+    for (int k = 0; k < 8; ++k) {
+      t += d[k] * v[k];
+      d[k] *= ps;
     }
-    const float dz = dpsi * ps * (1.f - ps);
-    a.dbnp[px] = dz;
-    s1 += dz;
-    s2 += (double)dz * ((a.p[px] - mean) * inv);
+    *reinterpret_cast<uint4*>(a.dxpsi + px * a.lddxpsi + chunk * 8) = pack8(d);
+    const float dpsi = group_sum(t, CC);
+    if (chunk == 0) {
+      const float dz = dpsi * ps * (1.f - ps);
+      a.dbnp[px] = dz;
+      s1 += dz;
+      s2 += (double)dz * ((a.p[px] - mean) * inv);
+    }
   }
   block_sum2(s1, s2, red);
   if (threadIdx.x == 0) {
@@ -398,11 +414,14 @@ static int grid_of(int64_t work, int cap = 2048) {
 }
 
 hipError_t launch_att_gate(const AttGateArgs& a, int pass, hipStream_t st) {
-  if (a.Fi % 8 || a.Fl % 8 || a.Fi / 8 > 256 || 256 % (a.Fi / 8) || a.npix <= 0) return hipErrorInvalidValue;
+  // lane groups of F/8 lanes per pixel must tile a wave
+  if (a.Fi % 8 || a.Fl % 8 || 64 % (a.Fi / 8) || 64 % (a.Fl / 8) || a.npix <= 0) return hipErrorInvalidValue;
   switch (pass) {
-    case 0: hipLaunchKernelGGL(att_psi_fwd_kernel, dim3(grid_of(a.npix)), dim3(256), 0, st, a); break;
+    case 0: hipLaunchKernelGGL(att_psi_fwd_kernel, dim3(grid_of(a.npix * (a.Fi / 8))), dim3(256), 0, st, a); break;
     case 1: hipLaunchKernelGGL(att_gate_fwd_kernel, dim3(grid_of(a.npix * (a.Fl / 8))), dim3(256), 0, st, a); break;
-    case 2: hipLaunchKernelGGL(att_gate_bwd_reduce_kernel, dim3(grid_of(a.npix)), dim3(256), 0, st, a); break;
+    case 2:
+      hipLaunchKernelGGL(att_gate_bwd_reduce_kernel, dim3(grid_of(a.npix * (a.Fl / 8))), dim3(256), 0, st, a);
+      break;
     case 3: {
       const int rows = 256 / (a.Fi / 8);
       const int g = (int)std::min<int64_t>(1024, (a.npix + rows * 8 - 1) / (rows * 8));

@@ -121,14 +121,16 @@ def test_train_epoch_evaluate_metrics(pkg, base, cuda):
         assert abs(v[k] - rv) <= (0.25 * abs(rv) if k == "loss" else 2e-2), (k, v[k], rv)
 
 
-def test_short_training_tracks_reference(pkg, cuda):
+@pytest.mark.parametrize("attention", [False, True], ids=["plain", "attention"])
+def test_short_training_tracks_reference(pkg, cuda, attention):
     """30 Adam steps on one synthetic batch: loss curves of the HIP path and the
-    fp32 oracle stay within 10 % and both fall."""
+    fp32 oracle stay within 10 % and both fall (with and without the attention
+    decoder)."""
     torch.manual_seed(0)
-    ref = oracle.ReferenceUNet()
+    ref = oracle.ReferenceUNet(use_attention=attention)
     sd = oracle.closed_form_state_dict(ref, seed=1)
     ref.load_state_dict(sd)
-    m = pkg.UNetWithBackbone(pretrained=False, use_attention=False)
+    m = pkg.UNetWithBackbone(pretrained=False, use_attention=attention)
     m.load_state_dict(sd)
     m = m.cuda()
     xs, ms = pkg.synthetic_cells(4, 128, 128, seed=77)
