@@ -115,18 +115,16 @@ __global__ void __launch_bounds__(256) att_psi_fwd_kernel(AttGateArgs a) {
 __global__ void __launch_bounds__(256) att_gate_fwd_kernel(AttGateArgs a) {
   float sc, sh, mean, inv, var;
   bn1_coef(a, sc, sh, mean, inv, var);
-  const int CC = a.Fl >> 3;
-  const int64_t total = a.npix * CC;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int64_t px = i / CC;
-    const int c8 = (int)(i - px * CC);
+  const int CC = a.Fl >> 3, ppb = 256 / CC;
+  const int chunk = threadIdx.x % CC, prow = threadIdx.x / CC;
+  for (int64_t px = (int64_t)blockIdx.x * ppb + prow; px < a.npix; px += (int64_t)gridDim.x * ppb) {
     const float ps = sigmoidf(a.p[px] * sc + sh);
-    if (c8 == 0) a.psi[px] = ps;
+    if (chunk == 0) a.psi[px] = ps;
     float v[8];
-    unpack8(*reinterpret_cast<const uint4*>(a.x + px * a.ldx + c8 * 8), v);
+    unpack8(*reinterpret_cast<const uint4*>(a.x + px * a.ldx + chunk * 8), v);
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] *= ps;
-    *reinterpret_cast<uint4*>(a.xatt + px * a.ldxatt + c8 * 8) = pack8(v);
+    *reinterpret_cast<uint4*>(a.xatt + px * a.ldxatt + chunk * 8) = pack8(v);
   }
   if (a.training && blockIdx.x == 0 && threadIdx.x == 0) {
     a.save[0] = mean;
@@ -299,19 +297,21 @@ __global__ void __launch_bounds__(256) ch_mlp_fwd_kernel(ChAttArgs a) {
   }
 }
 
-// out2 = y * gate[n][c]
+// out2 = y * gate[n][c]; grid (blocks, N), a thread keeps one 8-channel chunk
 __global__ void __launch_bounds__(256) ch_scale_kernel(ChAttArgs a) {
-  const int CC = a.C >> 3;
-  const int64_t total = (int64_t)a.N * a.HW * CC;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int64_t px = i / CC;
-    const int c8 = (int)(i - px * CC);
-    const int n = (int)(px / a.HW);
-    float v[8];
-    unpack8(*reinterpret_cast<const uint4*>(a.y + px * a.ldy + c8 * 8), v);
+  const int CC = a.C >> 3, rows = 256 / CC;
+  const int chunk = threadIdx.x % CC, row = threadIdx.x / CC;
+  const int n = blockIdx.y;
+  float g[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] *= a.gate[n * a.C + c8 * 8 + k];
-    *reinterpret_cast<uint4*>(a.out + px * a.ldo + c8 * 8) = pack8(v);
+  for (int k = 0; k < 8; ++k) g[k] = a.gate[n * a.C + chunk * 8 + k];
+  for (int64_t hw = (int64_t)blockIdx.x * rows + row; hw < a.HW; hw += (int64_t)gridDim.x * rows) {
+    const int64_t px = n * a.HW + hw;
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4*>(a.y + px * a.ldy + chunk * 8), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] *= g[k];
+    *reinterpret_cast<uint4*>(a.out + px * a.ldo + chunk * 8) = pack8(v);
   }
 }
 
@@ -381,25 +381,28 @@ __global__ void __launch_bounds__(256) ch_mlp_bwd_kernel(ChAttArgs a) {
   }
 }
 
-// dOut = dOut2 gate + davg / HW + [hw == argmax] dmax
+// dOut = dOut2 gate + davg / HW + [hw == argmax] dmax; layout as ch_scale_kernel
 __global__ void __launch_bounds__(256) ch_bwd_apply_kernel(ChAttArgs a) {
-  const int CC = a.C >> 3;
-  const int64_t total = (int64_t)a.N * a.HW * CC;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int64_t px = i / CC;
-    const int c8 = (int)(i - px * CC);
-    const int n = (int)(px / a.HW);
-    const unsigned hw = (unsigned)(px - (int64_t)n * a.HW);
-    float d[8];
-    unpack8(*reinterpret_cast<const uint4*>(a.dout2 + px * a.lddo2 + c8 * 8), d);
+  const int CC = a.C >> 3, rows = 256 / CC;
+  const int chunk = threadIdx.x % CC, row = threadIdx.x / CC;
+  const int n = blockIdx.y;
+  float g[8], da[8], dm[8];
+  unsigned arg[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int c = c8 * 8 + k;
-      float g = d[k] * a.gate[n * a.C + c] + a.dam[(size_t)n * 2 * a.C + c] * a.inv_hw;
-      if (key_index(a.pkey[n * a.C + c]) == hw) g += a.dam[(size_t)n * 2 * a.C + a.C + c];
-      d[k] = g;
-    }
-    *reinterpret_cast<uint4*>(a.dout + px * a.lddo + c8 * 8) = pack8(d);
+  for (int k = 0; k < 8; ++k) {
+    const int c = chunk * 8 + k;
+    g[k] = a.gate[n * a.C + c];
+    da[k] = a.dam[(size_t)n * 2 * a.C + c] * a.inv_hw;
+    dm[k] = a.dam[(size_t)n * 2 * a.C + a.C + c];
+    arg[k] = key_index(a.pkey[n * a.C + c]);
+  }
+  for (int64_t hw = (int64_t)blockIdx.x * rows + row; hw < a.HW; hw += (int64_t)gridDim.x * rows) {
+    const int64_t px = n * a.HW + hw;
+    float d[8];
+    unpack8(*reinterpret_cast<const uint4*>(a.dout2 + px * a.lddo2 + chunk * 8), d);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = d[k] * g[k] + da[k] + (arg[k] == (unsigned)hw ? dm[k] : 0.f);
+    *reinterpret_cast<uint4*>(a.dout + px * a.lddo + chunk * 8) = pack8(d);
   }
 }
 
@@ -438,6 +441,8 @@ hipError_t launch_ch_att(const ChAttArgs& a, int pass, hipStream_t st) {
   if ((int64_t)a.HW > 0xFFFFFFFEll) return hipErrorInvalidValue;
   const int rows = 256 / (a.C / 8);
   const int per_img = (int)std::min<int64_t>(64, (a.HW + rows * 16 - 1) / (rows * 16));
+  // elementwise passes: ~4 pixel rows per thread, <= 2048 blocks in total
+  const int ew_img = (int)std::max<int64_t>(1, std::min<int64_t>(2048 / a.N, (a.HW + rows * 4 - 1) / (rows * 4)));
   switch (pass) {
     case 0:
       hipLaunchKernelGGL(ch_pool_kernel, dim3(per_img, a.N), dim3(256), (size_t)rows * a.C * 12, st, a);
@@ -445,14 +450,14 @@ hipError_t launch_ch_att(const ChAttArgs& a, int pass, hipStream_t st) {
     case 1:
       hipLaunchKernelGGL(ch_mlp_fwd_kernel, dim3(a.N), dim3(256), (size_t)(2 * a.C + 2 * a.Cr) * sizeof(float), st, a);
       break;
-    case 2: hipLaunchKernelGGL(ch_scale_kernel, dim3(grid_of(a.N * a.HW * (a.C / 8))), dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL(ch_scale_kernel, dim3(ew_img, a.N), dim3(256), 0, st, a); break;
     case 3:
       hipLaunchKernelGGL(ch_bwd_reduce_kernel, dim3(per_img, a.N), dim3(256), (size_t)rows * a.C * sizeof(float), st, a);
       break;
     case 4:
       hipLaunchKernelGGL(ch_mlp_bwd_kernel, dim3(a.N), dim3(256), (size_t)(a.C + 2 * a.Cr) * sizeof(float), st, a);
       break;
-    case 5: hipLaunchKernelGGL(ch_bwd_apply_kernel, dim3(grid_of(a.N * a.HW * (a.C / 8))), dim3(256), 0, st, a); break;
+    case 5: hipLaunchKernelGGL(ch_bwd_apply_kernel, dim3(ew_img, a.N), dim3(256), 0, st, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
