@@ -179,37 +179,71 @@ __global__ void __launch_bounds__(256) att_gate_bwd_apply_kernel(AttGateArgs a) 
   extern __shared__ float wred[];  // [rows][Fi]
   const int CC = a.Fi >> 3, rows = 256 / CC;
   const int chunk = threadIdx.x % CC, row = threadIdx.x / CC;
+  const int c8 = chunk * 8;
   const float mean = a.save[0], inv = a.save[1];
   const double M = a.count;
   const float m1 = (float)(a.pbs[0] / M), m2 = (float)(a.pbs[1] / M);
   const float k1 = a.gamma[0] * inv;
-  float w[8], gw[8];
+  // fused: dS is stored as dZ = dS * (s > 0) and the BN_g / BN_x backward sums
+  // (sum dZ, sum dZ xhat_g, sum dZ xhat_x) are reduced here
+  const BnBwdArgs& bb = a.bb;
+  const bool fuse = bb.sums != nullptr;
+  float w[8], gw[8], s1[8], s2[8], t2[8], mu[8], is[8], mu2[8], is2[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    w[k] = a.psi_w[chunk * 8 + k];
-    gw[k] = 0.f;
+    w[k] = a.psi_w[c8 + k];
+    gw[k] = s1[k] = s2[k] = t2[k] = 0.f;
+    mu[k] = fuse ? bb.mean[c8 + k] : 0.f;
+    is[k] = fuse ? bb.invstd[c8 + k] : 0.f;
+    mu2[k] = fuse ? bb.mean2[c8 + k] : 0.f;
+    is2[k] = fuse ? bb.invstd2[c8 + k] : 0.f;
   }
   if (row < rows) {
     for (int64_t px = (int64_t)blockIdx.x * rows + row; px < a.npix; px += (int64_t)gridDim.x * rows) {
       const float phat = (a.p[px] - mean) * inv;
       const float dp = k1 * (a.dbnp[px] - m1 - phat * m2);
       float v[8], o[8];
-      unpack8(*reinterpret_cast<const uint4*>(a.s + px * a.lds + chunk * 8), v);
+      unpack8(*reinterpret_cast<const uint4*>(a.s + px * a.lds + c8), v);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         gw[k] += dp * v[k];
         o[k] = dp * w[k];
       }
-      *reinterpret_cast<uint4*>(a.dS + px * a.lddS + chunk * 8) = pack8(o);
-    }
+      if (fuse) {
+        float g[8], xa[8];
+        unpack8(*reinterpret_cast<const uint4*>(bb.y + px * bb.ldy + c8), g);
+        unpack8(*reinterpret_cast<const uint4*>(bb.y2 + px * bb.ldy2 + c8), xa);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) wred[row * a.Fi + chunk * 8 + k] = gw[k];
+        for (int k = 0; k < 8; ++k) {
+          o[k] = v[k] > 0.f ? o[k] : 0.f;
+          s1[k] += o[k];
+          s2[k] += o[k] * (g[k] - mu[k]) * is[k];
+          t2[k] += o[k] * (xa[k] - mu2[k]) * is2[k];
+        }
+      }
+      *reinterpret_cast<uint4*>(a.dS + px * a.lddS + c8) = pack8(o);
+    }
   }
-  __syncthreads();
-  for (int c = threadIdx.x; c < a.Fi; c += 256) {
-    float t = 0.f;
-    for (int r = 0; r < rows; ++r) t += wred[r * a.Fi + c];
-    atomicAdd(a.gpsi_w + c, t);
+  const int nq = fuse ? 4 : 1;
+  for (int q = 0; q < nq; ++q) {
+    const float* src = q == 0 ? gw : (q == 1 ? s1 : (q == 2 ? s2 : t2));
+    if (row < rows) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) wred[row * a.Fi + c8 + k] = src[k];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < a.Fi; c += 256) {
+      float t = 0.f;
+      for (int r = 0; r < rows; ++r) t += wred[r * a.Fi + c];
+      if (q == 0) {
+        atomicAdd(a.gpsi_w + c, t);
+      } else {
+        const size_t rep = (size_t)(blockIdx.x % kStatRep) * 2 * a.Fi;
+        double* dst = q == 1 ? bb.sums + rep : (q == 2 ? bb.sums + rep + a.Fi : bb.sums2 + rep + a.Fi);
+        atomicAdd(dst + c, (double)t);
+      }
+    }
+    __syncthreads();
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     a.ggamma[0] = (float)a.pbs[1];

@@ -1124,14 +1124,18 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     // (or enc4's) last BN
     if (att) {  // AttentionGate backward (skip gradient -> dskip, g-path gradient added into du)
       Att& t = p->atts[l];
-      const AttGateArgs a = gate_args(x, l, grads);
+      AttGateArgs a = gate_args(x, l, grads);
+      // relu(BN_g + BN_x) backward: its reduction runs inside the gate's apply
+      // pass (which produces dA and already reads the relu output)
+      a.bb = bwd_args(x, t.bng, t.dS, t.s, t.g1, t.dg1, t.bnx, &t.xa, &t.dxa, nullptr, grads);
+      a.bb.ticket = nullptr;  // the apply recomputes its coefficients from the sums
+      a.bb.coef = nullptr;
       {
         ProfScope ps(p, st, "att_gate_bwd", 0);
         CK(launch_att_gate(a, 2, st));
         CK(launch_att_gate(a, 3, st));
       }
-      RUN(bn_backward(x, t.bng, bwd_args(x, t.bng, t.dS, t.s, t.g1, t.dg1, t.bnx, &t.xa, &t.dxa, nullptr, grads),
-                      false));
+      RUN(bn_backward(x, t.bng, a.bb, true));
       RUN(fork());
       RUN(conv_wgrad(x, t.wg, t.dg1, d.up_out));
       RUN(conv_wgrad(x, t.wx, t.dxa, t.x));

@@ -209,6 +209,7 @@ struct AttGateArgs {
   bf16_t* dxpsi; int lddxpsi;          // gate-path skip gradient
   bf16_t* dS; int lddS;                // dA of relu(BN_g + BN_x)
   float* gpsi_w; float* ggamma; float* gbeta;
+  BnBwdArgs bb;                        // backward: relu(BN_g + BN_x) reduction fused into pass 3 (bb.sums != null)
   int64_t npix; int Fi, Fl;
 };
 struct ChAttArgs {

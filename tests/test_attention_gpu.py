@@ -129,7 +129,8 @@ def test_attention_ops_teacher_forced(run):
         xatt = xl * psi
         rows.append((ap + "x_att", _rel(v[p + "cat"][:, :skipc], xatt)))
         xatt.backward(dcat[:, :skipc])
-        rows += [(ap + "d.S", _rel(v[ap + "d.S"], st.grad)),
+        # stored as dZ of relu(BN_g + BN_x): dS masked by s > 0 (BN reduction fused)
+        rows += [(ap + "d.S", _rel(v[ap + "d.S"], st.grad * (v[ap + "s"] > 0).float())),
                  (f"g attention{lvl}.psi.0.weight", _rel(grads[f"attention{lvl}.psi.0.weight"], pw.grad)),
                  (f"g attention{lvl}.psi.1.weight", _rel(grads[f"attention{lvl}.psi.1.weight"], gm.grad)),
                  (f"g attention{lvl}.psi.1.bias", _rel(grads[f"attention{lvl}.psi.1.bias"], bt.grad))]

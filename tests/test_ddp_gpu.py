@@ -30,7 +30,8 @@ def _rel(a, b):
     return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()
 
 
-def test_bucketed_allreduce_rccl_world1(pkg, cuda):
+@pytest.mark.parametrize("attention", [False, True], ids=["plain", "attention"])
+def test_bucketed_allreduce_rccl_world1(pkg, cuda, attention):
     ddp = importlib.import_module("image-segmentation-project_amd.ddp")
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(_free_port())
@@ -41,7 +42,7 @@ def test_bucketed_allreduce_rccl_world1(pkg, cuda):
         x, y = torch.from_numpy(xs).to(dev), torch.from_numpy(ms).to(dev)
         crit = pkg.get_loss_function({"loss_fn": "bce"})
         torch.manual_seed(0)
-        m = pkg.UNetWithBackbone(pretrained=False, use_attention=False).to(dev).train()
+        m = pkg.UNetWithBackbone(pretrained=False, use_attention=attention).to(dev).train()
 
         def grads():
             for p in m.parameters():
