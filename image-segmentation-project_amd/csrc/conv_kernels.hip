@@ -1436,6 +1436,11 @@ static hipError_t launch_glds(const ConvFwdArgs& a, int classes, hipStream_t st)
   const bool bk64 = (a.C % 64) == 0;
   const long long M = (long long)a.N * a.Pc * a.Qc * classes;
   auto nblk = [&](long long bm, long long bn) { return ((M + bm - 1) / bm) * ((a.Cout + bn - 1) / bn); };
+  // attention-gate 1x1 convs (scripts/sweep_glds_cfg.sh --attention): the
+  // narrow full-resolution ones prefer 8-wave 256-pixel tiles (-25..-30 %)
+  const bool pw = a.R == 1 && a.S == 1 && a.stride == 1;
+  if (pw && a.Cout <= 32) return launch_glds_cfg<MODE, 256, 32, 32, 3, 8, 1>(a, classes, st);
+  if (pw && a.Cout == 64 && !bk64) return launch_glds_cfg<MODE, 256, 64, 32, 3, 4, 2>(a, classes, st);
   if (a.Cout <= 32) {
     return bk64 ? launch_glds_cfg<MODE, 128, 32, 64, 3, 4, 1>(a, classes, st)
                 : launch_glds_cfg<MODE, 128, 32, 32, 3, 4, 1>(a, classes, st);
