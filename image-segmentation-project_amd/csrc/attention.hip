@@ -415,28 +415,62 @@ __global__ void __launch_bounds__(256) ch_mlp_bwd_kernel(ChAttArgs a) {
   }
 }
 
-// dOut = dOut2 gate + davg / HW + [hw == argmax] dmax; layout as ch_scale_kernel
+// dOut = dOut2 gate + davg / HW + [hw == argmax] dmax; layout as ch_scale_kernel.
+// Fused (bb.sums): dOut is dA of the decoder's last BN + ReLU, so store
+// dZ = dOut * (out > 0) and reduce (sum dZ, sum dZ xhat) for its backward.
 __global__ void __launch_bounds__(256) ch_bwd_apply_kernel(ChAttArgs a) {
+  extern __shared__ float red[];  // [rows][C] (fused only)
   const int CC = a.C >> 3, rows = 256 / CC;
   const int chunk = threadIdx.x % CC, row = threadIdx.x / CC;
+  const int c8 = chunk * 8;
   const int n = blockIdx.y;
-  float g[8], da[8], dm[8];
+  const BnBwdArgs& bb = a.bb;
+  const bool fuse = bb.sums != nullptr;
+  float g[8], da[8], dm[8], mu[8], is[8], s1[8], s2[8];
   unsigned arg[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const int c = chunk * 8 + k;
+    const int c = c8 + k;
     g[k] = a.gate[n * a.C + c];
     da[k] = a.dam[(size_t)n * 2 * a.C + c] * a.inv_hw;
     dm[k] = a.dam[(size_t)n * 2 * a.C + a.C + c];
     arg[k] = key_index(a.pkey[n * a.C + c]);
+    mu[k] = fuse ? bb.mean[c] : 0.f;
+    is[k] = fuse ? bb.invstd[c] : 0.f;
+    s1[k] = s2[k] = 0.f;
   }
   for (int64_t hw = (int64_t)blockIdx.x * rows + row; hw < a.HW; hw += (int64_t)gridDim.x * rows) {
     const int64_t px = n * a.HW + hw;
     float d[8];
-    unpack8(*reinterpret_cast<const uint4*>(a.dout2 + px * a.lddo2 + chunk * 8), d);
+    unpack8(*reinterpret_cast<const uint4*>(a.dout2 + px * a.lddo2 + c8), d);
 #pragma unroll
     for (int k = 0; k < 8; ++k) d[k] = d[k] * g[k] + da[k] + (arg[k] == (unsigned)hw ? dm[k] : 0.f);
-    *reinterpret_cast<uint4*>(a.dout + px * a.lddo + chunk * 8) = pack8(d);
+    if (fuse) {
+      float act[8], y[8];
+      unpack8(*reinterpret_cast<const uint4*>(bb.act + px * bb.ldact + c8), act);
+      unpack8(*reinterpret_cast<const uint4*>(bb.y + px * bb.ldy + c8), y);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        d[k] = act[k] > 0.f ? d[k] : 0.f;
+        s1[k] += d[k];
+        s2[k] += d[k] * (y[k] - mu[k]) * is[k];
+      }
+    }
+    *reinterpret_cast<uint4*>(a.dout + px * a.lddo + c8) = pack8(d);
+  }
+  if (!fuse) return;
+  const size_t rep = (size_t)((blockIdx.y * gridDim.x + blockIdx.x) % kStatRep) * 2 * a.C;
+  for (int q = 0; q < 2; ++q) {
+    const float* src = q == 0 ? s1 : s2;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[row * a.C + c8 + k] = src[k];
+    __syncthreads();
+    for (int c = threadIdx.x; c < a.C; c += 256) {
+      float t = 0.f;
+      for (int r = 0; r < rows; ++r) t += red[r * a.C + c];
+      atomicAdd(bb.sums + rep + q * a.C + c, (double)t);
+    }
+    __syncthreads();
   }
 }
 
@@ -491,7 +525,10 @@ hipError_t launch_ch_att(const ChAttArgs& a, int pass, hipStream_t st) {
     case 4:
       hipLaunchKernelGGL(ch_mlp_bwd_kernel, dim3(a.N), dim3(256), (size_t)(a.C + 2 * a.Cr) * sizeof(float), st, a);
       break;
-    case 5: hipLaunchKernelGGL(ch_bwd_apply_kernel, dim3(ew_img, a.N), dim3(256), 0, st, a); break;
+    case 5:
+      hipLaunchKernelGGL(ch_bwd_apply_kernel, dim3(ew_img, a.N), dim3(256), a.bb.sums ? (size_t)rows * a.C * 4 : 0, st,
+                         a);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

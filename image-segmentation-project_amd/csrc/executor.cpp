@@ -1098,13 +1098,16 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
   // decoder1 .. decoder4 (+ their up-convs)
   for (int l = 3; l >= 0; --l) {
     Dec& d = p->decs[l];
-    if (att) {  // ChannelAttention backward: dOut2 -> dOut, then the unfused BN backward
-      const ChAttArgs c = ch_args(x, l, grads);
+    if (att) {  // ChannelAttention backward: dOut2 -> dZ of the decoder's last BN (its reduction fused)
+      ChAttArgs c = ch_args(x, l, grads);
+      c.bb = dec_bn2(l);
+      c.bb.ticket = nullptr;  // the apply recomputes its coefficients from the sums
+      c.bb.coef = nullptr;
       {
         ProfScope ps(p, st, "ch_att_bwd", 0);
         for (int pass = 3; pass < 6; ++pass) CK(launch_ch_att(c, pass, st));
       }
-      RUN(bn_backward(x, d.bn2, dec_bn2(l), false));
+      RUN(bn_backward(x, d.bn2, c.bb, true));
     } else {
       RUN(bn_backward(x, d.bn2, dec_bn2(l), fz));
     }

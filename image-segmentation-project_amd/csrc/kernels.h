@@ -222,6 +222,7 @@ struct ChAttArgs {
   float* dgate; float* dam;            // [N][C], [N][2][C]
   float* gw1; float* gw2;
   bf16_t* dout; int lddo;
+  BnBwdArgs bb;                        // backward: the decoder BN's reduction fused into pass 5 (bb.sums != null)
   float inv_hw;
   int64_t HW; int N, C, Cr;
 };

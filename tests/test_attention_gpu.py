@@ -162,7 +162,8 @@ def test_attention_ops_teacher_forced(run):
         o2 = cha(o)
         rows.append((ap + "out2", _rel(v[ap + "out2"], o2)))
         o2.backward(v[ap + "d.out2"])
-        rows.append((p + "d.out (ch-att bwd)", _rel(v[p + "d.out"], o.grad)))
+        # stored as dZ of the decoder's last BN + ReLU (its reduction is fused)
+        rows.append((p + "d.out (ch-att bwd)", _rel(v[p + "d.out"], o.grad * (v[p + "out"] > 0).float())))
         for k, q in cha.named_parameters():
             rows.append((f"g ch_attention{lvl}.{k}", _rel(grads[f"ch_attention{lvl}.{k}"], q.grad)))
     for name, e in rows:
