@@ -3,8 +3,11 @@
 (UNetWithBackbone resnet34, no attention, batch 16 per GPU), BASELINE.json
 configs[1] (N=1) / configs[2] (N>1, weak scaling, 16 per rank).
 
-python bench.py --gpus N --steps K --warmup W   (N>1: launched by torch.distributed.run)
-Prints ONE JSON line on rank 0.
+python bench.py --gpus N --steps K --warmup W
+N>1: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) every
+rank runs the step; started bare, the parent launches
+`python -m torch.distributed.run --nproc-per-node N` itself (before any GPU
+call) and exits with its return code.  Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
@@ -12,6 +15,7 @@ import argparse
 import importlib
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -73,6 +77,37 @@ def cpu_baseline(batch: int, h: int, steps: int, threads: int, width: int = 1, a
                       f"oracle/unet_ref.py on {threads} host threads"}
 
 
+def launch_ranks(n: int) -> int:
+    """Re-run this script as n ranks under torch.distributed.run (a child
+    process, never an exec: the parent has not touched the GPU)."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def miou_parity(model, x, y, width: int, attention: bool):
+    """North-star parity on the bench batch: foreground IoU of the HIP train-mode
+    forward vs the oracle (fp32 CPU restatement of the reference) on the same
+    weights and images, reference aggregation (utils.py:120-151)."""
+    import oracle
+    pkg = importlib.import_module("image-segmentation-project_amd")
+    ref = oracle.ReferenceUNet(width=width, use_attention=attention)
+    ref.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()})
+    ref.train()
+    with torch.no_grad():
+        out = model(x)
+        miou = pkg.calculate_metrics_from_logits(out, y)["iou"]
+        rl = ref(x.cpu())
+        miou_ref = oracle.calculate_metrics(torch.sigmoid(rl), y.cpu())["iou"]
+    return miou, miou_ref
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -86,7 +121,7 @@ def main():
                     help="channel multiplier: 1 = Base (configs[1]), 2 = Wide 128->1024 (configs[4], bf16 here)")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
-    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the CPU oracle legs (baseline + mIoU parity)")
     ap.add_argument("--graph", dest="graph", action="store_true", default=None,
                     help="replay the step as one HIP graph (default for --gpus 1)")
     ap.add_argument("--no-graph", dest="graph", action="store_false")
@@ -94,7 +129,11 @@ def main():
                     help="torch.optim.Adam (foreach) instead of the fused HIP Adam (optim.py)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -120,6 +159,11 @@ def main():
     x = torch.from_numpy(xs).to(dev)
     y = torch.from_numpy(ms).to(dev)
     model.train()
+    parity = None
+    if rank == 0 and not args.no_cpu_baseline:
+        parity = miou_parity(model, x, y, args.width, args.attention)  # step-0 weights, before any update
+    if world > 1:
+        dist.barrier()
 
     def eager_step():
         out = model(x)
@@ -157,7 +201,7 @@ def main():
     step_tflops = flops_step / (dt / args.steps) / 1e12
     # dominant kernel family (implicit-GEMM conv fwd/dgrad/wgrad): per-launch HIP
     # events around every launch of one eager step right after the timed region
-    plan = next(iter(model._plans.values()))
+    plan = model._last_plan
     torch.cuda.synchronize()
     plan.profile(True)
     eager_step()
@@ -193,6 +237,9 @@ def main():
         "dtype": "bf16",
         "data": "synthetic (Gaussian cells, seed 1234+rank), random-init weights",
         "miou": round(miou, 6),
+        "miou_step0": None if parity is None else round(parity[0], 6),
+        "miou_ref": None if parity is None else round(parity[1], 6),
+        "miou_abs_diff": None if parity is None else float(f"{abs(parity[0] - parity[1]):.3e}"),
         "config": {"workload": ("Base" if args.width == 1 else f"Wide (x{args.width} channels)")
                    + " U-Net resnet34 " + ("attention" if args.attention else "no-attention")
                    + " train step (fwd+bce+bwd+Adam)",

@@ -102,6 +102,8 @@ class _Plan:
         self.flops_train = lib.unet_plan_flops(handle, 1)
         self.flops_fwd = lib.unet_plan_flops(handle, 0)
         self.generation = 0
+        self.pins = 0  # GraphedTrainStep captures holding this plan's workspace
+        self.last_used = 0
 
     def profile(self, on: bool):
         _lib.check(self.lib.unet_profile_enable(self.handle, 1 if on else 0), "unet_profile_enable")
@@ -221,6 +223,8 @@ class UNetWithBackbone(nn.Module):
             self.ch_attention2 = _ChannelAttention(c0)
             self.ch_attention1 = _ChannelAttention(c0 // 2)
         self._plans = {}
+        self.max_plans = 3  # unpinned native plans (input shapes) kept alive
+        self._use_clock = 0
         self._ddp = None  # set by ddp.enable_data_parallel
 
     # ------------------------------------------------------------------ plumbing
@@ -228,6 +232,11 @@ class UNetWithBackbone(nn.Module):
         state = self.__dict__.copy()
         state["_plans"] = {}
         return state
+
+    @property
+    def _last_plan(self):
+        """The most recently used native plan (tests / profiling)."""
+        return max(self._plans.values(), key=lambda pl: pl.last_used)
 
     @property
     def _param_list(self):
@@ -247,8 +256,16 @@ class UNetWithBackbone(nn.Module):
             for p, s in zip(self._param_list, plan.param_shapes):
                 if tuple(p.shape) != s:
                     raise RuntimeError(f"parameter shape mismatch {tuple(p.shape)} vs {s}")
-            self._plans = {k: v for k, v in self._plans.items() if k[:3] == key[:3]}  # one live shape
+            # a small LRU of shapes (a ragged last batch or another val batch size
+            # must not rebuild the big plan every epoch); pinned plans (captured
+            # by a GraphedTrainStep) are never evicted
+            live = sorted((k for k, v in self._plans.items() if v.pins == 0),
+                          key=lambda k: self._plans[k].last_used)
+            while len(live) >= self.max_plans:
+                self._plans.pop(live.pop(0))
             self._plans[key] = plan
+        self._use_clock += 1
+        plan.last_used = self._use_clock
         return plan
 
     def _pointer_arrays(self):

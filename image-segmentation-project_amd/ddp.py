@@ -16,6 +16,7 @@ rank 0's running statistics (call it before evaluation / checkpointing).
 """
 from __future__ import annotations
 
+import weakref
 from typing import Callable, List, Optional, Sequence, Tuple
 
 import torch
@@ -52,6 +53,10 @@ class GradBucketReducer:
                 self._stream = torch.cuda.Stream(device=flat.device)
             comm = self._stream
             flat.record_stream(comm)
+            if wait_bucket is None:
+                # no per-bucket events (first DDP backward): the whole backward
+                # that wrote `flat` on the compute stream must finish first
+                comm.wait_stream(torch.cuda.current_stream(flat.device))
             with torch.cuda.stream(comm):
                 for b, (lo, hi) in enumerate(self.ranges):
                     if wait_bucket is not None:
@@ -73,13 +78,13 @@ class GradBucketReducer:
 class _NativeDDP:
     def __init__(self, group):
         self.group = group
-        self._reducers = {}
+        self._reducers = weakref.WeakKeyDictionary()  # one per live native plan (input shape)
 
     def reduce(self, plan, grads: torch.Tensor):
-        red = self._reducers.get(id(plan))
+        red = self._reducers.get(plan)
         if red is None:
             red = GradBucketReducer(plan.buckets, self.group)
-            self._reducers = {id(plan): red}
+            self._reducers[plan] = red
             # events are recorded from the NEXT backward on; order this one fully
             _lib.check(plan.lib.unet_plan_use_bucket_events(plan.handle, 1), "use_bucket_events")
             red.reduce(grads, None)
@@ -89,6 +94,31 @@ class _NativeDDP:
             _lib.check(plan.lib.unet_bucket_wait(plan.handle, b, stream.cuda_stream), "unet_bucket_wait")
 
         red.reduce(grads, wait)
+
+
+def plan_buckets(n: int = 1, h: int = 64, w: int = 64, width: int = 1, attention: bool = False):
+    """(parameter names, flat offsets, bucket ranges) of the native plan for this
+    topology, from the C ABI alone (plan creation needs no GPU)."""
+    import ctypes
+    lib = _lib.load()
+    cfg = _lib.UnetConfig(n, h, w, width, 1, 1e-5, 0.1, 1 if attention else 0)
+    handle = ctypes.c_void_p()
+    _lib.check(lib.unet_plan_create(ctypes.byref(cfg), ctypes.byref(handle)), "unet_plan_create")
+    try:
+        buf = ctypes.create_string_buffer(256)
+        names, offsets = [], []
+        for i in range(lib.unet_plan_num_params(handle)):
+            _lib.check(lib.unet_plan_param_name(handle, i, buf, 256), "param_name")
+            names.append(buf.value.decode())
+            offsets.append(lib.unet_plan_param_offset(handle, i))
+        b0, b1 = ctypes.c_int64(), ctypes.c_int64()
+        ranges = []
+        for b in range(lib.unet_plan_num_buckets(handle)):
+            _lib.check(lib.unet_plan_bucket_range(handle, b, ctypes.byref(b0), ctypes.byref(b1)), "bucket_range")
+            ranges.append((b0.value, b1.value))
+        return names, offsets, ranges
+    finally:
+        lib.unet_plan_destroy(handle)
 
 
 def broadcast_state(model: torch.nn.Module, group=None, src: int = 0):

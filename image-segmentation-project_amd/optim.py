@@ -16,11 +16,13 @@ moments) and one step is two launches of ``unet_adam_step``
   unchanged).  The U-Net's backward already returns every gradient as a view of
   one flat buffer in parameter order, so the step reads gradients in place;
   gradients laid out any other way are first gathered with ``torch.cat``.
-* The step counter is a device scalar shared by a group (``state[p]['step']``
-  is that tensor for every parameter of the group): the step is graph-capturable
-  (``capturable`` is always True).  Parameters whose ``.grad`` is None are
-  skipped like torch skips them; the group counter then still advances for the
-  others.
+* Step counters live on the device (graph-capturable; ``capturable`` is
+  always True).  While every parameter of a group has taken the same number of
+  steps they share one counter (``state[p]['step']`` is that tensor) and a step
+  is one launch over the group.  Parameters whose ``.grad`` is None are skipped
+  as torch skips them; from then on each parameter keeps its own counter (and
+  bias correction, exactly as torch's per-parameter ``state['step']``) and is
+  stepped by its own launch, until the counts agree again.
 * ``lr`` / ``weight_decay`` are read from ``param_groups`` at every call; under
   HIP-graph capture they are fixed at capture time.
 * ``amsgrad``, ``maximize`` and ``differentiable`` are not on the reference path
@@ -72,21 +74,37 @@ class _FlatGroup:
         self.m = torch.zeros(self.total, dtype=torch.float32, device=dev)
         self.v = torch.zeros(self.total, dtype=torch.float32, device=dev)
         self.coef = torch.zeros(3, dtype=torch.float32, device=dev)  # step, step_size, sqrt(bc2)
-        step0 = None
+        # per-parameter counters (used once the parameters' step counts differ)
+        self.pcoef = torch.zeros(len(params), 3, dtype=torch.float32, device=dev)
+        self.counts = []
         for p, o, n in zip(params, self.offsets, self.numels):  # carry over existing / loaded state
             st = state.get(p)
             if st and "exp_avg" in st:
                 self.m[o:o + n].copy_(st["exp_avg"].reshape(-1))
                 self.v[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
-                if step0 is None:
-                    step0 = float(st["step"])
-        if step0 is not None:
-            self.coef[0] = step0
-        self.step_t = self.coef[0]
-        for p, o, n in zip(params, self.offsets, self.numels):
-            state[p] = {"step": self.step_t, "exp_avg": self.m[o:o + n].view_as(p),
-                        "exp_avg_sq": self.v[o:o + n].view_as(p)}
+                self.counts.append(int(float(st["step"])))
+            else:
+                self.counts.append(0)
+        for i, (p, o, n) in enumerate(zip(params, self.offsets, self.numels)):
+            state[p] = {"exp_avg": self.m[o:o + n].view_as(p), "exp_avg_sq": self.v[o:o + n].view_as(p)}
+        self.state = state
+        self.uniform = None
+        self._set_mode(len(set(self.counts)) <= 1)
         self.gstage = None
+
+    def _set_mode(self, uniform: bool):
+        """uniform: one shared device counter; else one counter row per parameter."""
+        if uniform == self.uniform:
+            return
+        if uniform:
+            self.coef[0] = float(self.counts[0] if self.counts else 0)
+            for p in self.params:
+                self.state[p]["step"] = self.coef[0]
+        else:
+            self.pcoef[:, 0] = torch.tensor(self.counts, dtype=torch.float32)
+            for i, p in enumerate(self.params):
+                self.state[p]["step"] = self.pcoef[i, 0]
+        self.uniform = uniform
 
     def valid(self, params, state) -> bool:
         if len(params) != len(self.params) or any(a is not b for a, b in zip(params, self.params)):
@@ -148,7 +166,8 @@ class Adam(torch.optim.Optimizer):
             beta1, beta2 = group["betas"]
             lr, eps, wd = float(group["lr"]), float(group["eps"]), float(group["weight_decay"])
             stream = _lib.stream_handle(params[0].device)
-            if len(with_grad) == len(params):
+            full = len(with_grad) == len(params)
+            if full and fg.uniform:
                 grads = [p.grad for p in params]
                 if grads[0].storage_offset() >= 0 and _chain_ok(grads, grads[0]):
                     gptr = grads[0].data_ptr()
@@ -158,14 +177,17 @@ class Adam(torch.optim.Optimizer):
                 _lib.check(lib.unet_adam_step(fg.pflat.data_ptr(), gptr, fg.m.data_ptr(), fg.v.data_ptr(),
                                               fg.coef.data_ptr(), fg.total, lr, beta1, beta2, eps, wd, 1, stream),
                            "unet_adam_step")
-            else:  # torch skips parameters without gradients
-                _lib.check(lib.unet_adam_step(None, None, None, None, fg.coef.data_ptr(), 0, lr, beta1, beta2,
-                                              eps, wd, 1, stream), "unet_adam_step")
-                for p, o, n in zip(params, fg.offsets, fg.numels):
+                fg.counts = [c + 1 for c in fg.counts]
+            else:  # torch skips parameters without gradients; each keeps its own step count
+                fg._set_mode(False)
+                for i, (p, o, n) in enumerate(zip(params, fg.offsets, fg.numels)):
                     if p.grad is None:
                         continue
                     g = p.grad.contiguous()
                     _lib.check(lib.unet_adam_step(fg.pflat[o:].data_ptr(), g.data_ptr(), fg.m[o:].data_ptr(),
-                                                  fg.v[o:].data_ptr(), fg.coef.data_ptr(), n, lr, beta1, beta2,
-                                                  eps, wd, 0, stream), "unet_adam_step")
+                                                  fg.v[o:].data_ptr(), fg.pcoef[i].data_ptr(), n, lr, beta1,
+                                                  beta2, eps, wd, 1, stream), "unet_adam_step")
+                    fg.counts[i] += 1
+                if len(set(fg.counts)) == 1:
+                    fg._set_mode(True)
         return loss

@@ -97,6 +97,10 @@ class GraphedTrainStep:
         self.model, self.criterion, self.optimizer = model, criterion, optimizer
         self.x = images.clone()
         self.y = masks.clone()
+        # the captured kernels write this plan's workspace, events and side
+        # stream: keep it alive (and un-evictable) for the graph's lifetime
+        self._plan = model._plan_for(self.x)
+        self._plan.pins += 1
         for g in optimizer.param_groups:
             if not g.get("capturable", False):
                 raise ValueError("GraphedTrainStep needs an optimizer built with capturable=True")
@@ -120,6 +124,11 @@ class GraphedTrainStep:
         loss.backward()
         self.optimizer.step()
         return out, loss
+
+    def __del__(self):
+        plan = getattr(self, "_plan", None)
+        if plan is not None:
+            plan.pins -= 1
 
     def __call__(self, images=None, masks=None):
         if images is not None:

@@ -37,7 +37,7 @@ def step():
 for _ in range(3):
     step()
 torch.cuda.synchronize()
-plan = next(iter(m._plans.values()))
+plan = m._last_plan
 plan.profile(True)
 step()
 torch.cuda.synchronize()

@@ -52,7 +52,7 @@ def run(pkg, golden, cuda):
     loss = pkg.get_loss_function({"loss_fn": "bce"})(out, y.cuda())
     loss.backward()
     torch.cuda.synchronize()
-    plan = next(iter(m._plans.values()))
+    plan = m._last_plan
     v = {k: t.cpu() for k, t in plan.tensor_views().items()}
     grads = {k: p.grad.detach().cpu() for k, p in m.named_parameters()}
     bufs = {k: b.detach().cpu() for k, b in m.named_buffers()}

@@ -149,3 +149,27 @@ def test_synthetic_cells(pkg):
     assert set(np.unique(m)) <= {0.0, 1.0}
     x2, _ = pkg.synthetic_cells(2, 128, 128, seed=1234)
     assert np.array_equal(x, x2)
+
+
+def test_importable_alias_and_reference_layout_modules(pkg):
+    """`import image_segmentation_project_amd` and the reference's own flat module
+    names (dropin/advanced_models.py, losses.py, train.py, utils.py) resolve to
+    the same module objects as the hyphenated package."""
+    import sys
+    import image_segmentation_project_amd as amd
+    assert amd is pkg
+    from image_segmentation_project_amd.ddp import enable_data_parallel
+    assert enable_data_parallel is pkg.ddp.enable_data_parallel
+    sys.path.insert(0, os.path.join(REPO, "dropin"))
+    try:
+        for name, attrs in (("advanced_models", ["UNetWithBackbone"]),
+                            ("losses", ["get_loss_function", "BCELoss", "DiceLoss", "ComboLoss"]),
+                            ("train", ["train_epoch", "evaluate", "train_model", "quick_train"]),
+                            ("utils", ["calculate_metrics", "get_device", "EarlyStopping"])):
+            mod = importlib.import_module(name)
+            for a in attrs:
+                assert getattr(mod, a) is getattr(pkg, a), (name, a)
+    finally:
+        sys.path.remove(os.path.join(REPO, "dropin"))
+        for name in ("advanced_models", "losses", "train", "utils"):
+            sys.modules.pop(name, None)

@@ -6,7 +6,8 @@ reference; a random-init BN ResNet amplifies rounding with depth):
   train logits ||d||/||ref|| <= 0.10; masks agree on >= 95 % of pixels and are
   bit-exact where |logit_ref| > 1; BCE/Dice/Combo loss relative 1e-3;
   calculate_metrics of the HIP logits bit-exact vs. the oracle's aggregation of
-  the same logits; every gradient finite and one Adam step changes the loss.
+  the same logits, and within 1e-3 of the oracle's metrics on its own logits
+  (north-star mIoU bar); every gradient finite and one Adam step changes the loss.
 """
 import pytest
 import torch
@@ -55,6 +56,11 @@ def test_hires_1024_batch4_train_step(pkg, cuda):
     want = oracle.calculate_metrics(torch.sigmoid(lg), y)
     for k in want:
         assert got[k] == pytest.approx(want[k], abs=0.0, rel=1e-12), k
+    # north-star bar: mIoU of the HIP path within 1e-3 of the reference path's
+    want_ref = oracle.calculate_metrics(torch.sigmoid(ref_logits), y)
+    print(f"1024^2 IoU hip {got['iou']:.6f} ref {want_ref['iou']:.6f}")
+    for k in want_ref:
+        assert abs(got[k] - want_ref[k]) <= 1e-3, k
     loss = pkg.get_loss_function({"loss_fn": "bce"})(logits, y.cuda())
     opt.zero_grad()
     loss.backward()
