@@ -60,6 +60,10 @@ SIGNATURES = {
     "unet_conv_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]
                       + [c_int] * 12 + [c_void_p]),
     "unet_conv_wgrad": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p] + [c_int] * 12 + [c_void_p]),
+    "unet_conv_wgrad_slab": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int64]
+                             + [c_int] * 12 + [c_void_p]),
+    "unet_convt_wgrad_slab": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int64]
+                              + [c_int] * 5 + [c_void_p]),
     "unet_set_conv_config": (c_int, [c_int]),
     "unet_pack_weight": (c_int, [c_void_p, c_void_p] + [c_int] * 5 + [c_void_p]),
     "unet_unpack_grad": (c_int, [c_void_p, c_void_p] + [c_int] * 5 + [c_void_p]),

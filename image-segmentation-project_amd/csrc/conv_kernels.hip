@@ -822,9 +822,20 @@ conv_wgrad_kernel(ConvWgradArgs a) {
     if (kt + 1 < KT) store_tiles(buf ^ 1);
     __syncthreads();
   }
-  if (KT == 0) return;
+  if (a.slab && gridDim.z > 1) {  // this split's partial, register-native (SlabLayout SLAB_GEMM)
+    const size_t units = (size_t)gridDim.x * 4 * FM * FN * 64;
+    f32x4* dst = reinterpret_cast<f32x4*>(a.slab) + (size_t)blockIdx.z * units +
+                 ((size_t)blockIdx.x * 4 + wave) * (FM * FN * 64) + lane;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) dst[(i * FN + j) * 64] = acc[i][j];
+    return;
+  }
+  if (KT == 0 && !a.slab) return;
 
-  // D[co][c]: lane holds column c = .. + li, rows co = .. + 4g + e
+  // D[co][c]: lane holds column c = .. + li, rows co = .. + 4g + e.  One split
+  // with a slab: this block owns its dW tile (plain stores); else fp32 atomics
   const int Krow = (XLOAD == XLOAD_STEM) ? 64 : a.R * a.S * a.C;
   const int kcol0 = (XLOAD == XLOAD_STEM) ? 0 : tap * a.C;
 #pragma unroll
@@ -837,7 +848,11 @@ conv_wgrad_kernel(ConvWgradArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int co = co0 + wm * WTM + i * 16 + 4 * g + e;
-          if (co < a.Cout) atomicAdd(a.dw + (size_t)co * Krow + kcol0 + c, acc[i][j][e]);
+          if (co < a.Cout) {
+            float* d = a.dw + (size_t)co * Krow + kcol0 + c;
+            if (a.slab) *d = acc[i][j][e];
+            else atomicAdd(d, acc[i][j][e]);
+          }
         }
       }
     }
@@ -885,13 +900,20 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave & 1, wn = wave >> 1;  // wave tile 32 co x 16 ci
-  const int cob = blockIdx.x % a.co_blocks;
-  const int cib = blockIdx.x / a.co_blocks;
+  // 1-D grid of combos x splits, XCD-aware: the combos of one split (which
+  // share its dY rows and input halos) get consecutive logical ids, i.e. are
+  // dealt to one XCD and its L2
+  const int combos = a.co_blocks * a.c_blocks;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int combo = bid % combos, split = bid / combos;
+  const int cob = combo % a.co_blocks;
+  const int cib = combo / a.co_blocks;
   const int co0 = cob * (CO32 ? 32 : 64), c0 = cib * CI;
-  const int t0 = blockIdx.z * tiles_per_split;
+  const int t0 = split * tiles_per_split;
   const int t1 = min(tiles_total, t0 + tiles_per_split);
   const int KT = t1 - t0;
-  if (KT <= 0) return;
+  const int nsplit = gridDim.x / combos;
+  if (KT <= 0 && !(a.slab && nsplit > 1)) return;
   const int tq = a.Q / TW, tp = a.P / TH;
   const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, (unsigned)((size_t)a.N * a.P * a.Q * a.lddy * 2));
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
@@ -1005,11 +1027,21 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) acc[t][i] += red[(t * 2 + i) * 64];
   }
-  // epilogue: this split's partial dW[co][tap][ci] (plain stores into the
-  // slab) or fp32 atomics into dW
+  // epilogue: this split's partial in the register-native slab layout
+  // (SLAB_HALO: 18 fragments per wave, 16 B per lane per store), or -- one
+  // split -- the block's dW tile with plain stores, or fp32 atomics (no slab)
+  if (a.slab && nsplit > 1) {
+    const size_t units = (size_t)gridDim.x * NW * 18 * 64;
+    f32x4* dst = reinterpret_cast<f32x4*>(a.slab) + (size_t)split * units +
+                 ((size_t)combo * NW + wave) * (18 * 64) + lane;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) dst[(t * 2 + i) * 64] = acc[t][i];
+    return;
+  }
   const int Krow = 9 * a.C;
   const int c = c0 + wn * 16 + li;
-  float* slab = a.slab ? a.slab + (size_t)blockIdx.z * a.Cout * Krow : nullptr;
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
@@ -1018,28 +1050,69 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
       for (int e = 0; e < 4; ++e) {
         const int co = co0 + (CO32 ? 0 : wm * 32) + i * 16 + 4 * g + e;
         if (co < a.Cout) {
-          if (slab) slab[(size_t)co * Krow + t * a.C + c] = acc[t][i][e];
-          else atomicAdd(a.dw + (size_t)co * Krow + t * a.C + c, acc[t][i][e]);
+          float* d = a.dw + (size_t)co * Krow + t * a.C + c;
+          if (a.slab) *d = acc[t][i][e];
+          else atomicAdd(d, acc[t][i][e]);
         }
       }
 }
 
-// dW[i] (+)= sum of slab[s][i] over the 8 splits s = 8g .. 8g+7, g = blockIdx.y,
-// all 8 loads in flight at once.  gridDim.y > 1: fp32 atomics into the zeroed
-// dW (gridDim.y adds per element), one dword per lane so every wave
-// instruction covers 256 contiguous bytes (the full-rate atomic shape,
-// MI355X_MICROARCH.md "Global float atomics"); else a plain store.
-__global__ void __launch_bounds__(256) wgrad_slab_reduce_kernel(const float* __restrict__ slab, float* dw,
-                                                                int64_t n, int splits) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int s0 = blockIdx.y * 8;
-  float v[8];
+// dW index of element e of slab unit u (SlabLayout), -1 if that accumulator
+// lane holds no dW element (tile tails, the idle half of a CO32 block)
+__device__ __forceinline__ long long slab_dw_index(const SlabLayout& L, long long u, int e) {
+  const int lane = (int)(u & 63);
+  long long r = u >> 6;
+  const int frag = (int)(r % L.nf);
+  r /= L.nf;
+  const int wave = (int)(r % L.nw);
+  const int blk = (int)(r / L.nw);
+  const int g = lane >> 4, li = lane & 15;
+  if (L.kind == SLAB_HALO) {
+    const int t = frag >> 1, i = frag & 1, wm = wave & 1, wn = wave >> 1;
+    if (L.co32 && wm) return -1;
+    const int cob = blk % L.co_blocks, cib = blk / L.co_blocks;
+    const int co = cob * (L.co32 ? 32 : 64) + (L.co32 ? 0 : wm * 32) + i * 16 + 4 * g + e;
+    const int c = cib * L.ci + wn * 16 + li;
+    if (co >= L.Cout) return -1;
+    return (long long)co * L.Krow + t * L.C + c;
+  }
+  if (L.kind == SLAB_GEMM) {
+    const int i = frag / L.fn, j = frag % L.fn;
+    const int wm = wave % L.wm, wn = wave / L.wm;
+    const int cob = blk % L.co_blocks, rest = blk / L.co_blocks;
+    const int cblk = rest % L.c_blocks, tap = rest / L.c_blocks;
+    const int co = cob * L.bmo + wm * (L.bmo / L.wm) + i * 16 + 4 * g + e;
+    const int c = cblk * L.bnc + wn * (L.bnc / L.wn) + j * 16 + li;
+    if (c >= L.cmax || co >= L.Cout) return -1;
+    return (long long)co * L.Krow + (long long)tap * L.C + c;
+  }
+  // SLAB_STEM: one block per split, 4 waves of 32 co x 32 k
+  const int i = frag >> 1, j = frag & 1, wm = wave & 1, wn = wave >> 1;
+  return (long long)(wm * 32 + i * 16 + 4 * g + e) * 64 + wn * 32 + j * 16 + li;
+}
+
+// dW = sum over the splits of the slab, in split order (bit-reproducible),
+// four partial loads in flight per thread; every dW element is written once.
+__global__ void __launch_bounds__(256) wgrad_slab_reduce_kernel(const f32x4* __restrict__ slab,
+                                                                float* __restrict__ dw, SlabLayout L) {
+  const long long u = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (u >= L.units) return;
+  f32x4 acc = slab[u];
+  int k = 1;
+  for (; k + 4 <= L.splits; k += 4) {
+    const f32x4 a0 = slab[(long long)k * L.units + u], a1 = slab[(long long)(k + 1) * L.units + u];
+    const f32x4 a2 = slab[(long long)(k + 2) * L.units + u], a3 = slab[(long long)(k + 3) * L.units + u];
+    acc += a0;
+    acc += a1;
+    acc += a2;
+    acc += a3;
+  }
+  for (; k < L.splits; ++k) acc += slab[(long long)k * L.units + u];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) v[k] = s0 + k < splits ? slab[(size_t)(s0 + k) * n + i] : 0.f;
-  const float sum = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
-  if (gridDim.y == 1) dw[i] = sum;
-  else atomicAdd(dw + i, sum);
+  for (int e = 0; e < 4; ++e) {
+    const long long idx = slab_dw_index(L, u, e);
+    if (idx >= 0) dw[idx] = acc[e];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1307,6 +1380,14 @@ __global__ void __launch_bounds__(256, 2) stem_wgrad_kernel(ConvWgradArgs a, int
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
   }
+  if (a.slab && gridDim.x > 1) {  // one split per block (SLAB_STEM), summed by the reduce
+    f32x4* dst = reinterpret_cast<f32x4*>(a.slab) + (size_t)blockIdx.x * 1024 + (size_t)wave * 256 + lane;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) dst[(i * 2 + j) * 64] = acc[i][j];
+    return;
+  }
   // D[co][k]: lane holds k = .. + li, co = .. + 4g + e;  dW row length 64
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -1316,9 +1397,22 @@ __global__ void __launch_bounds__(256, 2) stem_wgrad_kernel(ConvWgradArgs a, int
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int co = wm * 32 + i * 16 + 4 * g + e;
-        atomicAdd(a.dw + co * 64 + k, acc[i][j][e]);
+        if (a.slab) a.dw[co * 64 + k] = acc[i][j][e];
+        else atomicAdd(a.dw + co * 64 + k, acc[i][j][e]);
       }
     }
+}
+
+// split-K partials of the last wgrad launch, summed by launch_wgrad_finish
+struct PendingReduce { const float* slab; float* dw; SlabLayout L; };
+static thread_local PendingReduce g_pending{};
+
+// largest split count whose register-native partials (bytes_per_split each)
+// fit the slab; 1 = no split-K reduction (each block owns its dW tile)
+static long long slab_split_cap(const ConvWgradArgs& a, long long bytes_per_split) {
+  if (!a.slab || bytes_per_split <= 0) return 1LL << 30;  // atomic path: no cap
+  const long long cap = (long long)(a.slab_bytes / (size_t)bytes_per_split);
+  return cap < 1 ? 1 : cap;
 }
 
 hipError_t launch_stem_fwd(const ConvFwdArgs& a, hipStream_t st) {
@@ -1334,10 +1428,20 @@ hipError_t launch_stem_fwd(const ConvFwdArgs& a, hipStream_t st) {
 hipError_t launch_stem_wgrad(const ConvWgradArgs& a, hipStream_t st) {
   if (a.Cout != 64 || a.R != 7 || a.stride != 2 || a.pad != 3) return hipErrorInvalidValue;
   const int rows = a.N * a.P * ((a.Q + 255) / 256);  // 256-pixel units
-  const int per = std::max(1, (rows + 511) / 512);  // ~2 blocks per CU
+  int per = std::max(1, (rows + 511) / 512);  // ~2 blocks per CU
+  // one register-native 64x64 partial (16 KiB) per block
+  const long long cap = slab_split_cap(a, 1024 * 16);
+  while ((rows + per - 1) / per > cap) ++per;
+  const int blocks = (rows + per - 1) / per;
   const size_t lds = 2 * 256 * 128 + 7 * kStemPatchW * 2;
   set_kernel_tag("stem_wgrad_kernel");
-  hipLaunchKernelGGL(stem_wgrad_kernel, dim3((rows + per - 1) / per), dim3(256), lds, st, a, per);
+  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(blocks), dim3(256), lds, st, a, per);
+  if (a.slab && blocks > 1) {
+    SlabLayout L = {};
+    L.kind = SLAB_STEM; L.splits = blocks; L.blocks = 1; L.nw = 4; L.nf = 4; L.units = 1024;
+    L.Cout = 64; L.C = 64; L.Krow = 64; L.cmax = 64;
+    g_pending = PendingReduce{a.slab, a.dw, L};
+  }
   return hipGetLastError();
 }
 
@@ -1557,6 +1661,10 @@ static hipError_t launch_wgrad_cfg(const ConvWgradArgs& a0, hipStream_t st) {
   const long long max_by_atomic = M / 512 > 0 ? M / 512 : 1;  // >= 512 px per block
   if (splits > max_by_atomic) splits = max_by_atomic;
   if (splits < 1) splits = 1;
+  constexpr int FM = BMO / WM / 16, FN = BNC / WN / 16;
+  const long long units = (long long)tiles * 4 * FM * FN * 64;
+  const long long cap = slab_split_cap(a, units * 16);
+  if (splits > cap) splits = cap;
   long long per = (M + splits - 1) / splits;
   per = (per + BKP - 1) / BKP * BKP;
   splits = (M + per - 1) / per;
@@ -1565,12 +1673,17 @@ static hipError_t launch_wgrad_cfg(const ConvWgradArgs& a0, hipStream_t st) {
   const size_t lds = 2 * (size_t)BKP * (BMO + BNC) * 2;
   set_kernel_tag("conv_wgrad_kernel<%d, %d, %d, %d, %d, %d>", XLOAD, BMO, BNC, BKP, WM, WN);
   hipLaunchKernelGGL((conv_wgrad_kernel<XLOAD, BMO, BNC, BKP, WM, WN>), grid, dim3(256), lds, st, a);
+  if (a.slab && splits > 1) {
+    SlabLayout L = {};
+    L.kind = SLAB_GEMM; L.splits = (int)splits; L.blocks = tiles; L.nw = 4; L.nf = FM * FN; L.units = units;
+    L.Cout = a.Cout; L.C = (XLOAD == XLOAD_STEM) ? 0 : a.C; L.Krow = (XLOAD == XLOAD_STEM) ? 64 : a.R * a.S * a.C;
+    L.cmax = ccount; L.co_blocks = a.co_blocks; L.c_blocks = a.c_blocks;
+    L.bmo = BMO; L.bnc = BNC; L.wm = WM; L.wn = WN; L.fn = FN;
+    g_pending = PendingReduce{a.slab, a.dw, L};
+  }
   return hipGetLastError();
 }
 
-// split-K partials of the last halo wgrad launch, summed by launch_wgrad_finish
-struct PendingReduce { const float* slab; float* dw; int64_t n; int splits; };
-static thread_local PendingReduce g_pending{};
 
 // splits so that the grid is ~one block per CU (the halo kernels hold 96-144 KB
 // of LDS), at least one tile per split
@@ -1591,15 +1704,27 @@ static hipError_t launch_wgrad_halo(const ConvWgradArgs& a0, hipStream_t st) {
   a.c_blocks = a.C / CI;
   int blocks_xy, tiles, per, splits;
   halo_geometry<TW, CI, CO32>(a, blocks_xy, tiles, per, splits);
-  const int64_t n = (int64_t)a.Cout * 9 * a.C;
-  if (a.slab && (size_t)splits * n * sizeof(float) > a.slab_bytes) a.slab = nullptr;  // atomics instead
+  constexpr int NW = CI / 8;
+  const long long units = (long long)blocks_xy * NW * 18 * 64;
+  const long long cap = slab_split_cap(a, units * 16);
+  if (splits > cap) {
+    splits = (int)cap;
+    per = (tiles + splits - 1) / splits;
+    splits = (tiles + per - 1) / per;
+  }
   constexpr int NS = CI == 64 ? 3 : 4;
   const size_t lds = (size_t)NS * (128 * 128 + 256 * CI * 2);
   if (CO32) set_kernel_tag("wgrad3x3_halo_kernel<%d, %d, %d, true>", TW, NS, CI);
   else set_kernel_tag("wgrad3x3_halo_kernel<%d, %d, %d>", TW, NS, CI);
-  hipLaunchKernelGGL((wgrad3x3_halo_kernel<TW, NS, CI, CO32>), dim3(blocks_xy, 1, splits), dim3(CI * 8), lds, st,
+  hipLaunchKernelGGL((wgrad3x3_halo_kernel<TW, NS, CI, CO32>), dim3(blocks_xy * splits), dim3(CI * 8), lds, st,
                      a, tiles, per);
-  if (a.slab) g_pending = PendingReduce{a.slab, a.dw, n, splits};
+  if (a.slab && splits > 1) {
+    SlabLayout L = {};
+    L.kind = SLAB_HALO; L.splits = splits; L.blocks = blocks_xy; L.nw = NW; L.nf = 18; L.units = units;
+    L.Cout = a.Cout; L.C = a.C; L.Krow = 9 * a.C; L.cmax = a.C;
+    L.co_blocks = a.co_blocks; L.c_blocks = a.c_blocks; L.ci = CI; L.co32 = CO32 ? 1 : 0;
+    g_pending = PendingReduce{a.slab, a.dw, L};
+  }
   return hipGetLastError();
 }
 
@@ -1609,10 +1734,10 @@ hipError_t launch_wgrad_finish(hipStream_t st) {
   if (!g_pending.slab) return hipSuccess;
   const PendingReduce r = g_pending;
   g_pending = PendingReduce{};
-  const int bx = (int)((r.n + 255) / 256);
-  const int G = (r.splits + 7) / 8;
+  const long long bx = (r.L.units + 255) / 256;
   set_kernel_tag("wgrad_slab_reduce_kernel");
-  hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3(bx, G), dim3(256), 0, st, r.slab, r.dw, r.n, r.splits);
+  hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)bx), dim3(256), 0, st,
+                     reinterpret_cast<const f32x4*>(r.slab), r.dw, r.L);
   return hipGetLastError();
 }
 

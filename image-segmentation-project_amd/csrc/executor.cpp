@@ -374,17 +374,20 @@ static int build_plan(unet_plan* p) {
   for (auto& cv : p->convs)
     if (cv.kind == L_CONVT) cv.bias_acc = A.take((size_t)kStatRep * cv.Co * sizeof(double));
   p->head_usum = A.take((size_t)(c0 / 2 * 4 + 1) * sizeof(double));
+  for (auto& t : p->atts) {
+    t.pbs = A.take(2 * sizeof(double));
+    t.cda = A.take((size_t)N * t.C * sizeof(float));
+  }
+  p->zero_bwd_bytes = A.top - p->zero_bwd_off;
+  // weight-gradient accumulators: every element is WRITTEN by its wgrad launch
+  // (deterministic split-K slab reduction, kernels.h SlabLayout), so they are
+  // not zeroed
   for (auto& cv : p->convs) {
     size_t n;
     if (cv.kind == L_STEM) n = (size_t)cv.Co * 64;
     else n = (size_t)cv.Co * cv.Ci * cv.R * cv.S;
     cv.wacc = A.take(n * sizeof(float));
   }
-  for (auto& t : p->atts) {
-    t.pbs = A.take(2 * sizeof(double));
-    t.cda = A.take((size_t)N * t.C * sizeof(float));
-  }
-  p->zero_bwd_bytes = A.top - p->zero_bwd_off;
   for (auto& b : p->bns) {
     b.save = A.take((size_t)2 * b.C * sizeof(float));
     b.ss = A.take((size_t)2 * b.C * sizeof(float));
@@ -407,8 +410,9 @@ static int build_plan(unet_plan* p) {
   p->y0 = act(A, N, H2, W2, c0);
   p->p0 = act(A, N, H4, W4, c0);
   p->pidx = A.take((size_t)N * H4 * W4 * c0);
-  // <= ~256 blocks x (64 co x 64 ci x 9 taps) fp32 partials, or one whole dW
-  p->wslab_bytes = (size_t)40 << 20;
+  // split-K partials of one weight-gradient launch (register-native layout);
+  // launchers cap their split count to what fits
+  p->wslab_bytes = (size_t)(64 * w * w) << 20;
   p->wslab = A.take(p->wslab_bytes);
   Act cats[4];  // cats[l] for decoder level index l (0 = level 4)
   cats[3] = cat1;
@@ -745,14 +749,13 @@ int conv_wgrad(const Ctx& x, int ci, const Act& dy, const Act& in) {
     a.H = dy.H; a.W = dy.W; a.C = 4 * cv.Co;
     a.P = in.H; a.Q = in.W; a.Cout = cv.Ci;
     CK(launch_convt_wgrad(a, x.wst));
-    return 0;
   } else {
     a.dy = x.A(dy); a.lddy = dy.ld;
     a.x = x.A(in); a.ldx = in.ld;
     a.H = in.H; a.W = in.W; a.C = cv.Ci;
     a.P = dy.H; a.Q = dy.W; a.Cout = cv.Co;
+    CK(launch_conv_wgrad(a, 0, x.wst));
   }
-  CK(launch_conv_wgrad(a, 0, x.wst));
   ps.close();
   if (wgrad_pending()) {
     ProfScope pr(x.p, x.wst, "wgrad_reduce " + pname(x, cv.w), 0);
@@ -1226,8 +1229,15 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     a.P = p->y0.H; a.Q = p->y0.W; a.Cout = cv.Co;
     a.R = 7; a.S = 7; a.stride = 2; a.pad = 3;
     a.x = reinterpret_cast<const bf16_t*>(image);
-    ProfScope ps(p, x.wst, "wgrad input_conv.weight", 2.0 * N * p->y0.H * p->y0.W * cv.Co * 49);
-    CK(launch_conv_wgrad(a, 1, x.wst));
+    a.slab = x.W<float>(p->wslab); a.slab_bytes = p->wslab_bytes;
+    {
+      ProfScope ps(p, x.wst, "wgrad input_conv.weight", 2.0 * N * p->y0.H * p->y0.W * cv.Co * 49);
+      CK(launch_conv_wgrad(a, 1, x.wst));
+    }
+    if (wgrad_pending()) {
+      ProfScope pr(p, x.wst, "wgrad_reduce input_conv.weight", 0);
+      CK(launch_wgrad_finish(x.wst));
+    }
   }
   RUN(unpack_bucket(x, 3, grads));
   if (p->nevents) CK(hipEventRecord(p->events[3], x.wst));
@@ -1425,6 +1435,33 @@ int unet_conv_wgrad(const void* dy, int lddy, const void* x, int ldx, float* dw_
   a.N = N; a.H = H; a.W = W; a.C = C; a.P = P; a.Q = Q; a.Cout = Cout;
   a.R = R; a.S = S; a.stride = stride; a.pad = pad;
   CK(launch_conv_wgrad(a, stem, stream));
+  return 0;
+}
+
+int unet_conv_wgrad_slab(const void* dy, int lddy, const void* x, int ldx, float* dw, void* slab,
+                         int64_t slab_bytes, int N, int H, int W, int C, int P, int Q, int Cout, int R, int S,
+                         int stride, int pad, int stem, hipStream_t stream) {
+  if (!slab || slab_bytes <= 0 || ((uintptr_t)slab & 15)) { set_err("unet_conv_wgrad_slab: bad slab"); return 1; }
+  ConvWgradArgs a = {};
+  a.dy = (const bf16_t*)dy; a.lddy = lddy; a.x = (const bf16_t*)x; a.ldx = ldx; a.dw = dw;
+  a.slab = (float*)slab; a.slab_bytes = (size_t)slab_bytes;
+  a.N = N; a.H = H; a.W = W; a.C = C; a.P = P; a.Q = Q; a.Cout = Cout;
+  a.R = R; a.S = S; a.stride = stride; a.pad = pad;
+  CK(launch_conv_wgrad(a, stem, stream));
+  CK(launch_wgrad_finish(stream));
+  return 0;
+}
+
+int unet_convt_wgrad_slab(const void* dy, int lddy, const void* x, int ldx, float* dw, void* slab,
+                          int64_t slab_bytes, int N, int H, int W, int Ci, int Co, hipStream_t stream) {
+  if (!slab || slab_bytes <= 0 || ((uintptr_t)slab & 15)) { set_err("unet_convt_wgrad_slab: bad slab"); return 1; }
+  ConvWgradArgs a = {};  // as the executor: "dy" := X [N,H,W,Ci], "x" := dY [N,2H,2W,Co]
+  a.dy = (const bf16_t*)x; a.lddy = ldx; a.x = (const bf16_t*)dy; a.ldx = lddy; a.dw = dw;
+  a.slab = (float*)slab; a.slab_bytes = (size_t)slab_bytes;
+  a.N = N; a.H = 2 * H; a.W = 2 * W; a.C = 4 * Co; a.P = H; a.Q = W; a.Cout = Ci;
+  a.R = 2; a.S = 2; a.stride = 2; a.pad = 0;
+  CK(launch_convt_wgrad(a, stream));
+  CK(launch_wgrad_finish(stream));
   return 0;
 }
 

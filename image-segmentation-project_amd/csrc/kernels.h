@@ -82,11 +82,31 @@ struct ConvFwdArgs {
   int mblocks, nblocks, Pc, Qc;  // filled by the launcher
 };
 
+// Split-K partials of the weight-gradient kernels ("register-native" slab):
+// every block stores its f32x4 accumulator fragments lane-contiguously (16 B
+// per lane, 1 KiB per wave instruction) at unit
+//   u = ((blk * nw + wave) * nf + frag) * 64 + lane     of split s: slab[s * units + u];
+// wgrad_slab_reduce_kernel sums the splits in a FIXED order (s = 0, 1, ...) and
+// scatters each unit's 4 values to dW [Cout][Krow]: deterministic, no atomics.
+enum { SLAB_HALO = 0, SLAB_GEMM = 1, SLAB_STEM = 2 };
+struct SlabLayout {
+  int kind, splits, blocks, nw, nf;
+  long long units;                 // f32x4 units per split
+  int Cout, C, Krow, cmax;         // dW geometry (cmax: valid reduction columns per tap)
+  int co_blocks, c_blocks;         // blk -> (co block, c block[, tap])
+  int bmo, bnc, wm, wn, fn;        // GEMM tile (BMO x BNC, WM x WN waves, FN column frags)
+  int ci, co32;                    // HALO: channels per block, 32-output-channel variant
+};
+
 struct ConvWgradArgs {
   const bf16_t* dy; int lddy;    // gradient wrt conv output [N,P,Q,Cout]
   const bf16_t* x; int ldx;      // conv input [N,H,W,C] (stem: fp32 image)
-  float* dw;                     // fp32 accumulator [Cout][R*S*C] (stem: [64][64])
-  float* slab; size_t slab_bytes; // optional split-K partial scratch (3x3 s1 halo path)
+  float* dw;                     // fp32 dW [Cout][R*S*C] (stem: [64][64])
+  // split-K partial scratch (16-B aligned).  With a slab every element of dW is
+  // WRITTEN (plain stores, deterministic split order; dW need not be zeroed);
+  // without one (single-op C ABI) the kernels add into a zeroed dW with fp32
+  // atomics.
+  float* slab; size_t slab_bytes;
   int N, H, W, C, P, Q, Cout, R, S, stride, pad;
   int px_per_split, co_blocks, c_blocks;  // filled by the launcher
 };
@@ -103,7 +123,8 @@ hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st);
 // ConvTranspose2d(k2,s2) weight gradient (XLOAD_SHUF): dy = X [N,P,Q,Ci] (Cout = Ci),
 // x = dY [N,H=2P,W=2Q,Co] with C = 4*Co; dw [Ci][4][Co]
 hipError_t launch_convt_wgrad(const ConvWgradArgs& a, hipStream_t st);
-// sums the split-K slab of the preceding launch_conv_wgrad into dW (no-op if it used atomics)
+// sums the split-K slab of the preceding launch_conv_wgrad into dW (no-op when
+// that launch needed no reduction: one split, or the atomic path)
 hipError_t launch_wgrad_finish(hipStream_t st);
 bool wgrad_pending();
 const char* last_kernel_tag();  // template instance of the last conv launch (profiler)

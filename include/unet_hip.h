@@ -116,6 +116,16 @@ int unet_conv_fwd(const void* x, int ldx, const void* w, void* y, int ldy, const
 int unet_conv_wgrad(const void* dy, int lddy, const void* x, int ldx, float* dw_acc, int N, int H,
                     int W, int C, int P, int Q, int Cout, int R, int S, int stride, int pad, int stem,
                     hipStream_t stream);
+/* the same with the executor's deterministic split-K: partials in the caller's
+ * 16-B aligned `slab` scratch, summed in a fixed split order; every element of
+ * dw is WRITTEN (no zeroing needed, bit-reproducible).  The convT form computes
+ * ConvTranspose2d(k2, s2) dW [Ci][Co][2][2]-packed as [Ci][4*Co] from
+ * x [N,H,W,Ci] and dy [N,2H,2W,Co]. */
+int unet_conv_wgrad_slab(const void* dy, int lddy, const void* x, int ldx, float* dw, void* slab,
+                         int64_t slab_bytes, int N, int H, int W, int C, int P, int Q, int Cout, int R,
+                         int S, int stride, int pad, int stem, hipStream_t stream);
+int unet_convt_wgrad_slab(const void* dy, int lddy, const void* x, int ldx, float* dw, void* slab,
+                          int64_t slab_bytes, int N, int H, int W, int Ci, int Co, hipStream_t stream);
 /* tile configuration of the implicit-GEMM conv kernels: 0 automatic (default),
  * >0 a fixed configuration from the tuning table (scripts/tune_conv.py) */
 int unet_set_conv_config(int cfg);

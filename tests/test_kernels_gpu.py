@@ -315,3 +315,101 @@ def test_maxpool_fwd_bwd(L, cuda, N, C, H):
                               N, H, H, C, S()) == 0
     torch.cuda.synchronize()
     close(nchw(dx), xr.grad + add.float())
+
+
+@pytest.mark.parametrize("N,C,H", [(2, 64, 32), (3, 64, 38)])
+def test_maxpool_bwd_inplace_addend_is_race_free(L, cuda, N, C, H):
+    """Aliasing pattern of the stem backward: dx written
+    IN PLACE over the addend (skip-concat gradient) buffer, every input row
+    gathered from the up-to-4 pooled windows that cover it.  Each dx element is
+    owned by exactly one thread (gather form, no scatter), so the result must
+    equal the out-of-place result bit for bit and be identical over repeated
+    launches (a cross-row or cross-block write would show up as a mismatch)."""
+    g = torch.Generator().manual_seed(11)
+    x = bf(torch.randn(N, C, H, H, generator=g)).relu()
+    xs = nhwc(x).cuda().contiguous()
+    P = (H - 1) // 2 + 1
+    y = torch.empty(N, P, P, C, dtype=torch.bfloat16, device="cuda")
+    idx = torch.empty(N, P, P, C, dtype=torch.uint8, device="cuda")
+    assert L.unet_maxpool_fwd(xs.data_ptr(), C, y.data_ptr(), idx.data_ptr(), N, H, H, C, S()) == 0
+    dyg = nhwc(bf(torch.randn(N, C, P, P, generator=g))).cuda()
+    addn = nhwc(bf(torch.randn(N, C, H, H, generator=g))).cuda()
+    out = torch.empty_like(addn)
+    assert L.unet_maxpool_bwd(dyg.data_ptr(), idx.data_ptr(), addn.data_ptr(), C, out.data_ptr(),
+                              N, H, H, C, S()) == 0
+    for _ in range(3):
+        inplace = addn.clone()
+        assert L.unet_maxpool_bwd(dyg.data_ptr(), idx.data_ptr(), inplace.data_ptr(), C, inplace.data_ptr(),
+                                  N, H, H, C, S()) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(inplace, out)
+
+
+SLAB_CASES = [  # N, Ci, H, Co, R, stride, pad, stem  -- every wgrad kernel family on its slab path
+    (8, 64, 128, 64, 3, 1, 1, 0),    # halo 64-channel blocks, many splits
+    (4, 32, 64, 32, 3, 1, 1, 0),     # halo CO32 (decoder1 shape)
+    (2, 96, 64, 32, 3, 1, 1, 0),     # halo 32-channel blocks, CO32
+    (2, 512, 16, 512, 3, 1, 1, 0),   # halo, one split (block owns its tile)
+    (2, 64, 32, 128, 3, 2, 1, 0),    # implicit-GEMM wgrad, stride 2
+    (2, 64, 32, 128, 1, 2, 0, 0),    # 1x1 downsample
+    (4, 1, 128, 64, 7, 2, 3, 1),     # 7x7 stem (one partial per block)
+]
+
+
+@pytest.mark.parametrize("case", SLAB_CASES)
+def test_conv_wgrad_slab_deterministic(L, case, cuda):
+    """The executor's weight-gradient path: split-K partials in a slab, summed
+    in split order.  dW starts as NaN (every element must be written), matches
+    torch at the wgrad tolerance, and two launches agree bit for bit."""
+    N, Ci, H, Co, R, st, pad, stem = case
+    g = torch.Generator().manual_seed(13)
+    P = (H + 2 * pad - R) // st + 1
+    dy = bf(torch.randn(N, Co, P, P, generator=g))
+    if stem:
+        img = torch.rand(N, 1, H, H, generator=g)
+        ref = torch.nn.grad.conv2d_weight(bf(img).float(), (Co, 1, 7, 7), dy.float(), stride=2, padding=3)
+        xg = img.cuda().contiguous()
+        ldx, n = 1, Co * 64
+    else:
+        x = bf(torch.randn(N, Ci, H, H, generator=g))
+        ref = torch.nn.grad.conv2d_weight(x.float(), (Co, Ci, R, R), dy.float(), stride=st, padding=pad)
+        xg = nhwc(x).cuda()
+        ldx, n = Ci, Co * R * R * Ci
+    dyg = nhwc(dy).cuda()
+    slab = torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
+    outs = []
+    for _ in range(2):
+        acc = torch.full((n,), float("nan"), dtype=torch.float32, device="cuda")
+        rc = L.unet_conv_wgrad_slab(dyg.data_ptr(), Co, xg.data_ptr(), ldx, acc.data_ptr(), slab.data_ptr(),
+                                    slab.numel(), N, H, H, Ci, P, P, Co, R, R, st, pad, stem, S())
+        assert rc == 0, L.unet_last_error()
+        out = torch.empty(Co, Ci, R, R, device="cuda")
+        assert L.unet_unpack_grad(acc.data_ptr(), out.data_ptr(), 2 if stem else 0, Co, Ci, R, R, S()) == 0
+        torch.cuda.synchronize()
+        assert torch.isfinite(out).all()
+        outs.append(out.cpu())
+    close(outs[0], ref, rel=2e-3)
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_convt_wgrad_slab_deterministic(L, cuda):
+    N, Ci, Co, H = 4, 64, 32, 64  # upconv1 shape class: many splits
+    g = torch.Generator().manual_seed(14)
+    x = bf(torch.randn(N, Ci, H, H, generator=g))
+    dy = bf(torch.randn(N, Co, 2 * H, 2 * H, generator=g))
+    w = torch.zeros(Ci, Co, 2, 2, requires_grad=True)
+    F.conv_transpose2d(x.float(), w, None, stride=2).backward(dy.float())
+    slab = torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
+    xg, dyg = nhwc(x).cuda(), nhwc(dy).cuda()
+    outs = []
+    for _ in range(2):
+        acc = torch.full((Ci * Co * 4,), float("nan"), dtype=torch.float32, device="cuda")
+        rc = L.unet_convt_wgrad_slab(dyg.data_ptr(), Co, xg.data_ptr(), Ci, acc.data_ptr(), slab.data_ptr(),
+                                     slab.numel(), N, H, H, Ci, Co, S())
+        assert rc == 0, L.unet_last_error()
+        out = torch.empty(Ci, Co, 2, 2, device="cuda")
+        assert L.unet_unpack_grad(acc.data_ptr(), out.data_ptr(), 1, Co, Ci, 2, 2, S()) == 0
+        torch.cuda.synchronize()
+        outs.append(out.cpu())
+    close(outs[0], w.grad, rel=2e-3)
+    assert torch.equal(outs[0], outs[1])
