@@ -130,7 +130,7 @@ struct TileEpi {
   uint2 uy2[TWO ? RW : 1][TWO ? FN : 1];  // raw conv output of the second BN (downsample pair)
 
   __device__ __forceinline__ void fetch(const ConvFwdArgs& a, const size_t (&pix)[RW], int co0, int lane) {
-    if (!FLIP) return;
+    if (!FLIP && !a.add) return;
     const BnBwdArgs& bb = a.bb;
     if (a.add) {  // conditions hoisted out of the loads (no per-load branch + wait)
 #pragma unroll
@@ -147,7 +147,7 @@ struct TileEpi {
 #pragma unroll
         for (int i = 0; i < FN; ++i) uadd[j][i] = make_uint2(0, 0);
     }
-    if (bb.sums) {
+    if (FLIP && bb.sums) {
 #pragma unroll
       for (int j = 0; j < RW; ++j)
 #pragma unroll
@@ -210,8 +210,22 @@ struct TileEpi {
         const int co = co0 + cl;
         const bool live = co < a.Cout;
         float v[4];
+        if (!FLIP && a.fold_on) {  // eval BN folded: (conv + bias) * scale + shift' (cst: shift' | scale)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = acc[j][i][e] + cst[cl + e];
+          for (int e = 0; e < 4; ++e) v[e] = acc[j][i][e] * cst[COT + cl + e] + cst[cl + e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[j][i][e] + cst[cl + e];
+        }
+        if (!FLIP && a.add) {  // forward residual, then the folded BN's ReLU
+          const uint2 u = uadd[j][i];
+          v[0] += __uint_as_float(u.x << 16); v[1] += __uint_as_float(u.x & 0xffff0000u);
+          v[2] += __uint_as_float(u.y << 16); v[3] += __uint_as_float(u.y & 0xffff0000u);
+        }
+        if (!FLIP && a.fold_relu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
         if (FLIP) {
           const uint2 u = uadd[j][i], m = uact[j][i];
           v[0] += __uint_as_float(u.x << 16); v[1] += __uint_as_float(u.x & 0xffff0000u);
@@ -284,6 +298,13 @@ __device__ __forceinline__ void load_epi_constants(const ConvFwdArgs& a, float* 
     const int co = co0 + c;
     const bool ok = co < a.Cout;
     cst[c] = (a.bias && ok) ? a.bias[co] : 0.f;
+    if (a.fold_on) {  // eval BN: shift' = bias * scale + shift, scale (running statistics)
+      float sc = 1.f, sh = 0.f, m, is, var;
+      if (ok) bn_scale_shift(a.fold, co, sc, sh, m, is, var);
+      cst[c] = cst[c] * sc + sh;
+      cst[COT + c] = sc;
+      continue;
+    }
     cst[COT + c] = (fbwd && ok) ? a.bb.mean[co] : 0.f;
     cst[2 * COT + c] = (fbwd && ok) ? a.bb.invstd[co] : 0.f;
     cst[3 * COT + c] = (two && ok) ? a.bb.mean2[co] : 0.f;
@@ -657,7 +678,9 @@ hipError_t launch_conv3x3_ws(const ConvFwdArgs& a, int mode, hipStream_t st) {
     return hipErrorNotSupported;
   if ((size_t)a.N * a.H * a.W * a.ldx * 2 >= 0x80000000ull) return hipErrorNotSupported;
   if ((size_t)a.Cout * 9 * a.C * 2 >= 0x80000000ull) return hipErrorNotSupported;
-  if (mode == 0 && (a.add || a.bb.sums)) return hipErrorNotSupported;  // forward epilogue: bias + BN sums only
+  // forward epilogue: bias, BN sums, or the eval-folded BN (+ residual addend, ReLU)
+  if (mode == 0 && (a.bb.sums || (a.add && !a.fold_on))) return hipErrorNotSupported;
+  if (mode == 1 && a.fold_on) return hipErrorNotSupported;
   return mode == 0 ? launch_halo_shape<false>(a, st) : launch_halo_shape<true>(a, st);
 }
 

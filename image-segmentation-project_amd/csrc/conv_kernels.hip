@@ -344,10 +344,22 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x4 (&acc)
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] += a.bias[co + e];
         }
+        if (a.fold_on) {  // eval BN folded into the epilogue (running statistics)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float sc, sh, m_, is_, var_;
+            bn_scale_shift(a.fold, co + e, sc, sh, m_, is_, var_);
+            v[e] = v[e] * sc + sh;
+          }
+        }
         if (a.add) {
           const uint2 u = *reinterpret_cast<const uint2*>(a.add + pix * a.ldadd + co);
           v[0] += __uint_as_float(u.x << 16); v[1] += __uint_as_float(u.x & 0xffff0000u);
           v[2] += __uint_as_float(u.y << 16); v[3] += __uint_as_float(u.y & 0xffff0000u);
+        }
+        if (a.fold_relu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
         }
         if (fbwd) {  // ReLU mask of the BN's forward output
           const uint2 u = *reinterpret_cast<const uint2*>(bb.act + pix * bb.ldact + co);
@@ -1031,7 +1043,7 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
   // (SLAB_HALO: 18 fragments per wave, 16 B per lane per store), or -- one
   // split -- the block's dW tile with plain stores, or fp32 atomics (no slab)
   if (a.slab && nsplit > 1) {
-    const size_t units = (size_t)gridDim.x * NW * 18 * 64;
+    const size_t units = (size_t)combos * NW * 18 * 64;  // per split (grid = combos x splits)
     f32x4* dst = reinterpret_cast<f32x4*>(a.slab) + (size_t)split * units +
                  ((size_t)combo * NW + wave) * (18 * 64) + lane;
 #pragma unroll
@@ -1579,6 +1591,7 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a0, int mode, hipStream_t st) {
   if (a0.ysplit && (!g_use_glds || mode == MODE_STEM || mode == MODE_SHUF || a0.csplit % 4 || a0.ldysplit % 4 ||
                     a0.bb.sums || a0.add))
     return hipErrorInvalidValue;
+  if (a0.fold_on && (mode != MODE_FWD || a0.stats || a0.bb.sums || !g_use_glds)) return hipErrorInvalidValue;
   // dedicated stem kernel: 64 output channels (Base); the Wide stem (128) takes
   // the generic implicit-GEMM path below
   if (g_use_glds && mode == MODE_STEM && a0.Cout == 64) return launch_stem_fwd(a0, st);

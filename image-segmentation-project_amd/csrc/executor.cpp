@@ -142,6 +142,8 @@ struct unet_plan {
   // kernel's last block, whose blocks must then drain their atomics and take a
   // ticket before exiting (UNET_BN_TICKET=1)
   bool bn_ticket = std::getenv("UNET_BN_TICKET") && std::getenv("UNET_BN_TICKET")[0] == '1';
+  // eval forward: BN folded into the conv epilogues (UNET_NO_EVAL_FOLD=1: separate BN passes, A/B only)
+  bool eval_fold = std::getenv("UNET_NO_EVAL_FOLD") == nullptr;
   double flops_fwd = 0, flops_train = 0;
   std::vector<std::pair<std::string, Act>> named;  // debug / test introspection
   // per-launch HIP-event profiler (unet_profile_*): one record per kernel
@@ -682,7 +684,11 @@ double conv_flops(const unet_plan* p, const Conv& cv, const Act& fwd_out) {
 }
 const std::string& pname(const Ctx& x, int param) { return x.p->params[param].name; }
 
-int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for_stats) {
+// fold_bn >= 0 (eval only): that BN (running statistics) is applied in the
+// conv epilogue, then `res` is added and ReLU applied (relu), so the BN pass
+// after the conv disappears (§8(f) row 4)
+int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for_stats, int fold_bn = -1,
+                 bool relu = false, const Act* res = nullptr) {
   const Conv& cv = x.p->convs[ci];
   ProfScope ps(x.p, x.st, "fwd " + pname(x, cv.w), conv_flops(x.p, cv, out));
   ConvFwdArgs a = {};
@@ -692,6 +698,13 @@ int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for
   a.bias = cv.b >= 0 ? x.prm[cv.b] : nullptr;
   a.stats = (bn_for_stats >= 0 && x.training) ? x.W<double>(x.p->bns[bn_for_stats].stats) : nullptr;
   if (a.stats) a.bn = bn_launch(x, bn_for_stats, (int64_t)x.p->cfg.N * out.H * out.W);
+  if (fold_bn >= 0) {
+    a.fold = bn_launch(x, fold_bn, (int64_t)x.p->cfg.N * out.H * out.W);
+    a.fold.training = 0;
+    a.fold_on = 1;
+    a.fold_relu = relu ? 1 : 0;
+    if (res) { a.add = x.A(*res); a.ldadd = res->ld; }
+  }
   a.N = x.p->cfg.N; a.H = in.H; a.W = in.W; a.C = cv.Ci;
   a.P = out.H; a.Q = out.W; a.Cout = cv.Co;
   a.R = cv.R; a.S = cv.S; a.stride = cv.stride; a.pad = cv.pad;
@@ -984,7 +997,16 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
       CK(launch_bn_relu_maxpool_fwd(m, st));
     }
   }
+  // eval: every BN of the encoder / decoder blocks folded into its conv's
+  // epilogue (running statistics; residual added there), no BN passes
+  const bool fold = !training && p->eval_fold;
   for (auto& b : p->blocks) {
+    if (fold) {
+      RUN(conv_forward(x, b.conv1, b.in, b.h, -1, b.bn1, true));
+      if (b.ds >= 0) RUN(conv_forward(x, b.ds, b.in, b.yds, -1, b.dsbn, false));
+      RUN(conv_forward(x, b.conv2, b.h, b.out, -1, b.bn2, true, b.ds >= 0 ? &b.yds : &b.in));
+      continue;
+    }
     RUN(conv_forward(x, b.conv1, b.in, b.y1, b.bn1));
     RUN(bn_apply(x, b.bn1, b.y1, b.h, 0, nullptr, -1, true));
     RUN(conv_forward(x, b.conv2, b.h, b.y2, b.bn2));
@@ -1000,10 +1022,15 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
     Dec& d = p->decs[l];
     RUN(conv_forward(x, d.up, d.up_in, d.up_out, -1));
     if (att) RUN(att_gate_forward(x, l));
-    RUN(conv_forward(x, d.conv1, d.cat, d.y1, d.bn1));
-    RUN(bn_apply(x, d.bn1, d.y1, d.h, 0, nullptr, -1, true));
-    RUN(conv_forward(x, d.conv2, d.h, d.y2, d.bn2));
-    RUN(bn_apply(x, d.bn2, d.y2, d.out, 0, nullptr, -1, true));
+    if (fold) {
+      RUN(conv_forward(x, d.conv1, d.cat, d.h, -1, d.bn1, true));
+      RUN(conv_forward(x, d.conv2, d.h, d.out, -1, d.bn2, true));
+    } else {
+      RUN(conv_forward(x, d.conv1, d.cat, d.y1, d.bn1));
+      RUN(bn_apply(x, d.bn1, d.y1, d.h, 0, nullptr, -1, true));
+      RUN(conv_forward(x, d.conv2, d.h, d.y2, d.bn2));
+      RUN(bn_apply(x, d.bn2, d.y2, d.out, 0, nullptr, -1, true));
+    }
     if (att) RUN(ch_att_forward(x, l));
   }
   {

@@ -76,6 +76,11 @@ struct ConvFwdArgs {
   // co - csplit] instead of y (a concat gradient whose narrow up-conv part is
   // kept in its own dense buffer so its consumers read whole cache lines)
   bf16_t* ysplit; int ldysplit; int csplit;
+  // eval-mode BatchNorm folded into the forward epilogue (fold_on != 0):
+  // y = act( (conv + bias) * scale + shift [+ add] ), scale/shift per output
+  // channel from the running statistics of `fold` (BnLaunch, training = 0);
+  // act = ReLU when fold_relu.  `add` (forward) is the block's residual.
+  BnLaunch fold; int fold_on; int fold_relu;
   int N, H, W, C;                // input geometry (C = GEMM reduction channels)
   int P, Q, Cout;                // output geometry
   int R, S, stride, pad;

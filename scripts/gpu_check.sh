@@ -1,5 +1,6 @@
 #!/bin/bash
-# Run GPU steps in order; stop at the first GPU fault/abort/timeout (rc not in {0,1}).
+# Run GPU steps in order; stop at the first failing step (a test failure can
+# be a GPU fault: start nothing more on the GPU after it).
 # usage: scripts/gpu_check.sh "<name>:<timeout>:<command>" ...
 mkdir -p gpurun_out
 for spec in "$@"; do
@@ -9,6 +10,6 @@ for spec in "$@"; do
   rc=$?
   echo "=== $name rc=$rc"
   tail -n 30 "gpurun_out/$name.log"
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP: $name rc=$rc"; exit $rc; fi
+  if [ $rc -ne 0 ]; then echo "STOP: $name rc=$rc"; exit $rc; fi
 done
 exit 0

@@ -129,3 +129,46 @@ def test_eval_after_training_teacher_forced(pkg, cuda):
     print(f"eval after 3 steps: logits rel {e:.3e}, IoU hip {got:.6f} ref {want:.6f}")
     assert e <= 0.05
     assert abs(got - want) <= IOU_TOL
+
+
+@pytest.mark.parametrize("attention", [False, True], ids=["plain", "attention"])
+def test_eval_bn_fold_matches_separate_bn_passes(pkg, cuda, monkeypatch, attention):
+    """§8(f) row 4: in eval mode every encoder/decoder BN (+ residual + ReLU) is
+    applied in its conv's epilogue from the running statistics.  Against the
+    unfused path (UNET_NO_EVAL_FOLD=1: conv, then a BN pass) on trained weights
+    and non-trivial running stats: relative L2 <= 1e-2 (the two round the
+    pre-BN activation to bf16 at different points), and the folded path stays
+    within the eval bar of the fp32 oracle."""
+    ref, m = _pair(pkg, attention, seed=6)
+    xs, ms = pkg.synthetic_cells(4, 128, 128, seed=9)
+    x, y = torch.from_numpy(xs), torch.from_numpy(ms)
+    xg, yg = x.cuda(), y.cuda()
+    crit = pkg.get_loss_function({"loss_fn": "bce"})
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    m.train()
+    for _ in range(2):
+        loss = crit(m(xg), yg)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m.eval()
+    with torch.no_grad():
+        folded = m(xg)
+    monkeypatch.setenv("UNET_NO_EVAL_FOLD", "1")
+    m2 = pkg.UNetWithBackbone(pretrained=False, use_attention=attention)
+    m2.load_state_dict(sd)
+    m2 = m2.cuda().eval()
+    with torch.no_grad():
+        plain = m2(xg)
+    ref.load_state_dict({k: v.cpu() for k, v in sd.items()})
+    ref.eval()
+    with torch.no_grad():
+        rl = ref(x)
+    e_fp, e_ref = _rel(folded, plain), _rel(folded, rl)
+    print(f"eval fold vs BN passes rel {e_fp:.3e}, vs oracle {e_ref:.3e} (BN passes vs oracle {_rel(plain, rl):.3e})")
+    assert e_fp <= 1e-2
+    assert e_ref <= 0.05
+    got = pkg.calculate_metrics_from_logits(folded, yg)["iou"]
+    want = oracle.calculate_metrics(torch.sigmoid(rl), y)["iou"]
+    assert abs(got - want) <= IOU_TOL
