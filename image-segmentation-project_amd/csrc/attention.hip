@@ -236,7 +236,7 @@ __global__ void __launch_bounds__(256) att_gate_bwd_apply_kernel(AttGateArgs a) 
       float t = 0.f;
       for (int r = 0; r < rows; ++r) t += wred[r * a.Fi + c];
       if (q == 0) {
-        atomicAdd(a.gpsi_w + c, t);
+        atomicAdd(a.gpsi_acc + (size_t)(blockIdx.x % kStatRep) * a.Fi + c, (double)t);
       } else {
         const size_t rep = (size_t)(blockIdx.x % kStatRep) * 2 * a.Fi;
         double* dst = q == 1 ? bb.sums + rep : (q == 2 ? bb.sums + rep + a.Fi : bb.sums2 + rep + a.Fi);
@@ -290,7 +290,7 @@ __global__ void __launch_bounds__(256) ch_pool_kernel(ChAttArgs a) {
       t += sred[r * a.C + c];
       kk = kk > kred[r * a.C + c] ? kk : kred[r * a.C + c];
     }
-    atomicAdd(a.psum + n * a.C + c, t);
+    atomicAdd(a.psum + n * a.C + c, (double)t);
     if (kk) atomicMax(a.pkey + n * a.C + c, kk);
   }
 }
@@ -304,7 +304,7 @@ __global__ void __launch_bounds__(256) ch_mlp_fwd_kernel(ChAttArgs a) {
   float* mv = sm + C;
   float* hh = sm + 2 * C;
   for (int c = threadIdx.x; c < C; c += 256) {
-    av[c] = a.psum[n * C + c] * a.inv_hw;
+    av[c] = (float)a.psum[n * C + c] * a.inv_hw;
     mv[c] = key_value(a.pkey[n * C + c]);
     a.am[(size_t)n * 2 * C + c] = av[c];
     a.am[(size_t)n * 2 * C + C + c] = mv[c];
@@ -373,7 +373,7 @@ __global__ void __launch_bounds__(256) ch_bwd_reduce_kernel(ChAttArgs a) {
   for (int c = threadIdx.x; c < a.C; c += 256) {
     float t = 0.f;
     for (int r = 0; r < rows; ++r) t += sred[r * a.C + c];
-    atomicAdd(a.dgate + n * a.C + c, t);
+    atomicAdd(a.dgate + n * a.C + c, (double)t);
   }
 }
 
@@ -388,7 +388,7 @@ __global__ void __launch_bounds__(256) ch_mlp_bwd_kernel(ChAttArgs a) {
   const float* am = a.am + (size_t)n * 2 * C;
   for (int c = threadIdx.x; c < C; c += 256) {
     const float g = a.gate[n * C + c];
-    dov[c] = a.dgate[n * C + c] * g * (1.f - g);
+    dov[c] = (float)a.dgate[n * C + c] * g * (1.f - g);
   }
   __syncthreads();
   for (int j = threadIdx.x; j < Cr; j += 256) {
@@ -398,10 +398,13 @@ __global__ void __launch_bounds__(256) ch_mlp_bwd_kernel(ChAttArgs a) {
     dh[Cr + j] = h[Cr + j] > 0.f ? t : 0.f;
   }
   __syncthreads();
+  // per-image weight-gradient terms, fp64 adds into replica n % kStatRep
+  // (summed and rounded to fp32 once by d2f: independent of the add order)
+  double* acc = a.gw_acc + (size_t)(n % kStatRep) * 2 * C * Cr;
   for (int i = threadIdx.x; i < C * Cr; i += 256) {
     const int c = i / Cr, j = i - c * Cr;
-    atomicAdd(a.gw2 + i, dov[c] * (h[j] + h[Cr + j]));           // W2 [C][Cr]
-    atomicAdd(a.gw1 + (size_t)j * C + c, dh[j] * am[c] + dh[Cr + j] * am[C + c]);  // W1 [Cr][C]
+    atomicAdd(acc + i, (double)(dov[c] * (h[j] + h[Cr + j])));                               // W2 [C][Cr]
+    atomicAdd(acc + C * Cr + (size_t)j * C + c, (double)(dh[j] * am[c] + dh[Cr + j] * am[C + c]));  // W1 [Cr][C]
   }
   for (int c = threadIdx.x; c < C; c += 256) {
     float ta = 0.f, tm = 0.f;
@@ -497,7 +500,8 @@ hipError_t launch_att_gate(const AttGateArgs& a, int pass, hipStream_t st) {
       const int rows = 256 / (a.Fi / 8);
       const int g = (int)std::min<int64_t>(1024, (a.npix + rows * 8 - 1) / (rows * 8));
       hipLaunchKernelGGL(att_gate_bwd_apply_kernel, dim3(g), dim3(256), (size_t)rows * a.Fi * sizeof(float), st, a);
-      break;
+      if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
+      return launch_d2f(a.gpsi_acc, a.gpsi_w, a.Fi, st);
     }
     default: return hipErrorInvalidValue;
   }
@@ -522,9 +526,16 @@ hipError_t launch_ch_att(const ChAttArgs& a, int pass, hipStream_t st) {
     case 3:
       hipLaunchKernelGGL(ch_bwd_reduce_kernel, dim3(per_img, a.N), dim3(256), (size_t)rows * a.C * sizeof(float), st, a);
       break;
-    case 4:
+    case 4: {
       hipLaunchKernelGGL(ch_mlp_bwd_kernel, dim3(a.N), dim3(256), (size_t)(a.C + 2 * a.Cr) * sizeof(float), st, a);
-      break;
+      if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
+      // d2f sums kStatRep replicas of stride n: run it over the [2][C*Cr] pair as one array
+      // and split the result into fc.2 and fc.0 -- they are separate tensors, so two launches
+      const int n2 = a.C * a.Cr;
+      hipError_t e = launch_d2f_strided(a.gw_acc, a.gw2, n2, 2 * n2, st);
+      if (e != hipSuccess) return e;
+      return launch_d2f_strided(a.gw_acc + n2, a.gw1, n2, 2 * n2, st);
+    }
     case 5:
       hipLaunchKernelGGL(ch_bwd_apply_kernel, dim3(ew_img, a.N), dim3(256), a.bb.sums ? (size_t)rows * a.C * 4 : 0, st,
                          a);

@@ -949,15 +949,18 @@ hipError_t launch_channel_sum(const bf16_t* x, int ldx, int64_t npix, int C, dou
 }
 
 // dst[i] = sum of the kStatRep replicas src[r][i]
-__global__ void d2f_kernel(const double* s, float* d, int n) {
+__global__ void d2f_kernel(const double* s, float* d, int n, int stride) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   double v = 0.0;
-  for (int r = 0; r < kStatRep; ++r) v += s[(size_t)r * n + i];
+  for (int r = 0; r < kStatRep; ++r) v += s[(size_t)r * stride + i];
   d[i] = (float)v;
 }
 hipError_t launch_d2f(const double* src, float* dst, int n, hipStream_t st) {
-  hipLaunchKernelGGL(d2f_kernel, dim3((n + 255) / 256), dim3(256), 0, st, src, dst, n);
+  return launch_d2f_strided(src, dst, n, n, st);
+}
+hipError_t launch_d2f_strided(const double* src, float* dst, int n, int stride, hipStream_t st) {
+  hipLaunchKernelGGL(d2f_kernel, dim3((n + 255) / 256), dim3(256), 0, st, src, dst, n, stride);
   return hipGetLastError();
 }
 

@@ -92,9 +92,10 @@ struct Att {
   size_t pst = 0, pbs = 0, psave = 0;  // fp64 [2] fwd sums, fp64 [2] bwd sums, fp32 mean|invstd
   Act dS, dg1, dxa, dxpsi, dskip, du;  // gradients (du = up-conv output grad incl. the W_g path)
   Act out2, d_out2;                    // decoder output * channel gate, and its gradient
-  size_t psum = 0, pkey = 0;           // fp32 [N][C] pooled sums, u64 [N][C] (max, first index) keys
+  size_t psum = 0, pkey = 0;           // fp64 [N][C] pooled sums, u64 [N][C] (max, first index) keys
   size_t ca = 0, ch = 0, cam = 0;      // fp32 gate [N][C], hidden [N][2][Cr], avg|max [N][2][C]
-  size_t cda = 0, cdam = 0;            // fp32 dL/dgate [N][C], dL/d(avg|max) [N][2][C]
+  size_t cda = 0, cdam = 0;            // fp64 dL/dgate [N][C], fp32 dL/d(avg|max) [N][2][C]
+  size_t gpsi = 0, gfc = 0;            // fp64 replica partials of the psi / fc.2|fc.0 weight gradients
 };
 
 }  // namespace unet
@@ -363,7 +364,7 @@ static int build_plan(unet_plan* p) {
   for (int l = 0; l < (int)p->atts.size(); ++l) {
     Att& t = p->atts[l];
     t.pst = A.take(2 * sizeof(double));
-    t.psum = A.take((size_t)N * t.C * sizeof(float));
+    t.psum = A.take((size_t)N * t.C * sizeof(double));
     t.pkey = A.take((size_t)N * t.C * sizeof(unsigned long long));
   }
   p->zero_fwd_bytes = A.top - p->zero_fwd_off;
@@ -378,7 +379,9 @@ static int build_plan(unet_plan* p) {
   p->head_usum = A.take((size_t)(c0 / 2 * 4 + 1) * sizeof(double));
   for (auto& t : p->atts) {
     t.pbs = A.take(2 * sizeof(double));
-    t.cda = A.take((size_t)N * t.C * sizeof(float));
+    t.cda = A.take((size_t)N * t.C * sizeof(double));
+    t.gpsi = A.take((size_t)kStatRep * t.Fi * sizeof(double));
+    t.gfc = A.take((size_t)kStatRep * 2 * t.C * t.Cr * sizeof(double));
   }
   p->zero_bwd_bytes = A.top - p->zero_bwd_off;
   // weight-gradient accumulators: every element is WRITTEN by its wgrad launch
@@ -886,6 +889,7 @@ AttGateArgs gate_args(const Ctx& x, int l, float* grads) {
   a.dS = x.A(t.dS); a.lddS = t.dS.ld;
   if (grads) {
     a.gpsi_w = grads + p->params[t.psi_w].flat;
+    a.gpsi_acc = x.W<double>(t.gpsi);
     a.ggamma = grads + p->params[b.gamma].flat;
     a.gbeta = grads + p->params[b.beta].flat;
   }
@@ -900,11 +904,12 @@ ChAttArgs ch_args(const Ctx& x, int l, float* grads) {
   ChAttArgs c = {};
   c.y = x.A(d.out); c.ldy = d.out.ld;
   c.out = x.A(t.out2); c.ldo = t.out2.ld;
-  c.psum = x.W<float>(t.psum); c.pkey = x.W<unsigned long long>(t.pkey);
+  c.psum = x.W<double>(t.psum); c.pkey = x.W<unsigned long long>(t.pkey);
+  c.gw_acc = x.W<double>(t.gfc);
   c.w1 = x.prm[t.fc1]; c.w2 = x.prm[t.fc2];
   c.am = x.W<float>(t.cam); c.h = x.W<float>(t.ch); c.gate = x.W<float>(t.ca);
   c.dout2 = x.A(t.d_out2); c.lddo2 = t.d_out2.ld;
-  c.dgate = x.W<float>(t.cda); c.dam = x.W<float>(t.cdam);
+  c.dgate = x.W<double>(t.cda); c.dam = x.W<float>(t.cdam);
   if (grads) {
     c.gw1 = grads + p->params[t.fc1].flat;
     c.gw2 = grads + p->params[t.fc2].flat;
@@ -1080,9 +1085,6 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
   auto fork = [&]() { return stream_edge(p, st, x.wst); };
   CK(hipMemsetAsync(ws + p->zero_bwd_off, 0, p->zero_bwd_bytes, st));
   const bool att = !p->atts.empty();
-  for (auto& t : p->atts)  // gradients accumulated with atomics
-    for (int pi : {t.psi_w, t.fc1, t.fc2})
-      CK(hipMemsetAsync(grads + p->params[pi].flat, 0, sizeof(float) * p->params[pi].numel, st));
   // head (upconv0 + conv_final)
   {
     const Act& o = att ? p->atts[3].out2 : p->decs[3].out;

@@ -193,6 +193,8 @@ hipError_t launch_head_grads(const HeadArgs& a, hipStream_t st);
 hipError_t launch_channel_sum(const bf16_t* x, int ldx, int64_t npix, int C, double* acc,
                               hipStream_t st);
 hipError_t launch_d2f(const double* src, float* dst, int n, hipStream_t st);
+// the same over replicas `stride` elements apart (src[r * stride + i], r < kStatRep)
+hipError_t launch_d2f_strided(const double* src, float* dst, int n, int stride, hipStream_t st);
 
 // weight (un)packing between torch fp32 layouts and kernel bf16 layouts
 enum { PK_CONV_FWD = 0, PK_CONV_DGRAD = 1, PK_CONVT_FWD = 2, PK_CONVT_DGRAD = 3, PK_STEM = 4 };
@@ -235,18 +237,20 @@ struct AttGateArgs {
   bf16_t* dxpsi; int lddxpsi;          // gate-path skip gradient
   bf16_t* dS; int lddS;                // dA of relu(BN_g + BN_x)
   float* gpsi_w; float* ggamma; float* gbeta;
+  double* gpsi_acc;                    // fp64 [kStatRep][Fi] psi-weight gradient partials (zeroed; -> gpsi_w)
   BnBwdArgs bb;                        // backward: relu(BN_g + BN_x) reduction fused into pass 3 (bb.sums != null)
   int64_t npix; int Fi, Fl;
 };
 struct ChAttArgs {
   const bf16_t* y; int ldy;            // decoder output
   bf16_t* out; int ldo;                // y * gate
-  float* psum; unsigned long long* pkey;
+  double* psum; unsigned long long* pkey;   // fp64 pooled sums (zeroed): order-independent to far below fp32
   const float* w1; const float* w2;    // fc.0 [Cr][C], fc.2 [C][Cr]
   float* am; float* h; float* gate;    // avg|max [N][2][C], hidden [N][2][Cr], gate [N][C]
   const bf16_t* dout2; int lddo2;
-  float* dgate; float* dam;            // [N][C], [N][2][C]
+  double* dgate; float* dam;           // fp64 [N][C] (zeroed), [N][2][C]
   float* gw1; float* gw2;
+  double* gw_acc;                      // fp64 [kStatRep][2][C*Cr] fc.2 | fc.0 gradient partials (zeroed)
   bf16_t* dout; int lddo;
   BnBwdArgs bb;                        // backward: the decoder BN's reduction fused into pass 5 (bb.sums != null)
   float inv_hw;

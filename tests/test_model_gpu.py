@@ -221,13 +221,15 @@ def test_base_512_step_properties(pkg, cuda):
         assert torch.isfinite(p.grad).all(), k
 
 
-def test_backward_is_bit_reproducible(pkg, cuda):
+@pytest.mark.parametrize("attention", [False, True], ids=["plain", "attention"])
+def test_backward_is_bit_reproducible(pkg, cuda, attention):
     """Two backward passes of the same step give bit-identical gradients: every
     weight gradient is a split-K partial slab summed in a fixed split order
-    (no fp32 atomics); BN / loss sums are fp64 accumulations of fp32 partials,
-    exact to far below the fp32 result they round to."""
+    (no fp32 atomics); BN / loss / attention pooling sums are fp64
+    accumulations of fp32 partials, exact to far below the fp32 result they
+    round to."""
     torch.manual_seed(0)
-    m = pkg.UNetWithBackbone(pretrained=False, use_attention=False).cuda().train()
+    m = pkg.UNetWithBackbone(pretrained=False, use_attention=attention).cuda().train()
     xs, ms = pkg.synthetic_cells(4, 128, 128, seed=12)
     x, y = torch.from_numpy(xs).cuda(), torch.from_numpy(ms).cuda()
     crit = pkg.get_loss_function({"loss_fn": "bce"})
