@@ -1103,23 +1103,34 @@ __device__ __forceinline__ long long slab_dw_index(const SlabLayout& L, long lon
   return (long long)(wm * 32 + i * 16 + 4 * g + e) * 64 + wn * 32 + j * 16 + li;
 }
 
-// dW = sum over the splits of the slab, in split order (bit-reproducible),
-// four partial loads in flight per thread; every dW element is written once.
+// dW = sum over the splits of the slab, bit-reproducible: T threads share one
+// unit (T | 256, T <= 64), thread r sums splits r, r+T, r+2T, ... in that order
+// (four loads in flight), then the T partials are added in r order through
+// LDS; the partition and both orders are fixed, so the result does not depend
+// on timing.  Every dW element is written once (plain stores).
 __global__ void __launch_bounds__(256) wgrad_slab_reduce_kernel(const f32x4* __restrict__ slab,
-                                                                float* __restrict__ dw, SlabLayout L) {
-  const long long u = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (u >= L.units) return;
-  f32x4 acc = slab[u];
-  int k = 1;
-  for (; k + 4 <= L.splits; k += 4) {
-    const f32x4 a0 = slab[(long long)k * L.units + u], a1 = slab[(long long)(k + 1) * L.units + u];
-    const f32x4 a2 = slab[(long long)(k + 2) * L.units + u], a3 = slab[(long long)(k + 3) * L.units + u];
-    acc += a0;
-    acc += a1;
-    acc += a2;
-    acc += a3;
+                                                                float* __restrict__ dw, SlabLayout L, int T) {
+  __shared__ f32x4 part[256];
+  const int tid = threadIdx.x;
+  const long long u = (long long)blockIdx.x * (256 / T) + tid / T;
+  const int r = tid % T;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (u < L.units) {
+    int k = r;
+    for (; k + 3 * T < L.splits; k += 4 * T) {
+      const f32x4 a0 = slab[(long long)k * L.units + u], a1 = slab[(long long)(k + T) * L.units + u];
+      const f32x4 a2 = slab[(long long)(k + 2 * T) * L.units + u], a3 = slab[(long long)(k + 3 * T) * L.units + u];
+      acc += a0;
+      acc += a1;
+      acc += a2;
+      acc += a3;
+    }
+    for (; k < L.splits; k += T) acc += slab[(long long)k * L.units + u];
   }
-  for (; k < L.splits; ++k) acc += slab[(long long)k * L.units + u];
+  part[tid] = acc;
+  __syncthreads();
+  if (r != 0 || u >= L.units) return;
+  for (int j = 1; j < T; ++j) acc += part[tid + j];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const long long idx = slab_dw_index(L, u, e);
@@ -1676,7 +1687,9 @@ static hipError_t launch_wgrad_cfg(const ConvWgradArgs& a0, hipStream_t st) {
   if (splits < 1) splits = 1;
   constexpr int FM = BMO / WM / 16, FN = BNC / WN / 16;
   const long long units = (long long)tiles * 4 * FM * FN * 64;
-  const long long cap = slab_split_cap(a, units * 16);
+  ConvWgradArgs capped = a;  // keep the partial slab (and its reduction) <= 16 MiB
+  if (capped.slab_bytes > ((size_t)16 << 20)) capped.slab_bytes = (size_t)16 << 20;
+  const long long cap = slab_split_cap(capped, units * 16);
   if (splits > cap) splits = cap;
   long long per = (M + splits - 1) / splits;
   per = (per + BKP - 1) / BKP * BKP;
@@ -1747,10 +1760,14 @@ hipError_t launch_wgrad_finish(hipStream_t st) {
   if (!g_pending.slab) return hipSuccess;
   const PendingReduce r = g_pending;
   g_pending = PendingReduce{};
-  const long long bx = (r.L.units + 255) / 256;
+  // threads per unit: enough that each sums <= ~16 splits, up to 64
+  int T = 1;
+  while (T < 64 && (long long)T * 16 < r.L.splits) T <<= 1;
+  const long long per = 256 / T;
+  const long long bx = (r.L.units + per - 1) / per;
   set_kernel_tag("wgrad_slab_reduce_kernel");
   hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)bx), dim3(256), 0, st,
-                     reinterpret_cast<const f32x4*>(r.slab), r.dw, r.L);
+                     reinterpret_cast<const f32x4*>(r.slab), r.dw, r.L, T);
   return hipGetLastError();
 }
 

@@ -33,6 +33,12 @@ void set_err(const std::string& s) { g_err = s; }
     }                                                                                 \
   } while (0)
 
+#define RUN(expr)              \
+  do {                         \
+    int r_ = (expr);           \
+    if (r_) return r_;         \
+  } while (0)
+
 struct Act {  // bf16 NHWC view: ws + off, channel stride ld
   size_t off = 0;
   int ld = 0, C = 0, H = 0, W = 0;
@@ -133,6 +139,15 @@ struct unet_plan {
   // opt-in: UNET_TWO_STREAM=1 (UNET_WS_PRIO=-1/0/1: weight-stream priority).
   bool two_stream = std::getenv("UNET_TWO_STREAM") != nullptr;
   hipStream_t wstream = nullptr;
+  // Split-K slab reductions (HBM-bound) run on their own stream, overlapping
+  // the next (MFMA-bound) conv; two slabs alternate so a wgrad never
+  // overwrites partials still being reduced (UNET_SERIAL_REDUCE=1: reduce on
+  // the weight stream, A/B only)
+  bool side_reduce = std::getenv("UNET_SERIAL_REDUCE") == nullptr;
+  hipStream_t rstream = nullptr;
+  int slab_next = 0;
+  bool slab_busy[2] = {false, false};
+  hipEvent_t slab_ev[2] = {};
   std::vector<hipEvent_t> syncpool;
   int syncused = 0;
   bool want_events = false;  // DDP overlap: record one hipEvent per gradient bucket
@@ -418,7 +433,7 @@ static int build_plan(unet_plan* p) {
   // split-K partials of one weight-gradient launch (register-native layout);
   // launchers cap their split count to what fits
   p->wslab_bytes = (size_t)(64 * w * w) << 20;
-  p->wslab = A.take(p->wslab_bytes);
+  p->wslab = A.take(2 * p->wslab_bytes);  // two slabs, alternating
   Act cats[4];  // cats[l] for decoder level index l (0 = level 4)
   cats[3] = cat1;
   cats[2] = act(A, N, H4, W4, 2 * c0);
@@ -646,6 +661,9 @@ static int ensure_events(unet_plan* p) {
 // ---------------------------------------------------------------------------
 // execution helpers
 // ---------------------------------------------------------------------------
+int stream_edge(unet_plan* p, hipStream_t from, hipStream_t to);
+int pooled_event(unet_plan* p, hipEvent_t* out);
+
 namespace {
 
 struct Ctx {
@@ -656,6 +674,7 @@ struct Ctx {
   hipStream_t st;
   int training;
   hipStream_t wst = nullptr;  // weight-gradient stream (== st when single-stream)
+  hipStream_t rst = nullptr;  // split-K reduction stream (== wst when serial)
   bf16_t* A(const Act& a) const { return reinterpret_cast<bf16_t*>(ws + a.off); }
   template <class T> T* W(size_t off) const { return reinterpret_cast<T*>(ws + off); }
 };
@@ -749,13 +768,43 @@ int conv_dgrad(const Ctx& x, int ci, const Act& dy, const Act& dx, const Act* ad
   return 0;
 }
 
+// launch one weight gradient (args a, slab filled in here) and its split-K
+// reduction: the reduction goes to the reduce stream, ordered after the wgrad;
+// the slab it reads is not reused until that reduction has finished
+int wgrad_and_reduce(const Ctx& x, ConvWgradArgs& a, int mode, const std::string& name, double flops) {
+  unet_plan* p = x.p;
+  const int si = p->slab_next;
+  p->slab_next ^= 1;
+  if (p->slab_busy[si]) {
+    CK(hipStreamWaitEvent(x.wst, p->slab_ev[si], 0));
+    p->slab_busy[si] = false;
+  }
+  a.slab = x.W<float>(p->wslab + (size_t)si * p->wslab_bytes);
+  a.slab_bytes = p->wslab_bytes;
+  {
+    ProfScope ps(p, x.wst, "wgrad " + name, flops);
+    if (mode == 2) CK(launch_convt_wgrad(a, x.wst));
+    else CK(launch_conv_wgrad(a, mode, x.wst));
+  }
+  if (!wgrad_pending()) return 0;
+  if (x.rst != x.wst) RUN(stream_edge(p, x.wst, x.rst));
+  {
+    ProfScope pr(p, x.rst, "wgrad_reduce " + name, 0);
+    CK(launch_wgrad_finish(x.rst));
+  }
+  if (x.rst != x.wst) {
+    RUN(pooled_event(p, &p->slab_ev[si]));
+    CK(hipEventRecord(p->slab_ev[si], x.rst));
+    p->slab_busy[si] = true;
+  }
+  return 0;
+}
+
 int conv_wgrad(const Ctx& x, int ci, const Act& dy, const Act& in) {
   const Conv& cv = x.p->convs[ci];
-  ProfScope ps(x.p, x.wst, "wgrad " + pname(x, cv.w), conv_flops(x.p, cv, dy));
   ConvWgradArgs a = {};
   a.N = x.p->cfg.N;
   a.dw = x.W<float>(cv.wacc);
-  a.slab = x.W<float>(x.p->wslab); a.slab_bytes = x.p->wslab_bytes;
   a.R = cv.R; a.S = cv.S; a.stride = cv.stride; a.pad = cv.pad;
   if (cv.kind == L_CONVT) {
     // one GEMM over the input pixels: "dy" := X [Ci], "x" := dY gathered as
@@ -764,20 +813,13 @@ int conv_wgrad(const Ctx& x, int ci, const Act& dy, const Act& in) {
     a.x = x.A(dy); a.ldx = dy.ld;
     a.H = dy.H; a.W = dy.W; a.C = 4 * cv.Co;
     a.P = in.H; a.Q = in.W; a.Cout = cv.Ci;
-    CK(launch_convt_wgrad(a, x.wst));
-  } else {
-    a.dy = x.A(dy); a.lddy = dy.ld;
-    a.x = x.A(in); a.ldx = in.ld;
-    a.H = in.H; a.W = in.W; a.C = cv.Ci;
-    a.P = dy.H; a.Q = dy.W; a.Cout = cv.Co;
-    CK(launch_conv_wgrad(a, 0, x.wst));
+    return wgrad_and_reduce(x, a, 2, pname(x, cv.w), conv_flops(x.p, cv, dy));
   }
-  ps.close();
-  if (wgrad_pending()) {
-    ProfScope pr(x.p, x.wst, "wgrad_reduce " + pname(x, cv.w), 0);
-    CK(launch_wgrad_finish(x.wst));
-  }
-  return 0;
+  a.dy = x.A(dy); a.lddy = dy.ld;
+  a.x = x.A(in); a.ldx = in.ld;
+  a.H = in.H; a.W = in.W; a.C = cv.Ci;
+  a.P = dy.H; a.Q = dy.W; a.Cout = cv.Co;
+  return wgrad_and_reduce(x, a, 0, pname(x, cv.w), conv_flops(x.p, cv, dy));
 }
 
 int bn_apply(const Ctx& x, int bi, const Act& y, const Act& out, int res_mode, const Act* res, int bi2,
@@ -839,6 +881,7 @@ int bn_backward(const Ctx& x, int bi, BnBwdArgs a, bool fused) {
 }
 
 int unpack_bucket(const Ctx& x, int bk, float* grads) {
+  if (x.rst != x.wst) RUN(stream_edge(x.p, x.rst, x.wst));  // every reduction so far is in dW
   ProfScope ps(x.p, x.wst, "unpack", 0);
   UnpackTable t;
   t.n = 0;
@@ -859,11 +902,6 @@ int unpack_bucket(const Ctx& x, int bk, float* grads) {
 
 }  // namespace
 
-#define RUN(expr)              \
-  do {                         \
-    int r_ = (expr);           \
-    if (r_) return r_;         \
-  } while (0)
 
 // attention-gate / channel-attention argument blocks of decoder level l
 AttGateArgs gate_args(const Ctx& x, int l, float* grads) {
@@ -1051,16 +1089,23 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
   return 0;
 }
 
-// `to` waits for everything issued so far on `from` (fresh pool event per
-// edge, so the order is also right under stream capture)
-static int stream_edge(unet_plan* p, hipStream_t from, hipStream_t to) {
-  if (from == to) return 0;
+// a fresh event of the per-pass pool (reset at every backward)
+int pooled_event(unet_plan* p, hipEvent_t* out) {
   if (p->syncused == (int)p->syncpool.size()) {
     hipEvent_t e;
     CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     p->syncpool.push_back(e);
   }
-  hipEvent_t e = p->syncpool[p->syncused++];
+  *out = p->syncpool[p->syncused++];
+  return 0;
+}
+
+// `to` waits for everything issued so far on `from` (fresh pool event per
+// edge, so the order is also right under stream capture)
+int stream_edge(unet_plan* p, hipStream_t from, hipStream_t to) {
+  if (from == to) return 0;
+  hipEvent_t e;
+  RUN(pooled_event(p, &e));
   CK(hipEventRecord(e, from));
   CK(hipStreamWaitEvent(to, e, 0));
   return 0;
@@ -1080,7 +1125,10 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     CK(hipStreamCreateWithPriority(&p->wstream, hipStreamNonBlocking, prio));
   }
   x.wst = p->two_stream ? p->wstream : st;
+  if (p->side_reduce && !p->rstream) CK(hipStreamCreateWithFlags(&p->rstream, hipStreamNonBlocking));
+  x.rst = p->side_reduce ? p->rstream : x.wst;
   p->syncused = 0;
+  p->slab_busy[0] = p->slab_busy[1] = false;
   // fork: the weight stream starts after the zeroing of the accumulators
   auto fork = [&]() { return stream_edge(p, st, x.wst); };
   CK(hipMemsetAsync(ws + p->zero_bwd_off, 0, p->zero_bwd_bytes, st));
@@ -1258,15 +1306,7 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     a.P = p->y0.H; a.Q = p->y0.W; a.Cout = cv.Co;
     a.R = 7; a.S = 7; a.stride = 2; a.pad = 3;
     a.x = reinterpret_cast<const bf16_t*>(image);
-    a.slab = x.W<float>(p->wslab); a.slab_bytes = p->wslab_bytes;
-    {
-      ProfScope ps(p, x.wst, "wgrad input_conv.weight", 2.0 * N * p->y0.H * p->y0.W * cv.Co * 49);
-      CK(launch_conv_wgrad(a, 1, x.wst));
-    }
-    if (wgrad_pending()) {
-      ProfScope pr(p, x.wst, "wgrad_reduce input_conv.weight", 0);
-      CK(launch_wgrad_finish(x.wst));
-    }
+    RUN(wgrad_and_reduce(x, a, 1, "input_conv.weight", 2.0 * N * p->y0.H * p->y0.W * cv.Co * 49));
   }
   RUN(unpack_bucket(x, 3, grads));
   if (p->nevents) CK(hipEventRecord(p->events[3], x.wst));
@@ -1311,6 +1351,7 @@ void unet_plan_destroy(unet_plan* p) {
   for (int i = 0; i < p->nevents; ++i) (void)hipEventDestroy(p->events[i]);
   for (hipEvent_t e : p->syncpool) (void)hipEventDestroy(e);
   if (p->wstream) (void)hipStreamDestroy(p->wstream);
+  if (p->rstream) (void)hipStreamDestroy(p->rstream);
   delete p;
 }
 
