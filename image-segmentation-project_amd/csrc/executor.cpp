@@ -139,11 +139,12 @@ struct unet_plan {
   // opt-in: UNET_TWO_STREAM=1 (UNET_WS_PRIO=-1/0/1: weight-stream priority).
   bool two_stream = std::getenv("UNET_TWO_STREAM") != nullptr;
   hipStream_t wstream = nullptr;
-  // Split-K slab reductions (HBM-bound) run on their own stream, overlapping
-  // the next (MFMA-bound) conv; two slabs alternate so a wgrad never
-  // overwrites partials still being reduced (UNET_SERIAL_REDUCE=1: reduce on
-  // the weight stream, A/B only)
-  bool side_reduce = std::getenv("UNET_SERIAL_REDUCE") == nullptr;
+  // Split-K slab reductions on their own stream, overlapping the next conv
+  // (two slabs alternate so a wgrad never overwrites partials still being
+  // reduced).  Measured slower on MI355X (2019 vs 2201 img/s, the reductions
+  // compete with the critical dgrad chain for CUs), so it is opt-in:
+  // UNET_SIDE_REDUCE=1.
+  bool side_reduce = std::getenv("UNET_SIDE_REDUCE") != nullptr;
   hipStream_t rstream = nullptr;
   int slab_next = 0;
   bool slab_busy[2] = {false, false};
