@@ -14,6 +14,8 @@ from .utils import (EarlyStopping, calculate_metrics, calculate_metrics_from_log
 from .train import (evaluate, quick_train, train_epoch, train_model, TensorLoader,  # noqa: F401
                     GraphedTrainStep)
 from .synthetic import random_batch, synthetic_cells  # noqa: F401
+from . import dataset  # noqa: F401
+from .dataset import CellAugmenter, CellSegmentationDataset, prepare_data, preprocess  # noqa: F401
 from . import ddp  # noqa: F401
 from . import optim  # noqa: F401
 from .optim import Adam  # noqa: F401

@@ -1103,34 +1103,35 @@ __device__ __forceinline__ long long slab_dw_index(const SlabLayout& L, long lon
   return (long long)(wm * 32 + i * 16 + 4 * g + e) * 64 + wn * 32 + j * 16 + li;
 }
 
-// dW = sum over the splits of the slab, bit-reproducible: T threads share one
-// unit (T | 256, T <= 64), thread r sums splits r, r+T, r+2T, ... in that order
-// (four loads in flight), then the T partials are added in r order through
-// LDS; the partition and both orders are fixed, so the result does not depend
-// on timing.  Every dW element is written once (plain stores).
+// dW = sum over the splits of the slab, bit-reproducible: a block covers
+// 256/T consecutive units x T split lanes (lane-major over units, so every wave
+// instruction reads whole runs of 16-B units); split lane r sums splits r, r+T,
+// r+2T, ... in that order (eight loads in flight), then the T partials are
+// added in r order through LDS.  The partition and both orders are fixed, so
+// the result does not depend on timing.  Every dW element is written once.
 __global__ void __launch_bounds__(256) wgrad_slab_reduce_kernel(const f32x4* __restrict__ slab,
                                                                 float* __restrict__ dw, SlabLayout L, int T) {
   __shared__ f32x4 part[256];
   const int tid = threadIdx.x;
-  const long long u = (long long)blockIdx.x * (256 / T) + tid / T;
-  const int r = tid % T;
+  const int per = 256 / T;
+  const int ul = tid % per, r = tid / per;
+  const long long u = (long long)blockIdx.x * per + ul;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   if (u < L.units) {
     int k = r;
-    for (; k + 3 * T < L.splits; k += 4 * T) {
-      const f32x4 a0 = slab[(long long)k * L.units + u], a1 = slab[(long long)(k + T) * L.units + u];
-      const f32x4 a2 = slab[(long long)(k + 2 * T) * L.units + u], a3 = slab[(long long)(k + 3 * T) * L.units + u];
-      acc += a0;
-      acc += a1;
-      acc += a2;
-      acc += a3;
+    for (; k + 7 * T < L.splits; k += 8 * T) {
+      f32x4 v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = slab[(long long)(k + q * T) * L.units + u];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc += v[q];
     }
     for (; k < L.splits; k += T) acc += slab[(long long)k * L.units + u];
   }
   part[tid] = acc;
   __syncthreads();
   if (r != 0 || u >= L.units) return;
-  for (int j = 1; j < T; ++j) acc += part[tid + j];
+  for (int j = 1; j < T; ++j) acc += part[j * per + ul];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const long long idx = slab_dw_index(L, u, e);
@@ -1760,9 +1761,9 @@ hipError_t launch_wgrad_finish(hipStream_t st) {
   if (!g_pending.slab) return hipSuccess;
   const PendingReduce r = g_pending;
   g_pending = PendingReduce{};
-  // threads per unit: enough that each sums <= ~16 splits, up to 64
+  // split lanes per unit: each thread's loads (<= 8) all in flight at once, up to 16
   int T = 1;
-  while (T < 64 && (long long)T * 16 < r.L.splits) T <<= 1;
+  while (T < 16 && (long long)T * 8 < r.L.splits) T <<= 1;
   const long long per = 256 / T;
   const long long bx = (r.L.units + per - 1) / per;
   set_kernel_tag("wgrad_slab_reduce_kernel");

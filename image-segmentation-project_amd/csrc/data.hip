@@ -1,0 +1,289 @@
+// On-GPU image preprocessing of the reference's data path (SURVEY.md §8(f)
+// row 3): CellSegmentationDataset.__getitem__ / normalize_microscopy_image
+// (/root/reference/dataset.py:30-66) and the index-exact transforms of
+// CellAugmenter (dataset.py:147-151), for a batch of decoded uint8 frames
+// resident in HBM.  The reference runs this per image on the host with cv2 and
+// num_workers=0 (dataset.py:138), which cannot feed even one MI355X.
+//
+//   resize_area_kernel      cv2.resize INTER_AREA (downscale): integer factors
+//                           as resizeAreaFast_ (block sum * 1/area), otherwise
+//                           the computeResizeAreaTab coverage weights, float
+//                           accumulation, cvRound                        (:51)
+//   mask_kernel             cv2.resize INTER_NEAREST, then mask > 0 -> 1.f (:52,61)
+//   normalize_kernel        np.percentile(2, 98) + clip + astype(uint8) (:33-34),
+//                           CLAHE(2.0, 8x8) (:37-38), min-max to [0, 1] (:41);
+//                           one 1024-thread block per image: 256-bin and
+//                           64 x 256 tile histograms in LDS (integer atomics:
+//                           order-independent), tile LUTs, bilinear LUT blend
+//   rot90_vflip_kernel      A.RandomRotate90 (np.rot90 by k) + A.VerticalFlip
+//
+// Everything is byte / integer work except the float blends, which follow the
+// restated OpenCV expressions with explicit roundings (no FMA contraction) so
+// the numpy oracle (oracle/dataset_ref.py) reproduces them bit for bit.
+#include <math.h>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace unet {
+
+__device__ __forceinline__ int cv_round(float v) { return (int)rintf(v); }
+__device__ __forceinline__ uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+
+// computeResizeAreaTab entries of destination index d: up to 3 kinds (partial
+// head, full cells, partial tail); returns the count and fills (si, alpha)
+__device__ __forceinline__ int area_entries(int d, int ssize, double scale, int* si, float* al, int cap) {
+  const double fs1 = d * scale, fs2 = fs1 + scale;
+  const double cell = fmin(scale, (double)ssize - fs1);
+  int s1 = (int)ceil(fs1), s2 = (int)floor(fs2);
+  s2 = min(s2, ssize - 1);
+  s1 = min(s1, s2);
+  int k = 0;
+  if (s1 - fs1 > 1e-3 && k < cap) { si[k] = s1 - 1; al[k++] = (float)((s1 - fs1) / cell); }
+  for (int s = s1; s < s2 && k < cap; ++s) { si[k] = s; al[k++] = (float)(1.0 / cell); }
+  if (fs2 - s2 > 1e-3 && k < cap) { si[k] = s2; al[k++] = (float)(fmin(fmin(fs2 - s2, 1.0), cell) / cell); }
+  return k;
+}
+
+constexpr int kAreaCap = 64;  // scale factors up to 62 per axis
+
+__global__ void __launch_bounds__(256) resize_area_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                          int N, int H, int W, int oh, int ow, int fx, int fy) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)N * oh * ow) return;
+  const int dx = (int)(i % ow), dy = (int)((i / ow) % oh), n = (int)(i / ((int64_t)oh * ow));
+  const uint8_t* img = src + (int64_t)n * H * W;
+  if (fx > 0) {  // integer factors: resizeAreaFast_
+    int s = 0;
+    for (int y = 0; y < fy; ++y)
+      for (int x = 0; x < fx; ++x) s += img[(int64_t)(dy * fy + y) * W + dx * fx + x];
+    if (fx == 2 && fy == 2) {  // ResizeAreaFastVec_SIMD_8u: (a + b + c + d + 2) >> 2
+      dst[i] = (uint8_t)((s + 2) >> 2);
+      return;
+    }
+    const float scale = 1.f / (float)(fx * fy);
+    dst[i] = sat_u8(cv_round(__fmul_rn((float)s, scale)));
+    return;
+  }
+  int xs[kAreaCap], ys[kAreaCap];
+  float xa[kAreaCap], ya[kAreaCap];
+  const int nx = area_entries(dx, W, 1.0 / ((double)ow / W), xs, xa, kAreaCap);
+  const int ny = area_entries(dy, H, 1.0 / ((double)oh / H), ys, ya, kAreaCap);
+  float acc = 0.f;
+  for (int j = 0; j < ny; ++j) {
+    const uint8_t* row = img + (int64_t)ys[j] * W;
+    float b = 0.f;
+    for (int k = 0; k < nx; ++k) b = __fadd_rn(b, __fmul_rn((float)row[xs[k]], xa[k]));
+    const float t = __fmul_rn(b, ya[j]);
+    acc = j == 0 ? t : __fadd_rn(acc, t);
+  }
+  dst[i] = sat_u8(cv_round(acc));
+}
+
+__global__ void __launch_bounds__(256) mask_kernel(const uint8_t* __restrict__ src, float* __restrict__ dst, int N,
+                                                   int H, int W, int oh, int ow) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)N * oh * ow) return;
+  const int dx = (int)(i % ow), dy = (int)((i / ow) % oh), n = (int)(i / ((int64_t)oh * ow));
+  const int sx = min((int)floor(dx * (1.0 / ((double)ow / W))), W - 1);  // cv::resize ifx = 1 / inv_scale
+  const int sy = min((int)floor(dy * (1.0 / ((double)oh / H))), H - 1);
+  dst[i] = src[((int64_t)n * H + sy) * W + sx] > 0 ? 1.f : 0.f;
+}
+
+// k-th smallest value (0-based) of an image from its 256-bin histogram
+__device__ __forceinline__ int kth_from_hist(const int* hist, int64_t k) {
+  int64_t c = 0;
+  for (int v = 0; v < 256; ++v) {
+    c += hist[v];
+    if (c > k) return v;
+  }
+  return 255;
+}
+
+// np.percentile(img, q), method 'linear' (numpy's _lerp form), float64
+__device__ double percentile_from_hist(const int* hist, int64_t n, double q) {
+  const double h = (double)(n - 1) * (q / 100.0);
+  const int64_t lo = (int64_t)floor(h);
+  const int64_t hi = lo + 1 < n ? lo + 1 : n - 1;
+  const double t = h - (double)lo;
+  const double a = kth_from_hist(hist, lo), b = kth_from_hist(hist, hi);
+  const double d = b - a;
+  return t >= 0.5 ? b - d * (1.0 - t) : a + d * t;
+}
+
+// clip to [plo, phi] in float64, then astype(uint8) (truncation)
+__device__ __forceinline__ int clip_trunc(int v, double plo, double phi) {
+  const double c = v < plo ? plo : (v > phi ? phi : (double)v);
+  return (int)c;
+}
+
+// BORDER_REFLECT_101 index into [0, n)
+__device__ __forceinline__ int reflect101(int i, int n) {
+  if (n == 1) return 0;
+  while (i < 0 || i >= n) i = i < 0 ? -i : 2 * n - 2 - i;
+  return i;
+}
+
+constexpr int kGrid = 8;
+
+struct NormSmem {
+  int hist[256];
+  int thist[kGrid * kGrid][256];
+  uint8_t lut[kGrid * kGrid][256];
+  double plo, phi;
+  int mn, mx;
+};
+
+// CLAHE value of pixel (y, x) of the clipped image (LUT blend, clahe.cpp
+// CLAHE_Interpolation_Body)
+__device__ __forceinline__ int clahe_px(const NormSmem& s, int v, int y, int x, int tw, int th) {
+  const float inv_tw = 1.f / (float)tw, inv_th = 1.f / (float)th;
+  const float txf = __fadd_rn(__fmul_rn((float)x, inv_tw), -0.5f);
+  const float tyf = __fadd_rn(__fmul_rn((float)y, inv_th), -0.5f);
+  int tx1 = (int)floorf(txf), ty1 = (int)floorf(tyf);
+  const float xa = __fadd_rn(txf, -(float)tx1), ya = __fadd_rn(tyf, -(float)ty1);
+  const float xa1 = __fadd_rn(1.f, -xa), ya1 = __fadd_rn(1.f, -ya);
+  const int tx2 = min(tx1 + 1, kGrid - 1), ty2 = min(ty1 + 1, kGrid - 1);
+  tx1 = max(tx1, 0);
+  ty1 = max(ty1, 0);
+  const float l11 = s.lut[ty1 * kGrid + tx1][v], l12 = s.lut[ty1 * kGrid + tx2][v];
+  const float l21 = s.lut[ty2 * kGrid + tx1][v], l22 = s.lut[ty2 * kGrid + tx2][v];
+  const float top = __fadd_rn(__fmul_rn(l11, xa1), __fmul_rn(l12, xa));
+  const float bot = __fadd_rn(__fmul_rn(l21, xa1), __fmul_rn(l22, xa));
+  const float r = __fadd_rn(__fmul_rn(top, ya1), __fmul_rn(bot, ya));
+  return sat_u8(cv_round(r));
+}
+
+__global__ void __launch_bounds__(1024) normalize_kernel(const uint8_t* __restrict__ src, float* __restrict__ dst,
+                                                         int H, int W, int normalize) {
+  __shared__ NormSmem s;
+  const int n = blockIdx.x, tid = threadIdx.x;
+  const uint8_t* img = src + (int64_t)n * H * W;
+  float* out = dst + (int64_t)n * H * W;
+  const int64_t npx = (int64_t)H * W;
+  if (!normalize) {  // image.astype(np.float32) / 255.0  (dataset.py:56)
+    for (int64_t i = tid; i < npx; i += blockDim.x) out[i] = __fdiv_rn((float)img[i], 255.f);
+    return;
+  }
+  for (int i = tid; i < 256; i += blockDim.x) s.hist[i] = 0;
+  for (int i = tid; i < kGrid * kGrid * 256; i += blockDim.x) (&s.thist[0][0])[i] = 0;
+  if (tid == 0) { s.mn = 255; s.mx = 0; }
+  __syncthreads();
+  for (int64_t i = tid; i < npx; i += blockDim.x) atomicAdd(&s.hist[img[i]], 1);
+  __syncthreads();
+  if (tid == 0) {
+    s.plo = percentile_from_hist(s.hist, npx, 2.0);
+    s.phi = percentile_from_hist(s.hist, npx, 98.0);
+  }
+  __syncthreads();
+  const double plo = s.plo, phi = s.phi;
+  // tile histograms of the clipped image, padded to a multiple of the grid by reflection
+  const int He = H + (kGrid - H % kGrid) % kGrid, We = W + (kGrid - W % kGrid) % kGrid;
+  const int th = He / kGrid, tw = We / kGrid;
+  for (int64_t i = tid; i < (int64_t)He * We; i += blockDim.x) {
+    const int y = (int)(i / We), x = (int)(i % We);
+    const int v = clip_trunc(img[(int64_t)reflect101(y, H) * W + reflect101(x, W)], plo, phi);
+    atomicAdd(&s.thist[(y / th) * kGrid + x / tw][v], 1);
+  }
+  __syncthreads();
+  // per tile: clip at the limit, redistribute the excess, cumulative LUT
+  const int area = th * tw;
+  const int limit = max((int)(2.0 * area / 256.0), 1);
+  const float lut_scale = 255.f / (float)area;
+  if (tid < kGrid * kGrid) {
+    int* hst = s.thist[tid];
+    int clipped = 0;
+    for (int v = 0; v < 256; ++v)
+      if (hst[v] > limit) { clipped += hst[v] - limit; hst[v] = limit; }
+    const int batch = clipped / 256;
+    int residual = clipped - batch * 256;
+    for (int v = 0; v < 256; ++v) hst[v] += batch;
+    if (residual) {
+      const int step = max(256 / residual, 1);
+      for (int v = 0; v < 256 && residual > 0; v += step, --residual) hst[v] += 1;
+    }
+    int sum = 0;
+    for (int v = 0; v < 256; ++v) {
+      sum += hst[v];
+      s.lut[tid][v] = sat_u8(cv_round(__fmul_rn((float)sum, lut_scale)));
+    }
+  }
+  __syncthreads();
+  int mn = 255, mx = 0;
+  for (int64_t i = tid; i < npx; i += blockDim.x) {
+    const int y = (int)(i / W), x = (int)(i % W);
+    const int c = clahe_px(s, clip_trunc(img[i], plo, phi), y, x, tw, th);
+    mn = min(mn, c);
+    mx = max(mx, c);
+  }
+  atomicMin(&s.mn, mn);
+  atomicMax(&s.mx, mx);
+  __syncthreads();
+  const int cmin = s.mn;
+  const double den = (double)(s.mx - cmin) + 1e-8;  // uint8 range + 1e-8 -> float64
+  for (int64_t i = tid; i < npx; i += blockDim.x) {
+    const int y = (int)(i / W), x = (int)(i % W);
+    const int c = clahe_px(s, clip_trunc(img[i], plo, phi), y, x, tw, th);
+    out[i] = (float)((double)(c - cmin) / den);
+  }
+}
+
+// out = vflip(rot90(in, k)) per image (square frames when k is odd)
+__global__ void __launch_bounds__(256) rot90_vflip_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                          int N, int H, int W, const int* __restrict__ ks,
+                                                          const int* __restrict__ flips) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)N * H * W) return;
+  const int n = (int)(i / ((int64_t)H * W));
+  const int k = ((ks[n] % 4) + 4) % 4;
+  const int Ho = (k & 1) ? W : H, Wo = (k & 1) ? H : W;  // output dims
+  const int64_t r = i - (int64_t)n * H * W;
+  int y = (int)(r / Wo), x = (int)(r % Wo);
+  if (flips[n]) y = Ho - 1 - y;
+  // np.rot90(a, k) (counter-clockwise): out[y][x] = a[...]
+  int sy, sx;
+  switch (k) {
+    case 0: sy = y; sx = x; break;
+    case 1: sy = x; sx = W - 1 - y; break;
+    case 2: sy = H - 1 - y; sx = W - 1 - x; break;
+    default: sy = H - 1 - x; sx = y; break;
+  }
+  dst[i] = src[(int64_t)n * H * W + (int64_t)sy * W + sx];
+}
+
+static inline unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
+
+hipError_t launch_resize_area(const uint8_t* src, uint8_t* dst, int N, int H, int W, int oh, int ow, hipStream_t st) {
+  if (N <= 0 || oh <= 0 || ow <= 0 || oh > H || ow > W) return hipErrorInvalidValue;
+  if ((double)W / ow > kAreaCap - 2 || (double)H / oh > kAreaCap - 2) return hipErrorInvalidValue;
+  // cv::resize is_area_fast: both scales 1 / (dsize / ssize) within DBL_EPSILON of an integer
+  const double sx = 1.0 / ((double)ow / W), sy = 1.0 / ((double)oh / H);
+  const bool fast = fabs(sx - rint(sx)) < 2.220446049250313e-16 && fabs(sy - rint(sy)) < 2.220446049250313e-16;
+  const int fx = fast ? (int)rint(sx) : 0;
+  const int fy = fast ? (int)rint(sy) : 0;
+  hipLaunchKernelGGL(resize_area_kernel, dim3(blocks_for((int64_t)N * oh * ow)), dim3(256), 0, st, src, dst, N, H, W,
+                     oh, ow, fx, fy);
+  return hipGetLastError();
+}
+
+hipError_t launch_mask_prep(const uint8_t* src, float* dst, int N, int H, int W, int oh, int ow, hipStream_t st) {
+  if (N <= 0 || oh <= 0 || ow <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(mask_kernel, dim3(blocks_for((int64_t)N * oh * ow)), dim3(256), 0, st, src, dst, N, H, W, oh, ow);
+  return hipGetLastError();
+}
+
+hipError_t launch_normalize(const uint8_t* src, float* dst, int N, int H, int W, int normalize, hipStream_t st) {
+  if (N <= 0 || H < kGrid || W < kGrid) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(normalize_kernel, dim3(N), dim3(1024), 0, st, src, dst, H, W, normalize);
+  return hipGetLastError();
+}
+
+hipError_t launch_rot90_vflip(const uint8_t* src, uint8_t* dst, int N, int H, int W, const int* k, const int* flip,
+                              hipStream_t st) {
+  if (N <= 0 || H <= 0 || W <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rot90_vflip_kernel, dim3(blocks_for((int64_t)N * H * W)), dim3(256), 0, st, src, dst, N, H, W, k,
+                     flip);
+  return hipGetLastError();
+}
+
+}  // namespace unet

@@ -1580,6 +1580,32 @@ int unet_bn_backward(const void* dout, int ldd, const void* out, int ldo, const 
   return 0;
 }
 
+int unet_resize_area_u8(const uint8_t* src, int N, int H, int W, uint8_t* dst, int oh, int ow, hipStream_t stream) {
+  if (!src || !dst) { set_err("unet_resize_area_u8: null buffer"); return 1; }
+  CK(launch_resize_area(src, dst, N, H, W, oh, ow, stream));
+  return 0;
+}
+
+int unet_mask_prep(const uint8_t* src, int N, int H, int W, float* dst, int oh, int ow, hipStream_t stream) {
+  if (!src || !dst) { set_err("unet_mask_prep: null buffer"); return 1; }
+  CK(launch_mask_prep(src, dst, N, H, W, oh, ow, stream));
+  return 0;
+}
+
+int unet_normalize_microscopy(const uint8_t* src, int N, int H, int W, float* dst, int normalize,
+                              hipStream_t stream) {
+  if (!src || !dst) { set_err("unet_normalize_microscopy: null buffer"); return 1; }
+  CK(launch_normalize(src, dst, N, H, W, normalize, stream));
+  return 0;
+}
+
+int unet_rot90_vflip_u8(const uint8_t* src, int N, int H, int W, const int* k, const int* vflip, uint8_t* dst,
+                        hipStream_t stream) {
+  if (!src || !dst || !k || !vflip) { set_err("unet_rot90_vflip_u8: null buffer"); return 1; }
+  CK(launch_rot90_vflip(src, dst, N, H, W, k, vflip, stream));
+  return 0;
+}
+
 int unet_maxpool_fwd(const void* x, int ldx, void* y, uint8_t* idx, int N, int H, int W, int C,
                      hipStream_t stream) {
   MaxPoolArgs m = {};

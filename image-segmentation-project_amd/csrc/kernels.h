@@ -222,6 +222,13 @@ hipError_t launch_loss_grad(const float* logits, const float* target, int64_t n,
 hipError_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float* coef, float lr,
                        float beta1, float beta2, float eps, float wd, int advance_step, hipStream_t st);
 
+// on-GPU preprocessing of uint8 frames (data.hip; dataset.py:30-66,147-151)
+hipError_t launch_resize_area(const uint8_t* src, uint8_t* dst, int N, int H, int W, int oh, int ow, hipStream_t st);
+hipError_t launch_mask_prep(const uint8_t* src, float* dst, int N, int H, int W, int oh, int ow, hipStream_t st);
+hipError_t launch_normalize(const uint8_t* src, float* dst, int N, int H, int W, int normalize, hipStream_t st);
+hipError_t launch_rot90_vflip(const uint8_t* src, uint8_t* dst, int N, int H, int W, const int* k, const int* flip,
+                              hipStream_t st);
+
 // attention decoder (attention.hip; advanced_models.py:7-61)
 struct AttGateArgs {
   const bf16_t* s; int lds;            // relu(BN_g + BN_x), F_int channels

@@ -138,6 +138,16 @@ class GraphedTrainStep:
         return self.out, self.loss
 
 
+def _is_frames(x) -> bool:
+    """uint8 [N,H,W] frames (tensor, array or list of 2-D arrays)?"""
+    if isinstance(x, torch.Tensor):
+        return x.dtype == torch.uint8
+    import numpy as np
+    if isinstance(x, np.ndarray):
+        return x.dtype == np.uint8
+    return isinstance(x, (list, tuple)) and len(x) > 0 and getattr(x[0], "dtype", None) == np.uint8
+
+
 class TensorLoader:
     """Minimal in-memory replacement for ``prepare_data`` (dataset.py:121-138)."""
 
@@ -162,13 +172,29 @@ class TensorLoader:
 def train_model(model, train_images, train_masks, val_images, val_masks, criterion, optimizer,
                 scheduler: Optional[object], num_epochs: int, device, config: Dict,
                 augmentations_per_image: int = 0, save_plots: bool = True) -> Dict:
-    """train.py:115-244 epoch loop over in-memory tensors [N,1,H,W]."""
-    if augmentations_per_image:
-        raise NotImplementedError("CellAugmenter (dataset.py:140-210) is outside the MI355X hot path")
+    """train.py:115-244 epoch loop.  Inputs are either preprocessed float
+    tensors [N,1,H,W] or decoded uint8 frames [N,H,W] (``cv2.imread`` output);
+    frames go through the on-GPU data pipeline (dataset.py: augmentation,
+    resize to ``config['img_size']``, normalisation) exactly where the
+    reference calls CellAugmenter / prepare_data (train.py:141-157)."""
     if isinstance(train_images, (list, tuple)) and train_images and isinstance(train_images[0], str):
-        raise NotImplementedError("image paths need the cv2 pipeline (dataset.py:17-66); pass tensors")
-    train_loader = TensorLoader(train_images, train_masks, config["batch_size"], shuffle=True)
-    val_loader = TensorLoader(val_images, val_masks, config["batch_size"], shuffle=False)
+        raise NotImplementedError("file paths need host TIFF decoding (cv2.imread): pass decoded uint8 frames")
+    if _is_frames(train_images):
+        from .dataset import CellAugmenter, prepare_data
+        size = config.get("img_size", (256, 256))
+        size = (size, size) if isinstance(size, int) else tuple(size)
+        if augmentations_per_image > 0:
+            train_images, train_masks = CellAugmenter(augmentations_per_image).augment_training_data(
+                train_images, train_masks)
+        train_loader = prepare_data(train_images, train_masks, config["batch_size"], size, shuffle=True,
+                                    device=device)
+        val_loader = prepare_data(val_images, val_masks, config["batch_size"], size, shuffle=False, device=device)
+    else:
+        if augmentations_per_image:
+            raise ValueError("augmentation works on uint8 frames (before resize / normalisation), as the "
+                             "reference's CellAugmenter does; pass frames, not preprocessed tensors")
+        train_loader = TensorLoader(train_images, train_masks, config["batch_size"], shuffle=True)
+        val_loader = TensorLoader(val_images, val_masks, config["batch_size"], shuffle=False)
     train_hist, val_hist, lr_hist = [], [], []
     best_iou, best_state, best_epoch = 0.0, None, 0
     stopper = EarlyStopping(patience=config.get("early_stopping_patience", 7),

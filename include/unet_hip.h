@@ -154,6 +154,21 @@ int unet_maxpool_fwd(const void* x, int ldx, void* y, uint8_t* idx, int N, int H
 int unet_maxpool_bwd(const void* dy, const uint8_t* idx, const void* addend, int ldadd, void* dx,
                      int N, int H, int W, int C, hipStream_t stream);
 
+/* ---- on-GPU data pipeline (CellSegmentationDataset / CellAugmenter,
+ * dataset.py:30-66,147-151) over N decoded uint8 frames [N][H][W] ---- */
+/* cv2.resize(..., INTER_AREA) downscale to [N][oh][ow] uint8 (dataset.py:51) */
+int unet_resize_area_u8(const uint8_t* src, int N, int H, int W, uint8_t* dst, int oh, int ow, hipStream_t stream);
+/* cv2.resize(..., INTER_NEAREST) then (mask > 0) -> float32 [N][oh][ow] (dataset.py:52,61) */
+int unet_mask_prep(const uint8_t* src, int N, int H, int W, float* dst, int oh, int ow, hipStream_t stream);
+/* normalize_microscopy_image (dataset.py:30-42: 2/98 percentile clip, CLAHE(2.0, 8x8),
+ * min-max) -> float32 [N][H][W]; normalize = 0: x / 255 (dataset.py:56) */
+int unet_normalize_microscopy(const uint8_t* src, int N, int H, int W, float* dst, int normalize,
+                              hipStream_t stream);
+/* A.RandomRotate90 + A.VerticalFlip (dataset.py:147,150): dst[n] = vflip?(rot90(src[n], k[n]));
+ * k, vflip: device int32 [N]; frames square when any k is odd */
+int unet_rot90_vflip_u8(const uint8_t* src, int N, int H, int W, const int* k, const int* vflip, uint8_t* dst,
+                        hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

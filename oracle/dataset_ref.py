@@ -1,0 +1,209 @@
+"""TEST INFRASTRUCTURE ONLY — numpy restatement of the reference's image
+preprocessing, the checker for the HIP data pipeline.
+
+Reference: ``CellSegmentationDataset.__getitem__`` / ``normalize_microscopy_image``
+(/root/reference/dataset.py:30-66):
+
+    image = cv2.resize(image, img_size, interpolation=cv2.INTER_AREA)        # :51
+    mask  = cv2.resize(mask,  img_size, interpolation=cv2.INTER_NEAREST)     # :52
+    p_low, p_high = np.percentile(image, [2, 98])                           # :33
+    image_clipped = np.clip(image, p_low, p_high)                           # :34
+    image_clahe = cv2.createCLAHE(2.0, (8, 8)).apply(image_clipped.astype(np.uint8))  # :37-38
+    image_norm = (image_clahe - image_clahe.min()) / (image_clahe.max() - image_clahe.min() + 1e-8)  # :41
+    mask = (mask > 0).astype(np.float32)                                    # :61
+
+and the two deterministic transforms of ``CellAugmenter`` (dataset.py:147-152):
+``A.RandomRotate90`` (np.rot90 by k) and ``A.VerticalFlip``.
+
+Third-party algorithms restated (neither OpenCV nor albumentations is
+installed here, and the reference ships no image fixtures, so the cv2 parts
+are PARITY UNPINNED; numpy's percentile is pinned against numpy itself):
+
+* ``np.percentile`` (numpy 2.2, method='linear'): virtual index
+  h = (n-1) q/100, v[floor] + (v[ceil]-v[floor]) * frac, numpy's _lerp form
+  (``b - (b-a)(1-t)`` for t >= 0.5), float64.
+* ``cv2.resize`` INTER_AREA, downscaling (OpenCV 4.x imgproc/src/resize.cpp):
+  integer factors: ``resizeAreaFast_`` = integer block sum * (1/area) in float,
+  ``cvRound``; otherwise ``computeResizeAreaTab`` coverage weights (float
+  alpha per source column / row) accumulated horizontally then vertically in
+  float, ``cvRound``.  INTER_NEAREST: ``sx = min(floor(dx * (ssize/dsize)), ssize-1)``.
+* ``cv2.CLAHE`` (imgproc/src/clahe.cpp, 8-bit path): tile grid 8x8 (BORDER_REFLECT_101
+  padding to a multiple of the grid), clip limit max(int(2.0 * tileArea / 256), 1),
+  excess redistributed as ``clipped // 256`` per bin + a residual every
+  ``max(256 // residual, 1)`` bins, LUT = saturate(round(cumsum * 255 / tileArea)),
+  bilinear interpolation between the 4 nearest tile LUTs in float
+  (``txf = x / tileW - 0.5``), ``cvRound``.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+
+def percentile_linear(img: np.ndarray, q: float) -> float:
+    """np.percentile(img, q) (method 'linear'), restated on the sorted values."""
+    v = np.sort(img.reshape(-1)).astype(np.float64)
+    n = v.size
+    h = (n - 1) * (q / 100.0)
+    lo = int(math.floor(h))
+    hi = min(lo + 1, n - 1)
+    t = h - lo
+    a, b = v[lo], v[hi]
+    d = b - a
+    return float(b - d * (1.0 - t)) if t >= 0.5 else float(a + d * t)
+
+
+def _cv_round(x: np.ndarray) -> np.ndarray:
+    return np.rint(x)  # cvRound: round half to even (default FP rounding mode)
+
+
+def area_tab(ssize: int, dsize: int):
+    """computeResizeAreaTab: list per destination index of (src index, float32 alpha)."""
+    scale = _cv_scale(ssize, dsize)
+    tab = []
+    for dx in range(dsize):
+        fsx1 = dx * scale
+        fsx2 = fsx1 + scale
+        cell = min(scale, ssize - fsx1)
+        sx1, sx2 = math.ceil(fsx1), math.floor(fsx2)
+        sx2 = min(sx2, ssize - 1)
+        sx1 = min(sx1, sx2)
+        row = []
+        if sx1 - fsx1 > 1e-3:
+            row.append((sx1 - 1, np.float32((sx1 - fsx1) / cell)))
+        for sx in range(sx1, sx2):
+            row.append((sx, np.float32(1.0 / cell)))
+        if fsx2 - sx2 > 1e-3:
+            row.append((sx2, np.float32(min(min(fsx2 - sx2, 1.0), cell) / cell)))
+        tab.append(row)
+    return tab
+
+
+def _cv_scale(ssize: int, dsize: int) -> float:
+    """cv::resize's scale: 1. / inv_scale with inv_scale = (double)dsize / ssize."""
+    return 1.0 / (dsize / ssize)
+
+
+def resize_area_u8(img: np.ndarray, oh: int, ow: int) -> np.ndarray:
+    """cv2.resize(img, (ow, oh), interpolation=cv2.INTER_AREA) for uint8, downscaling."""
+    h, w = img.shape
+    if oh == h and ow == w:
+        return img.copy()
+    if oh > h or ow > w:
+        raise NotImplementedError("INTER_AREA upscaling is not on the reference path (images are downscaled)")
+    sx, sy = _cv_scale(w, ow), _cv_scale(h, oh)
+    eps = np.finfo(np.float64).eps
+    if abs(sx - round(sx)) < eps and abs(sy - round(sy)) < eps:  # is_area_fast: resizeAreaFast_
+        fx, fy = int(round(sx)), int(round(sy))
+        blk = img[:oh * fy, :ow * fx].astype(np.int64).reshape(oh, fy, ow, fx).sum(axis=(1, 3))
+        if fx == 2 and fy == 2:  # ResizeAreaFastVec_SIMD_8u: (a + b + c + d + 2) >> 2
+            return ((blk + 2) >> 2).astype(np.uint8)
+        scale = np.float32(1.0) / np.float32(fx * fy)
+        return np.clip(_cv_round(blk.astype(np.float32) * scale), 0, 255).astype(np.uint8)
+    xt, yt = area_tab(w, ow), area_tab(h, oh)
+    out = np.empty((oh, ow), np.uint8)
+    src = img.astype(np.float32)
+    for dy in range(oh):
+        acc = np.zeros(ow, np.float32)
+        first = True
+        for sy_, beta in yt[dy]:
+            buf = np.zeros(ow, np.float32)
+            for dx in range(ow):
+                s = np.float32(0.0)
+                for sx_, alpha in xt[dx]:
+                    s = np.float32(s + np.float32(src[sy_, sx_] * alpha))
+                buf[dx] = s
+            if first:
+                acc = (buf * beta).astype(np.float32)
+                first = False
+            else:
+                acc = (acc + (buf * beta).astype(np.float32)).astype(np.float32)
+        out[dy] = np.clip(_cv_round(acc), 0, 255).astype(np.uint8)
+    return out
+
+
+def resize_nearest_u8(img: np.ndarray, oh: int, ow: int) -> np.ndarray:
+    """cv2.resize(img, (ow, oh), interpolation=cv2.INTER_NEAREST)."""
+    h, w = img.shape
+    ys = np.minimum(np.floor(np.arange(oh) * _cv_scale(h, oh)).astype(np.int64), h - 1)
+    xs = np.minimum(np.floor(np.arange(ow) * _cv_scale(w, ow)).astype(np.int64), w - 1)
+    return img[ys][:, xs]
+
+
+def clahe_u8(img: np.ndarray, clip_limit: float = 2.0, grid: int = 8) -> np.ndarray:
+    """cv2.createCLAHE(clipLimit, (grid, grid)).apply(img) for uint8."""
+    h, w = img.shape
+    ph = (grid - h % grid) % grid
+    pw = (grid - w % grid) % grid
+    ext = np.pad(img, ((0, ph), (0, pw)), mode="reflect") if (ph or pw) else img  # BORDER_REFLECT_101
+    th, tw = ext.shape[0] // grid, ext.shape[1] // grid
+    area = th * tw
+    limit = max(int(clip_limit * area / 256), 1) if clip_limit > 0 else 0
+    lut_scale = np.float32(255.0) / np.float32(area)
+    luts = np.empty((grid, grid, 256), np.uint8)
+    for ty in range(grid):
+        for tx in range(grid):
+            tile = ext[ty * th:(ty + 1) * th, tx * tw:(tx + 1) * tw]
+            hist = np.bincount(tile.reshape(-1), minlength=256).astype(np.int64)
+            if limit > 0:
+                clipped = int(np.maximum(hist - limit, 0).sum())
+                hist = np.minimum(hist, limit)
+                batch = clipped // 256
+                residual = clipped - batch * 256
+                hist += batch
+                if residual:
+                    step = max(256 // residual, 1)
+                    i = 0
+                    while i < 256 and residual > 0:
+                        hist[i] += 1
+                        i += step
+                        residual -= 1
+            cum = np.cumsum(hist)
+            luts[ty, tx] = np.clip(_cv_round(cum.astype(np.float32) * lut_scale), 0, 255).astype(np.uint8)
+    inv_tw, inv_th = np.float32(1.0) / np.float32(tw), np.float32(1.0) / np.float32(th)
+    xf = np.arange(w, dtype=np.float32) * inv_tw - np.float32(0.5)
+    yf = np.arange(h, dtype=np.float32) * inv_th - np.float32(0.5)
+    tx1 = np.floor(xf).astype(np.int64)
+    ty1 = np.floor(yf).astype(np.int64)
+    xa = (xf - tx1.astype(np.float32)).astype(np.float32)
+    ya = (yf - ty1.astype(np.float32)).astype(np.float32)
+    tx2, ty2 = np.minimum(tx1 + 1, grid - 1), np.minimum(ty1 + 1, grid - 1)
+    tx1, ty1 = np.maximum(tx1, 0), np.maximum(ty1, 0)
+    v = img.astype(np.int64)
+    l11 = luts[ty1[:, None], tx1[None, :], v].astype(np.float32)
+    l12 = luts[ty1[:, None], tx2[None, :], v].astype(np.float32)
+    l21 = luts[ty2[:, None], tx1[None, :], v].astype(np.float32)
+    l22 = luts[ty2[:, None], tx2[None, :], v].astype(np.float32)
+    xa_, xa1 = xa[None, :], np.float32(1.0) - xa[None, :]
+    ya_, ya1 = ya[:, None], np.float32(1.0) - ya[:, None]
+    res = ((l11 * xa1 + l12 * xa_) * ya1 + (l21 * xa1 + l22 * xa_) * ya_).astype(np.float32)
+    return np.clip(_cv_round(res), 0, 255).astype(np.uint8)
+
+
+def normalize_microscopy_image(img: np.ndarray) -> np.ndarray:
+    """dataset.py:30-42 on a uint8 image; float64 result as the reference's
+    (np.percentile is the reference's own call; percentile_linear restates it
+    for the GPU kernel and is checked against it)."""
+    p_low, p_high = np.percentile(img, [2, 98])
+    clipped = np.clip(img, p_low, p_high)
+    c = clahe_u8(clipped.astype(np.uint8))
+    return (c - c.min()) / (c.max() - c.min() + 1e-8)
+
+
+def preprocess(image: np.ndarray, mask: np.ndarray, img_size=(256, 256), normalize: bool = True):
+    """dataset.py:44-66 after cv2.imread: (float32 [1,h,w] image, float32 [1,h,w] mask)."""
+    ow, oh = img_size  # cv2 dsize order (width, height)
+    image = resize_area_u8(image, oh, ow)
+    mask = resize_nearest_u8(mask, oh, ow)
+    image = normalize_microscopy_image(image) if normalize else image.astype(np.float32) / np.float32(255.0)
+    mask = (mask > 0).astype(np.float32)
+    return image.astype(np.float32)[None], mask[None]
+
+
+def rot90_vflip(img: np.ndarray, k: int, vflip: bool) -> np.ndarray:
+    """A.RandomRotate90 (np.rot90(img, k)) then A.VerticalFlip (img[::-1]), dataset.py:147-151."""
+    out = np.rot90(img, k)
+    if vflip:
+        out = out[::-1]
+    return np.ascontiguousarray(out)
