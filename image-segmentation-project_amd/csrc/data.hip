@@ -61,7 +61,7 @@ __global__ void __launch_bounds__(256) resize_area_kernel(const uint8_t* __restr
       dst[i] = (uint8_t)((s + 2) >> 2);
       return;
     }
-    const float scale = 1.f / (float)(fx * fy);
+    const float scale = __fdiv_rn(1.f, (float)(fx * fy));
     dst[i] = sat_u8(cv_round(__fmul_rn((float)s, scale)));
     return;
   }
@@ -137,7 +137,7 @@ struct NormSmem {
 // CLAHE value of pixel (y, x) of the clipped image (LUT blend, clahe.cpp
 // CLAHE_Interpolation_Body)
 __device__ __forceinline__ int clahe_px(const NormSmem& s, int v, int y, int x, int tw, int th) {
-  const float inv_tw = 1.f / (float)tw, inv_th = 1.f / (float)th;
+  const float inv_tw = __fdiv_rn(1.f, (float)tw), inv_th = __fdiv_rn(1.f, (float)th);
   const float txf = __fadd_rn(__fmul_rn((float)x, inv_tw), -0.5f);
   const float tyf = __fadd_rn(__fmul_rn((float)y, inv_th), -0.5f);
   int tx1 = (int)floorf(txf), ty1 = (int)floorf(tyf);
@@ -189,7 +189,7 @@ __global__ void __launch_bounds__(1024) normalize_kernel(const uint8_t* __restri
   // per tile: clip at the limit, redistribute the excess, cumulative LUT
   const int area = th * tw;
   const int limit = max((int)(2.0 * area / 256.0), 1);
-  const float lut_scale = 255.f / (float)area;
+  const float lut_scale = __fdiv_rn(255.f, (float)area);
   if (tid < kGrid * kGrid) {
     int* hst = s.thist[tid];
     int clipped = 0;
