@@ -25,6 +25,11 @@
 #include "common.h"
 #include "kernels.h"
 
+// The float blends restate OpenCV's expressions operation by operation: no
+// fused multiply-adds in this file (hipcc contracts a*b+c by default, and the
+// __fmul_rn / __fadd_rn spellings alone do not stop it).
+#pragma clang fp contract(off)
+
 namespace unet {
 
 __device__ __forceinline__ int cv_round(float v) { return (int)rintf(v); }
