@@ -23,7 +23,7 @@ c_int, c_int64, c_float, c_double, c_void_p, c_char_p = (
 
 class UnetConfig(ctypes.Structure):
     _fields_ = [("N", c_int), ("H", c_int), ("W", c_int), ("width", c_int), ("n_classes", c_int),
-                ("bn_eps", c_float), ("bn_momentum", c_float), ("attention", c_int)]
+                ("bn_eps", c_float), ("bn_momentum", c_float), ("attention", c_int), ("backbone", c_int)]
 
 
 # name -> (restype, argtypes); every exported symbol of include/unet_hip.h

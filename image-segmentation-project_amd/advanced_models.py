@@ -38,8 +38,33 @@ class _BasicBlock(nn.Module):
         self.stride = stride
 
 
+class _Bottleneck(nn.Module):
+    """Parameter container with torchvision Bottleneck names (resnet50 encoder,
+    advanced_models.py:102-117): conv1 1x1 / bn1 / conv2 3x3 (stride) / bn2 /
+    conv3 1x1 (x4) / bn3 / downsample."""
+
+    def __init__(self, cin: int, planes: int, stride: int):
+        super().__init__()
+        cout = planes * 4
+        self.conv1 = nn.Conv2d(cin, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = nn.Conv2d(planes, cout, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(cout)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = None
+        if stride != 1 or cin != cout:
+            self.downsample = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
+        self.stride = stride
+
+
 def _layer(cin, cout, n, stride):
     return nn.Sequential(_BasicBlock(cin, cout, stride), *[_BasicBlock(cout, cout, 1) for _ in range(n - 1)])
+
+
+def _layer50(cin, planes, n, stride):
+    return nn.Sequential(_Bottleneck(cin, planes, stride), *[_Bottleneck(planes * 4, planes, 1) for _ in range(n - 1)])
 
 
 def _decoder_block(cin, cout):
@@ -74,9 +99,9 @@ class _ChannelAttention(nn.Module):
 class _Plan:
     """Owns one native plan (per input shape) and its persistent workspace."""
 
-    def __init__(self, n, h, w, width, n_classes, device, attention=False):
+    def __init__(self, n, h, w, width, n_classes, device, attention=False, backbone=34):
         lib = _lib.load()
-        cfg = _lib.UnetConfig(n, h, w, width, n_classes, 1e-5, 0.1, 1 if attention else 0)
+        cfg = _lib.UnetConfig(n, h, w, width, n_classes, 1e-5, 0.1, 1 if attention else 0, backbone)
         handle = ctypes.c_void_p()
         _lib.check(lib.unet_plan_create(ctypes.byref(cfg), ctypes.byref(handle)), "unet_plan_create")
         self.lib, self.handle = lib, handle
@@ -174,18 +199,24 @@ class _UNetFunction(torch.autograd.Function):
 
 
 class UNetWithBackbone(nn.Module):
-    """Drop-in for ``advanced_models.UNetWithBackbone`` (resnet34, with or without attention).
+    """Drop-in for ``advanced_models.UNetWithBackbone`` (resnet34 or resnet50,
+    with or without attention).
 
-    ``width`` is a build extension (1 = reference channels); ``backbone`` other
-    than 'resnet34' is a SURVEY.md §8(f) "next" row and raises
+    ``width`` is a build extension (1 = reference channels; resnet34 only).
+    ``backbone='resnet50'`` builds the Bottleneck encoder (256..2048 channels)
+    and its decoder (advanced_models.py:102-130,158-159); 'densenet121' is not
+    runnable in the reference and raises
     ``NotImplementedError``.  ``use_attention=True`` (the reference default)
     adds the AttentionGate / ChannelAttention decoder (advanced_models.py:7-61).
     """
 
     def __init__(self, n_classes=1, backbone="resnet34", pretrained=True, use_attention=True, width=1):
         super().__init__()
-        if backbone != "resnet34":
-            raise NotImplementedError(f"backbone={backbone!r}: only 'resnet34' is built for MI355X (SURVEY.md §8)")
+        if backbone not in ("resnet34", "resnet50"):
+            raise NotImplementedError(f"backbone={backbone!r}: 'resnet34' and 'resnet50' are built for MI355X "
+                                      "(densenet121 is broken in the reference, SURVEY.md §2 row 1)")
+        if backbone == "resnet50" and width != 1:
+            raise NotImplementedError("width != 1 is a resnet34 build extension")
         if n_classes != 1:
             raise NotImplementedError("n_classes must be 1 (binary segmentation, advanced_models.py:160)")
         if pretrained:
@@ -193,35 +224,44 @@ class UNetWithBackbone(nn.Module):
                           "the encoder keeps its random init — load a state_dict instead", RuntimeWarning)
         self.use_attention = use_attention
         self.backbone_name = backbone
+        self._backbone_id = 50 if backbone == "resnet50" else 34
         self.width = width
-        c0, c1, c2, c3 = 64 * width, 128 * width, 256 * width, 512 * width
+        c0 = 64 * width
         self.input_conv = nn.Conv2d(1, c0, kernel_size=7, stride=2, padding=3, bias=False)
         self.bn1 = nn.BatchNorm2d(c0)
         self.relu = nn.ReLU(inplace=True)
         self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
-        self.enc1 = _layer(c0, c0, 3, 1)
-        self.enc2 = _layer(c0, c1, 4, 2)
-        self.enc3 = _layer(c1, c2, 6, 2)
-        self.enc4 = _layer(c2, c3, 3, 2)
-        self.upconv4 = nn.ConvTranspose2d(c3, c2, kernel_size=2, stride=2)
-        self.decoder4 = _decoder_block(2 * c2, c2)
-        self.upconv3 = nn.ConvTranspose2d(c2, c1, kernel_size=2, stride=2)
-        self.decoder3 = _decoder_block(2 * c1, c1)
-        self.upconv2 = nn.ConvTranspose2d(c1, c0, kernel_size=2, stride=2)
-        self.decoder2 = _decoder_block(2 * c0, c0)
-        self.upconv1 = nn.ConvTranspose2d(c0, c0 // 2, kernel_size=2, stride=2)
-        self.decoder1 = _decoder_block(c0 + c0 // 2, c0 // 2)
-        self.upconv0 = nn.ConvTranspose2d(c0 // 2, c0 // 4, kernel_size=2, stride=2)
+        if backbone == "resnet50":  # advanced_models.py:102-130
+            ch = [256, 512, 1024, 2048]
+            self.enc1 = _layer50(64, 64, 3, 1)
+            self.enc2 = _layer50(256, 128, 4, 2)
+            self.enc3 = _layer50(512, 256, 6, 2)
+            self.enc4 = _layer50(1024, 512, 3, 2)
+            up1, d1 = 64, 64
+            att = [(1024, 1024, 512), (512, 512, 256), (256, 256, 128), (64, 64, 32)]
+        else:  # advanced_models.py:72-100
+            ch = [c0, 2 * c0, 4 * c0, 8 * c0]
+            self.enc1 = _layer(ch[0], ch[0], 3, 1)
+            self.enc2 = _layer(ch[0], ch[1], 4, 2)
+            self.enc3 = _layer(ch[1], ch[2], 6, 2)
+            self.enc4 = _layer(ch[2], ch[3], 3, 2)
+            up1, d1 = c0 // 2, c0 // 2
+            att = [(ch[2], ch[2], ch[1]), (ch[1], ch[1], ch[0]), (ch[0], ch[0], c0 // 2), (c0 // 2, c0, c0 // 2)]
+        self.upconv4 = nn.ConvTranspose2d(ch[3], ch[2], kernel_size=2, stride=2)
+        self.decoder4 = _decoder_block(2 * ch[2], ch[2])
+        self.upconv3 = nn.ConvTranspose2d(ch[2], ch[1], kernel_size=2, stride=2)
+        self.decoder3 = _decoder_block(2 * ch[1], ch[1])
+        self.upconv2 = nn.ConvTranspose2d(ch[1], ch[0], kernel_size=2, stride=2)
+        self.decoder2 = _decoder_block(2 * ch[0], ch[0])
+        self.upconv1 = nn.ConvTranspose2d(ch[0], up1, kernel_size=2, stride=2)
+        self.decoder1 = _decoder_block(c0 + up1, d1)
+        self.upconv0 = nn.ConvTranspose2d(d1, c0 // 4, kernel_size=2, stride=2)
         self.conv_final = nn.Conv2d(c0 // 4, n_classes, kernel_size=1)
-        if use_attention:  # advanced_models.py:163-172 (resnet34), registered after conv_final
-            self.attention4 = _AttentionGate(c2, c2, c1)
-            self.attention3 = _AttentionGate(c1, c1, c0)
-            self.attention2 = _AttentionGate(c0, c0, c0 // 2)
-            self.attention1 = _AttentionGate(c0 // 2, c0, c0 // 2)
-            self.ch_attention4 = _ChannelAttention(c2)
-            self.ch_attention3 = _ChannelAttention(c1)
-            self.ch_attention2 = _ChannelAttention(c0)
-            self.ch_attention1 = _ChannelAttention(c0 // 2)
+        if use_attention:  # advanced_models.py:163-183, registered after conv_final
+            for lvl, (fg, fl, fi) in zip((4, 3, 2, 1), att):
+                setattr(self, f"attention{lvl}", _AttentionGate(fg, fl, fi))
+            for lvl, c in zip((4, 3, 2, 1), (ch[2], ch[1], ch[0], d1)):
+                setattr(self, f"ch_attention{lvl}", _ChannelAttention(c))
         self._plans = {}
         self.max_plans = 3  # unpinned native plans (input shapes) kept alive
         self._use_clock = 0
@@ -249,7 +289,7 @@ class UNetWithBackbone(nn.Module):
         key = (n, h, w, x.device)
         plan = self._plans.get(key)
         if plan is None:
-            plan = _Plan(n, h, w, self.width, 1, x.device, self.use_attention)
+            plan = _Plan(n, h, w, self.width, 1, x.device, self.use_attention, self._backbone_id)
             names = [k for k, _ in self.named_parameters()]
             if names != plan.param_names:
                 raise RuntimeError("native parameter table does not match the module's named_parameters()")
@@ -320,7 +360,7 @@ class UNetWithBackbone(nn.Module):
         """Algorithmic FLOPs of one step at input shape [N,1,H,W]."""
         n, _, h, w = x_shape
         lib = _lib.load()
-        cfg = _lib.UnetConfig(n, h, w, self.width, 1, 1e-5, 0.1, 1 if self.use_attention else 0)
+        cfg = _lib.UnetConfig(n, h, w, self.width, 1, 1e-5, 0.1, 1 if self.use_attention else 0, self._backbone_id)
         handle = ctypes.c_void_p()
         _lib.check(lib.unet_plan_create(ctypes.byref(cfg), ctypes.byref(handle)), "unet_plan_create")
         try:

@@ -67,12 +67,24 @@ struct Conv {
   size_t bias_acc = 0;                        // fp64 [kStatRep][Co] (convT bias grads)
 };
 
+// BasicBlock (resnet34): conv1 3x3/s - bn1 - relu - conv2 3x3 - bn2 (+ skip) - relu.
+// Bottleneck (resnet50, torchvision v1.5): conv1 1x1 - bn1 - relu - conv2 3x3/s -
+// bn2 - relu - conv3 1x1 (x4 channels) - bn3 (+ skip) - relu; the block's LAST
+// conv / BN are (conv3, bn3), its middle pair (conv2, bn2, y2 -> h2).
 struct Block {
   int conv1, bn1, conv2, bn2, ds = -1, dsbn = -1;
+  int conv3 = -1, bn3 = -1;             // bottleneck only
   Act in, y1, h, y2, yds, out;
+  Act h2, y3;                           // bottleneck: relu(bn2(y2)), conv3 output
   Act d_out, dy1, dh, dy2, dyds, dres;  // grads
+  Act dh2, dy3, dds;                    // bottleneck: grads of h2 / y3, downsample dgrad (then added)
   Act d_in;                             // == previous block's d_out (or dP0)
   Act skip_add;                         // skip-concat gradient slice for the input (or empty)
+  bool bottleneck() const { return conv3 >= 0; }
+  int last_conv() const { return conv3 >= 0 ? conv3 : conv2; }
+  int last_bn() const { return conv3 >= 0 ? bn3 : bn2; }
+  const Act& last_y() const { return conv3 >= 0 ? y3 : y2; }
+  const Act& last_dy() const { return conv3 >= 0 ? dy3 : dy2; }
 };
 
 struct Dec {
@@ -271,14 +283,22 @@ static int build_plan(unet_plan* p) {
     return 1;
   }
   if (c.n_classes != 1) { set_err("unet_plan_create: only n_classes == 1 is supported"); return 1; }
+  const bool r50 = c.backbone == 50;
+  if (c.backbone != 0 && c.backbone != 34 && c.backbone != 50) {
+    set_err("unet_plan_create: backbone must be 34 (resnet34) or 50 (resnet50)");
+    return 1;
+  }
+  if (r50 && w != 1) { set_err("unet_plan_create: resnet50 is built at width 1 only"); return 1; }
+  // stage output channels (x2..x5): resnet34 64..512, resnet50 (expansion 4) 256..2048
   const int c0 = 64 * w, c1 = 128 * w, c2 = 256 * w, c3 = 512 * w;
-  const int chan[4] = {c0, c1, c2, c3};
+  const int chan[4] = {r50 ? 256 : c0, r50 ? 512 : c1, r50 ? 1024 : c2, r50 ? 2048 : c3};
+  const int planes[4] = {64, 128, 256, 512};
   const int nblk[4] = {3, 4, 6, 3};
 
   // ---- parameters, in reference registration order ----
   p->stem_conv = add_conv(p, "input_conv", L_STEM, 1, c0, 7, 2, 3, false);
   p->stem_bn = add_bn(p, "bn1", c0);
-  struct BlkSpec { int conv1, bn1, conv2, bn2, ds, dsbn, cin, cout, stride, stage; };
+  struct BlkSpec { int conv1, bn1, conv2, bn2, conv3, bn3, ds, dsbn, cin, cout, mid, stride, stage; };
   std::vector<BlkSpec> specs;
   int cin = c0;
   for (int s = 0; s < 4; ++s) {
@@ -287,10 +307,23 @@ static int build_plan(unet_plan* p) {
       const int stride = (b == 0 && s > 0) ? 2 : 1;
       const int cout = chan[s];
       BlkSpec bs;
-      bs.conv1 = add_conv(p, pre + ".conv1", L_CONV, cin, cout, 3, stride, 1, false);
-      bs.bn1 = add_bn(p, pre + ".bn1", cout);
-      bs.conv2 = add_conv(p, pre + ".conv2", L_CONV, cout, cout, 3, 1, 1, false);
-      bs.bn2 = add_bn(p, pre + ".bn2", cout);
+      bs.conv3 = bs.bn3 = -1;
+      if (r50) {  // torchvision Bottleneck: 1x1 -> 3x3/stride -> 1x1 (x4)
+        const int mid = planes[s];
+        bs.conv1 = add_conv(p, pre + ".conv1", L_CONV, cin, mid, 1, 1, 0, false);
+        bs.bn1 = add_bn(p, pre + ".bn1", mid);
+        bs.conv2 = add_conv(p, pre + ".conv2", L_CONV, mid, mid, 3, stride, 1, false);
+        bs.bn2 = add_bn(p, pre + ".bn2", mid);
+        bs.conv3 = add_conv(p, pre + ".conv3", L_CONV, mid, cout, 1, 1, 0, false);
+        bs.bn3 = add_bn(p, pre + ".bn3", cout);
+        bs.mid = mid;
+      } else {
+        bs.conv1 = add_conv(p, pre + ".conv1", L_CONV, cin, cout, 3, stride, 1, false);
+        bs.bn1 = add_bn(p, pre + ".bn1", cout);
+        bs.conv2 = add_conv(p, pre + ".conv2", L_CONV, cout, cout, 3, 1, 1, false);
+        bs.bn2 = add_bn(p, pre + ".bn2", cout);
+        bs.mid = cout;
+      }
       bs.ds = bs.dsbn = -1;
       if (stride != 1 || cin != cout) {
         bs.ds = add_conv(p, pre + ".downsample.0", L_CONV, cin, cout, 1, stride, 0, false);
@@ -306,10 +339,11 @@ static int build_plan(unet_plan* p) {
   struct DecSpec { int up, conv1, bn1, conv2, bn2, upin, upout, skipc, outc; };
   std::vector<DecSpec> dspecs;
   {
-    const int upin[4] = {c3, c2, c1, c0};
-    const int upout[4] = {c2, c1, c0, c0 / 2};
-    const int skipc[4] = {c2, c1, c0, c0};
-    const int outc[4] = {c2, c1, c0, c0 / 2};
+    // advanced_models.py:89-100 (resnet34) / :119-130 (resnet50)
+    const int upin[4] = {chan[3], chan[2], chan[1], chan[0]};
+    const int upout[4] = {chan[2], chan[1], chan[0], r50 ? c0 : c0 / 2};
+    const int skipc[4] = {chan[2], chan[1], chan[0], c0};
+    const int outc[4] = {chan[2], chan[1], chan[0], r50 ? c0 : c0 / 2};
     for (int l = 0; l < 4; ++l) {
       const int lvl = 4 - l;
       DecSpec d;
@@ -324,12 +358,14 @@ static int build_plan(unet_plan* p) {
       dspecs.push_back(d);
     }
   }
-  p->up0_w = add_param(p, "upconv0.weight", {c0 / 2, c0 / 4, 2, 2});
+  const int up0_in = dspecs[3].outc;  // 32 (resnet34) / 64 (resnet50), advanced_models.py:158-159
+  p->up0_w = add_param(p, "upconv0.weight", {up0_in, c0 / 4, 2, 2});
   p->up0_b = add_param(p, "upconv0.bias", {c0 / 4});
   p->fin_w = add_param(p, "conv_final.weight", {c.n_classes, c0 / 4, 1, 1});
   p->fin_b = add_param(p, "conv_final.bias", {c.n_classes});
-  if (c.attention) {  // advanced_models.py:163-172, registered after conv_final
-    const int fi[4] = {c1, c0, c0 / 2, c0 / 2};
+  if (c.attention) {  // advanced_models.py:163-172 / :175-183, registered after conv_final
+    const int fi34[4] = {c1, c0, c0 / 2, c0 / 2}, fi50[4] = {512, 256, 128, 32};
+    const int* fi = r50 ? fi50 : fi34;
     for (int l = 0; l < 4; ++l) {
       const std::string pre = "attention" + std::to_string(4 - l);
       Att t;
@@ -392,7 +428,7 @@ static int build_plan(unet_plan* p) {
   }
   for (auto& cv : p->convs)
     if (cv.kind == L_CONVT) cv.bias_acc = A.take((size_t)kStatRep * cv.Co * sizeof(double));
-  p->head_usum = A.take((size_t)(c0 / 2 * 4 + 1) * sizeof(double));
+  p->head_usum = A.take((size_t)(up0_in * 4 + 1) * sizeof(double));
   for (auto& t : p->atts) {
     t.pbs = A.take(2 * sizeof(double));
     t.cda = A.take((size_t)N * t.C * sizeof(double));
@@ -426,7 +462,7 @@ static int build_plan(unet_plan* p) {
 
   // forward activations
   const int H2 = H / 2, W2 = W / 2, H4 = H / 4, W4 = W / 4;
-  Act cat1 = act(A, N, H2, W2, c0 + c0 / 2);
+  Act cat1 = act(A, N, H2, W2, c0 + dspecs[3].upout);
   p->x1 = c.attention ? act(A, N, H2, W2, c0) : slice(cat1, 0, c0);
   p->y0 = act(A, N, H2, W2, c0);
   p->p0 = act(A, N, H4, W4, c0);
@@ -437,21 +473,30 @@ static int build_plan(unet_plan* p) {
   p->wslab = A.take(2 * p->wslab_bytes);  // two slabs, alternating
   Act cats[4];  // cats[l] for decoder level index l (0 = level 4)
   cats[3] = cat1;
-  cats[2] = act(A, N, H4, W4, 2 * c0);
-  cats[1] = act(A, N, H / 8, W / 8, 2 * c1);
-  cats[0] = act(A, N, H / 16, W / 16, 2 * c2);
-  Act x5 = act(A, N, H / 32, W / 32, c3);
+  cats[2] = act(A, N, H4, W4, 2 * chan[0]);
+  cats[1] = act(A, N, H / 8, W / 8, 2 * chan[1]);
+  cats[0] = act(A, N, H / 16, W / 16, 2 * chan[2]);
+  Act x5 = act(A, N, H / 32, W / 32, chan[3]);
 
   Act prev = p->p0;
   for (size_t i = 0; i < specs.size(); ++i) {
     const BlkSpec& s = specs[i];
     Block b;
     b.conv1 = s.conv1; b.bn1 = s.bn1; b.conv2 = s.conv2; b.bn2 = s.bn2; b.ds = s.ds; b.dsbn = s.dsbn;
+    b.conv3 = s.conv3; b.bn3 = s.bn3;
     const int Hs = H4 >> s.stage, Ws = W4 >> s.stage;
     b.in = prev;
-    b.y1 = act(A, N, Hs, Ws, s.cout);
-    b.h = act(A, N, Hs, Ws, s.cout);
-    b.y2 = act(A, N, Hs, Ws, s.cout);
+    if (b.bottleneck()) {  // conv1 (1x1) at the input resolution, the stride sits on conv2
+      b.y1 = act(A, N, prev.H, prev.W, s.mid);
+      b.h = act(A, N, prev.H, prev.W, s.mid);
+      b.y2 = act(A, N, Hs, Ws, s.mid);
+      b.h2 = act(A, N, Hs, Ws, s.mid);
+      b.y3 = act(A, N, Hs, Ws, s.cout);
+    } else {
+      b.y1 = act(A, N, Hs, Ws, s.cout);
+      b.h = act(A, N, Hs, Ws, s.cout);
+      b.y2 = act(A, N, Hs, Ws, s.cout);
+    }
     if (s.ds >= 0) b.yds = act(A, N, Hs, Ws, s.cout);
     const bool last = (i + 1 == specs.size()) || specs[i + 1].stage != s.stage;
     if (last) {
@@ -534,16 +579,21 @@ static int build_plan(unet_plan* p) {
   }
   for (int l = 0; l < 4; ++l) {
     Dec& d = p->decs[l];
-    d.d_up_in = (l == 0) ? act(A, N, H / 32, W / 32, c3)
+    d.d_up_in = (l == 0) ? act(A, N, H / 32, W / 32, chan[3])
                          : (c.attention ? p->atts[l - 1].d_out2 : p->decs[l - 1].d_out);
   }
   for (auto& b : p->blocks) {
-    const int Hs = b.y1.H, Ws = b.y1.W, C = b.y1.C;
-    b.dy1 = act(A, N, Hs, Ws, C);
-    b.dh = act(A, N, Hs, Ws, C);
-    b.dy2 = act(A, N, Hs, Ws, C);
-    if (b.ds >= 0) b.dyds = act(A, N, Hs, Ws, C);
-    else b.dres = act(A, N, Hs, Ws, C);
+    b.dy1 = act(A, N, b.y1.H, b.y1.W, b.y1.C);
+    b.dh = act(A, N, b.h.H, b.h.W, b.h.C);
+    b.dy2 = act(A, N, b.y2.H, b.y2.W, b.y2.C);
+    if (b.bottleneck()) {
+      b.dh2 = act(A, N, b.h2.H, b.h2.W, b.h2.C);
+      b.dy3 = act(A, N, b.y3.H, b.y3.W, b.y3.C);
+      if (b.ds >= 0) b.dds = act(A, N, b.in.H, b.in.W, b.in.C);
+    }
+    const Act& o = b.out;
+    if (b.ds >= 0) b.dyds = act(A, N, o.H, o.W, o.C);
+    else b.dres = act(A, N, o.H, o.W, o.C);
   }
   // block output grads: last encoder block's d_out = decoder-4's d_up_in
   const int nb = (int)p->blocks.size();
@@ -579,6 +629,10 @@ static int build_plan(unet_plan* p) {
         const Block& b = p->blocks[bi];
         const std::string pre = "enc" + std::to_string(s + 1) + "." + std::to_string(k) + ".";
         nm.push_back({pre + "y1", b.y1}); nm.push_back({pre + "h", b.h}); nm.push_back({pre + "y2", b.y2});
+        if (b.bottleneck()) {
+          nm.push_back({pre + "h2", b.h2}); nm.push_back({pre + "y3", b.y3});
+          nm.push_back({pre + "d.h2", b.dh2}); nm.push_back({pre + "d.y3", b.dy3});
+        }
         if (b.ds >= 0) { nm.push_back({pre + "yds", b.yds}); nm.push_back({pre + "d.yds", b.dyds}); }
         nm.push_back({pre + "out", b.out});
         nm.push_back({pre + "d.out", b.d_out}); nm.push_back({pre + "d.y2", b.dy2});
@@ -630,9 +684,14 @@ static int build_plan(unet_plan* p) {
   }
   for (auto& b : p->blocks) {
     const double px = (double)N * b.y1.H * b.y1.W;
-    fw += 2 * px * p->convs[b.conv1].Ci * p->convs[b.conv1].Co * 9;
-    fw += 2 * px * p->convs[b.conv2].Ci * p->convs[b.conv2].Co * 9;
-    if (b.ds >= 0) fw += 2 * px * p->convs[b.ds].Ci * p->convs[b.ds].Co;
+    auto cf = [&](int ci, const Act& o) {
+      const Conv& cv = p->convs[ci];
+      return 2.0 * N * o.H * o.W * cv.Ci * cv.Co * cv.R * cv.S;
+    };
+    (void)px;
+    fw += cf(b.conv1, b.y1) + cf(b.conv2, b.y2);
+    if (b.bottleneck()) fw += cf(b.conv3, b.y3);
+    if (b.ds >= 0) fw += cf(b.ds, b.yds);
   }
   for (auto& d : p->decs) {
     const double px = (double)N * d.y1.H * d.y1.W;
@@ -644,7 +703,7 @@ static int build_plan(unet_plan* p) {
     const double px = (double)N * p->decs[l].y1.H * p->decs[l].y1.W;
     fw += 2 * px * t.Fi * (t.Fg + t.Fl + 1) + 2.0 * N * 2 * 2 * t.C * t.Cr;
   }
-  fw += 2.0 * N * H2 * W2 * (c0 / 2) * (c0 / 4) * 4;  // upconv0
+  fw += 2.0 * N * H2 * W2 * up0_in * (c0 / 4) * 4;  // upconv0
   fw += 2.0 * N * H * W * (c0 / 4);                    // conv_final
   p->flops_fwd = fw;
   p->flops_train = 3 * fw - stem;
@@ -1045,6 +1104,27 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
   // epilogue (running statistics; residual added there), no BN passes
   const bool fold = !training && p->eval_fold;
   for (auto& b : p->blocks) {
+    if (b.bottleneck()) {  // torchvision Bottleneck (resnet50)
+      if (fold) {
+        RUN(conv_forward(x, b.conv1, b.in, b.h, -1, b.bn1, true));
+        RUN(conv_forward(x, b.conv2, b.h, b.h2, -1, b.bn2, true));
+        if (b.ds >= 0) RUN(conv_forward(x, b.ds, b.in, b.yds, -1, b.dsbn, false));
+        RUN(conv_forward(x, b.conv3, b.h2, b.out, -1, b.bn3, true, b.ds >= 0 ? &b.yds : &b.in));
+        continue;
+      }
+      RUN(conv_forward(x, b.conv1, b.in, b.y1, b.bn1));
+      RUN(bn_apply(x, b.bn1, b.y1, b.h, 0, nullptr, -1, true));
+      RUN(conv_forward(x, b.conv2, b.h, b.y2, b.bn2));
+      RUN(bn_apply(x, b.bn2, b.y2, b.h2, 0, nullptr, -1, true));
+      RUN(conv_forward(x, b.conv3, b.h2, b.y3, b.bn3));
+      if (b.ds >= 0) {
+        RUN(conv_forward(x, b.ds, b.in, b.yds, b.dsbn));
+        RUN(bn_apply(x, b.bn3, b.y3, b.out, 2, &b.yds, b.dsbn, true));
+      } else {
+        RUN(bn_apply(x, b.bn3, b.y3, b.out, 1, &b.in, -1, true));
+      }
+      continue;
+    }
     if (fold) {
       RUN(conv_forward(x, b.conv1, b.in, b.h, -1, b.bn1, true));
       if (b.ds >= 0) RUN(conv_forward(x, b.ds, b.in, b.yds, -1, b.dsbn, false));
@@ -1171,10 +1251,15 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     Block& b = p->blocks[i];
     return bwd_args(x, b.bn1, b.dh, b.h, b.y1, b.dy1, -1, nullptr, nullptr, nullptr, grads);
   };
+  // the block's last BN (bn2 of a BasicBlock, bn3 of a Bottleneck), paired
+  // with the downsample BN when the block has one
   auto blk_bn2 = [&](int i) {
     Block& b = p->blocks[i];
-    if (b.ds >= 0) return bwd_args(x, b.bn2, b.d_out, b.out, b.y2, b.dy2, b.dsbn, &b.yds, &b.dyds, nullptr, grads);
-    return bwd_args(x, b.bn2, b.d_out, b.out, b.y2, b.dy2, -1, nullptr, nullptr, &b.dres, grads);
+    const int bl = b.last_bn();
+    const Act& yl = b.last_y();
+    const Act& dyl = b.last_dy();
+    if (b.ds >= 0) return bwd_args(x, bl, b.d_out, b.out, yl, dyl, b.dsbn, &b.yds, &b.dyds, nullptr, grads);
+    return bwd_args(x, bl, b.d_out, b.out, yl, dyl, -1, nullptr, nullptr, &b.dres, grads);
   };
   // decoder1 .. decoder4 (+ their up-convs)
   for (int l = 3; l >= 0; --l) {
@@ -1252,6 +1337,41 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
   // encoder blocks, deepest first
   for (int i = nb - 1; i >= 0; --i) {
     Block& b = p->blocks[i];
+    if (b.bottleneck()) {
+      RUN(bn_backward(x, b.bn3, blk_bn2(i), fz));  // dY3 (+ dY of the downsample BN)
+      RUN(fork());
+      RUN(conv_wgrad(x, b.conv3, b.dy3, b.h2));
+      if (b.ds >= 0) RUN(conv_wgrad(x, b.ds, b.dyds, b.in));
+      const BnBwdArgs f2 = bwd_args(x, b.bn2, b.dh2, b.h2, b.y2, b.dy2, -1, nullptr, nullptr, nullptr, grads);
+      RUN(conv_dgrad(x, b.conv3, b.dy3, b.dh2, nullptr, fz ? &f2 : nullptr));
+      RUN(bn_backward(x, b.bn2, f2, fz));
+      RUN(fork());
+      RUN(conv_wgrad(x, b.conv2, b.dy2, b.h));
+      const BnBwdArgs f1 = blk_bn1(i);
+      RUN(conv_dgrad(x, b.conv2, b.dy2, b.dh, nullptr, fz ? &f1 : nullptr));
+      RUN(bn_backward(x, b.bn1, f1, fz));
+      RUN(fork());
+      RUN(conv_wgrad(x, b.conv1, b.dy1, b.in));
+      BnBwdArgs fp = {};
+      const BnBwdArgs* fprev = nullptr;
+      if (fz && i > 0) { fp = blk_bn2(i - 1); fprev = &fp; }
+      if (b.ds >= 0) {
+        // downsample (1x1 / stride) data gradient (+ the skip-concat gradient
+        // of the input), then conv1's (1x1) added to it with the previous
+        // block's BN-backward reduction in the epilogue
+        RUN(conv_dgrad(x, b.ds, b.dyds, b.dds, b.skip_add.ld ? &b.skip_add : nullptr));
+        RUN(conv_dgrad(x, b.conv1, b.dy1, b.d_in, &b.dds, fprev));
+      } else {
+        RUN(conv_dgrad(x, b.conv1, b.dy1, b.d_in, fz ? &b.d_out : &b.dres, fprev));
+      }
+      if (i == 13 || i == 7) {
+        const int bk = i == 13 ? 1 : 2;
+        RUN(stream_edge(p, st, x.wst));
+        RUN(unpack_bucket(x, bk, grads));
+        if (p->nevents) CK(hipEventRecord(p->events[bk], x.wst));
+      }
+      continue;
+    }
     RUN(bn_backward(x, b.bn2, blk_bn2(i), fz));
     RUN(fork());
     RUN(conv_wgrad(x, b.conv2, b.dy2, b.h));

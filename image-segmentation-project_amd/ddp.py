@@ -96,12 +96,12 @@ class _NativeDDP:
         red.reduce(grads, wait)
 
 
-def plan_buckets(n: int = 1, h: int = 64, w: int = 64, width: int = 1, attention: bool = False):
+def plan_buckets(n: int = 1, h: int = 64, w: int = 64, width: int = 1, attention: bool = False, backbone: int = 34):
     """(parameter names, flat offsets, bucket ranges) of the native plan for this
     topology, from the C ABI alone (plan creation needs no GPU)."""
     import ctypes
     lib = _lib.load()
-    cfg = _lib.UnetConfig(n, h, w, width, 1, 1e-5, 0.1, 1 if attention else 0)
+    cfg = _lib.UnetConfig(n, h, w, width, 1, 1e-5, 0.1, 1 if attention else 0, backbone)
     handle = ctypes.c_void_p()
     _lib.check(lib.unet_plan_create(ctypes.byref(cfg), ctypes.byref(handle)), "unet_plan_create")
     try:

@@ -44,6 +44,8 @@ typedef struct unet_config {
   float bn_momentum; /* 0.1                                                    */
   int attention;     /* 1: AttentionGate + ChannelAttention decoder            */
                      /*    (use_attention=True, advanced_models.py:7-61,163-172) */
+  int backbone;      /* 34: resnet34 (BasicBlock encoder, advanced_models.py:72-100);     */
+                     /* 50: resnet50 (Bottleneck encoder 256..2048, :102-130,158-159)     */
 } unet_config;
 
 const char* unet_last_error(void);

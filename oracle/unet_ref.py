@@ -3,8 +3,8 @@
 Never imported by the product package.  Every function cites the reference
 file:line (under ``/root/reference``) whose behaviour it restates:
 
-* ``ReferenceUNet`` — ``advanced_models.py:64-100,157-172,197-205,264-357``
-  (``UNetWithBackbone(backbone='resnet34', use_attention=False|True)``;
+* ``ReferenceUNet`` — ``advanced_models.py:64-130,157-183,197-205,264-357``
+  (``UNetWithBackbone(backbone='resnet34'|'resnet50', use_attention=False|True)``;
   ``AttentionGate`` :7-40, ``ChannelAttention`` :43-61) with the
   torchvision ResNet34 encoder (``advanced_models.py:73,81-87``; torchvision's
   ``BasicBlock`` layout: conv1/bn1/conv2/bn2/downsample.{0,1}).
@@ -109,6 +109,36 @@ class BasicBlock(nn.Module):
         return self.relu(h + skip)
 
 
+class Bottleneck(nn.Module):
+    """torchvision ResNet Bottleneck, v1.5 (stride on the 3x3): the resnet50
+    encoder of advanced_models.py:102-117."""
+
+    def __init__(self, cin: int, planes: int, stride: int):
+        super().__init__()
+        cout = planes * 4
+        self.conv1 = nn.Conv2d(cin, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = nn.Conv2d(planes, cout, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(cout)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = None
+        if stride != 1 or cin != cout:
+            self.downsample = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
+
+    def forward(self, x):
+        h = self.relu(self.bn1(self.conv1(x)))
+        h = self.relu(self.bn2(self.conv2(h)))
+        h = self.bn3(self.conv3(h))
+        skip = x if self.downsample is None else self.downsample(x)
+        return self.relu(h + skip)
+
+
+def _stage50(cin: int, planes: int, blocks: int, stride: int) -> nn.Sequential:
+    return nn.Sequential(Bottleneck(cin, planes, stride), *[Bottleneck(planes * 4, planes, 1) for _ in range(blocks - 1)])
+
+
 def _stage(cin: int, cout: int, blocks: int, stride: int) -> nn.Sequential:
     layers = [BasicBlock(cin, cout, stride)]
     layers += [BasicBlock(cout, cout, 1) for _ in range(blocks - 1)]
@@ -159,37 +189,45 @@ class ReferenceUNet(nn.Module):
     the build-defined "wide" config of SURVEY.md §0).
     """
 
-    def __init__(self, n_classes: int = 1, width: int = 1, use_attention: bool = False):
+    def __init__(self, n_classes: int = 1, width: int = 1, use_attention: bool = False, backbone: str = "resnet34"):
         super().__init__()
-        c = [64 * width, 128 * width, 256 * width, 512 * width]
         self.use_attention = use_attention
-        self.input_conv = nn.Conv2d(1, c[0], 7, 2, 3, bias=False)
-        self.bn1 = nn.BatchNorm2d(c[0])
+        c0 = 64 * width
+        self.input_conv = nn.Conv2d(1, c0, 7, 2, 3, bias=False)
+        self.bn1 = nn.BatchNorm2d(c0)
         self.relu = nn.ReLU(inplace=True)
         self.maxpool = nn.MaxPool2d(3, 2, 1)
-        self.enc1 = _stage(c[0], c[0], 3, 1)
-        self.enc2 = _stage(c[0], c[1], 4, 2)
-        self.enc3 = _stage(c[1], c[2], 6, 2)
-        self.enc4 = _stage(c[2], c[3], 3, 2)
+        if backbone == "resnet50":   # advanced_models.py:102-130 (torchvision resnet50 layers)
+            c = [256, 512, 1024, 2048]
+            self.enc1 = _stage50(64, 64, 3, 1)
+            self.enc2 = _stage50(256, 128, 4, 2)
+            self.enc3 = _stage50(512, 256, 6, 2)
+            self.enc4 = _stage50(1024, 512, 3, 2)
+            up1 = d1 = 64
+            att = [(1024, 1024, 512), (512, 512, 256), (256, 256, 128), (64, 64, 32)]   # :175-183
+        else:                        # advanced_models.py:72-100
+            c = [c0, 2 * c0, 4 * c0, 8 * c0]
+            self.enc1 = _stage(c[0], c[0], 3, 1)
+            self.enc2 = _stage(c[0], c[1], 4, 2)
+            self.enc3 = _stage(c[1], c[2], 6, 2)
+            self.enc4 = _stage(c[2], c[3], 3, 2)
+            up1 = d1 = c0 // 2
+            att = [(c[2], c[2], c[1]), (c[1], c[1], c[0]), (c[0], c[0], c0 // 2), (c0 // 2, c0, c0 // 2)]
         self.upconv4 = nn.ConvTranspose2d(c[3], c[2], 2, 2)
         self.decoder4 = decoder_block(2 * c[2], c[2])
         self.upconv3 = nn.ConvTranspose2d(c[2], c[1], 2, 2)
         self.decoder3 = decoder_block(2 * c[1], c[1])
         self.upconv2 = nn.ConvTranspose2d(c[1], c[0], 2, 2)
         self.decoder2 = decoder_block(2 * c[0], c[0])
-        self.upconv1 = nn.ConvTranspose2d(c[0], c[0] // 2, 2, 2)
-        self.decoder1 = decoder_block(c[0] + c[0] // 2, c[0] // 2)
-        self.upconv0 = nn.ConvTranspose2d(c[0] // 2, c[0] // 4, 2, 2)
-        self.conv_final = nn.Conv2d(c[0] // 4, n_classes, 1)
-        if use_attention:   # advanced_models.py:163-172 (resnet34 branch), registered after conv_final
-            self.attention4 = AttentionGate(c[2], c[2], c[1])
-            self.attention3 = AttentionGate(c[1], c[1], c[0])
-            self.attention2 = AttentionGate(c[0], c[0], c[0] // 2)
-            self.attention1 = AttentionGate(c[0] // 2, c[0], c[0] // 2)
-            self.ch_attention4 = ChannelAttention(c[2])
-            self.ch_attention3 = ChannelAttention(c[1])
-            self.ch_attention2 = ChannelAttention(c[0])
-            self.ch_attention1 = ChannelAttention(c[0] // 2)
+        self.upconv1 = nn.ConvTranspose2d(c[0], up1, 2, 2)
+        self.decoder1 = decoder_block(c0 + up1, d1)
+        self.upconv0 = nn.ConvTranspose2d(d1, c0 // 4, 2, 2)          # :158-159
+        self.conv_final = nn.Conv2d(c0 // 4, n_classes, 1)
+        if use_attention:   # advanced_models.py:163-183, registered after conv_final
+            for lvl, (fg, fl, fi) in zip((4, 3, 2, 1), att):
+                setattr(self, f"attention{lvl}", AttentionGate(fg, fl, fi))
+            for lvl, ch in zip((4, 3, 2, 1), (c[2], c[1], c[0], d1)):
+                setattr(self, f"ch_attention{lvl}", ChannelAttention(ch))
 
     def _level(self, lvl: int, skip, up):
         """One decoder level: skip-first concat (+ attention gate / channel attention, :286-334)."""

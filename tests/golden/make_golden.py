@@ -15,7 +15,7 @@ It then checks that ``oracle/`` is ``torch.equal`` to the reference on every
 fixture and writes the vectors.  Nothing from the reference is copied: only
 inputs and outputs are stored.
 
-Usage:  python tests/golden/make_golden.py
+Usage:  python tests/golden/make_golden.py [--only-r50]
 """
 from __future__ import annotations
 
@@ -148,12 +148,59 @@ def _proj(t: torch.Tensor, stream: int) -> float:
     return float((t.detach().double().reshape(-1) * v).sum())
 
 
+def resnet50_fixture(am, ref_losses, oracle, syn):
+    """backbone='resnet50' (advanced_models.py:102-130): the Bottleneck encoder
+    and its decoder, with and without attention, at 2x1x64x64."""
+    x_np, m_np = syn.synthetic_cells(2, 64, 64, seed=4321)
+    x, m = torch.from_numpy(x_np), torch.from_numpy(m_np)
+    out = {"x": x_np, "masks": m_np}
+    for att in (False, True):
+        tag = "att_" if att else ""
+        torch.manual_seed(0)
+        ref = am.UNetWithBackbone(n_classes=1, backbone="resnet50", pretrained=False, use_attention=att)
+        orc = oracle.ReferenceUNet(backbone="resnet50", use_attention=att)
+        rk = [(k, tuple(v.shape)) for k, v in ref.state_dict().items()]
+        ok = [(k, tuple(v.shape)) for k, v in orc.state_dict().items()]
+        assert rk == ok, "resnet50 state_dict layout differs from the reference"
+        sd = oracle.closed_form_state_dict(orc, seed=0)
+        ref.load_state_dict(sd); orc.load_state_dict(sd)
+        ref.train(); orc.train()
+        lr_ = ref(x); lo_ = orc(x)
+        assert torch.equal(lr_, lo_), "resnet50: oracle logits != reference logits"
+        loss_r = ref_losses.get_loss_function({"loss_fn": "bce"})(lr_, m)
+        loss_o = oracle.get_loss_function({"loss_fn": "bce"})(lo_, m)
+        assert torch.equal(loss_r, loss_o)
+        loss_r.backward(); loss_o.backward()
+        gr = dict(ref.named_parameters()); go = dict(orc.named_parameters())
+        for k in gr:
+            assert torch.equal(gr[k].grad, go[k].grad), k
+        out[tag + "n_params"] = np.int64(sum(p.numel() for p in ref.parameters()))
+        out[tag + "logits_train"] = lr_.detach().numpy()
+        out[tag + "loss_bce"] = np.float32(loss_r.item())
+        for k in ("conv_final.weight", "conv_final.bias", "upconv0.weight", "enc4.2.bn3.weight"):
+            out[tag + "grad/" + k] = gr[k].grad.numpy().copy()
+        bref = dict(ref.named_buffers())
+        for k in ("bn1.running_mean", "enc1.0.bn3.running_var", "enc4.2.bn3.running_mean"):
+            out[tag + "buf/" + k] = bref[k].numpy().copy()
+        ref.load_state_dict(sd); orc.load_state_dict(sd)
+        ref.eval(); orc.eval()
+        with torch.no_grad():
+            le = ref(x); lo = orc(x)
+        assert torch.equal(le, lo)
+        out[tag + "logits_eval"] = le.numpy()
+    np.savez_compressed(os.path.join(HERE, "r50_64.npz"), **out)
+    print("r50_64.npz: params", int(out["n_params"]), int(out["att_n_params"]), "bce", out["loss_bce"])
+
+
 def main():
     sys.path.insert(0, REPO)
     torch.set_num_threads(8)
     am, ref_losses, ref_utils, ref_train = _import_reference()
     import oracle
     syn = _load_synthetic()
+    if "--only-r50" in sys.argv:
+        resnet50_fixture(am, ref_losses, oracle, syn)
+        return
 
     # ---------------- base topology at 4x1x64x64 ----------------
     torch.manual_seed(0)
@@ -350,6 +397,7 @@ def main():
     aout["logits_eval"] = le.numpy()
     np.savez_compressed(os.path.join(HERE, "attn64.npz"), **aout)
     print("attn64.npz: params", int(aout["n_params"]), "bce", aout["loss_bce"])
+    resnet50_fixture(am, ref_losses, oracle, syn)
     print("fixtures written; oracle == reference on every case")
 
 

@@ -96,7 +96,9 @@ def test_module_state_dict_equals_reference_layout(pkg):
 
 def test_unsupported_configs_raise(pkg):
     with pytest.raises(NotImplementedError):
-        pkg.UNetWithBackbone(backbone="resnet50", pretrained=False, use_attention=False)
+        pkg.UNetWithBackbone(backbone="densenet121", pretrained=False, use_attention=False)
+    with pytest.raises(NotImplementedError):
+        pkg.UNetWithBackbone(backbone="resnet50", pretrained=False, use_attention=False, width=2)
     with pytest.warns(RuntimeWarning):
         pkg.UNetWithBackbone(pretrained=True, use_attention=False)
 
