@@ -592,6 +592,243 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_hs_kernel(ConvFwdArgs a, int 
 }
 
 // ---------------------------------------------------------------------------
+// stride-2 3x3 / pad-1 data gradient by output parity class (a, b):
+//   dX[2i+a][2j+b] = sum of W[r][s] . dY[i + dr][j + ds] over the taps of the class,
+//   a = 0: r = 1 (dr 0);  a = 1: r = 0 (dr 1), r = 2 (dr 0);  the same for b / s.
+// A block owns class rows i0 .. i0+TI and class columns j0 .. j0+16 of all
+// four classes (a 2TI x 32 tile of dX) and COT dX channels.  Per 32-channel
+// chunk of dY it stages one (TI+1) x 18 dY halo and the chunk's 9 weight taps;
+// each class is an MFMA over that halo at a (dr, ds) shift, so the dY tile
+// crosses L2 -> LDS once for all 9 taps and 4 classes (the implicit-GEMM
+// MODE_TRANS kernel stages it once per class and tap).  Every wave owns RW
+// class rows of all four classes, i.e. the same 9 tap-MFMA sets per row as the
+// stride-1 kernel.  EXT: the block's folded 1x1 / stride-2 downsample dgrad
+// (x2 = dY_ds, w2) rides in the SAME stages (a TI x 16 dY_ds tile + its 1x1
+// weights per chunk, C2 == C) and feeds class (0, 0) only: pixel (2i, 2j) reads
+// dY_ds (i, j).  Epilogue: TileEpi per class.
+// ---------------------------------------------------------------------------
+template <int FN, int RW, int NW, bool EXT>
+__global__ void __launch_bounds__(NW * 64) conv3x3s2_dgrad_kernel(ConvFwdArgs a, int ncb) {
+  constexpr int COT = FN * 16;
+  constexpr int TI = RW * NW;
+  constexpr int HR = TI + 1;
+  constexpr int HPR = (HR * kHW + 15) / 16 * 16;
+  constexpr int HBYTES = HPR * 64;
+  constexpr int WBYTES = 9 * COT * 64;
+  constexpr int DBYTES = EXT ? TI * 16 * 64 : 0;  // dY_ds tile
+  constexpr int D2BYTES = EXT ? COT * 64 : 0;     // 1x1 weights
+  constexpr int STAGE = HBYTES + WBYTES + DBYTES + D2BYTES;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* cst = reinterpret_cast<float*>(smem + 2 * STAGE);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int cob = bid % ncb, tile = bid / ncb;
+  const int co0 = cob * COT;
+  const int tq = a.W >> 4, tp = a.H / TI;  // class grid = the dY grid
+  const int n = tile / (tp * tq);
+  const int rem = tile - n * (tp * tq);
+  const int i0 = (rem / tq) * TI, j0 = (rem % tq) << 4;
+  const int KC = a.C >> 5;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (unsigned)((size_t)a.Cout * 9 * a.C * 2));
+  const __amdgpu_buffer_rsrc_t x2r =
+      make_rsrc(EXT ? a.x2 : a.x, EXT ? (unsigned)((size_t)a.N * a.H * a.W * a.ldx2 * 2) : 0u);
+  const __amdgpu_buffer_rsrc_t w2r = make_rsrc(EXT ? a.w2 : a.w, EXT ? (unsigned)((size_t)a.Cout * a.C2 * 2) : 0u);
+
+  constexpr int H_NINS = HPR / 16, H_PER = (H_NINS + NW - 1) / NW;
+  constexpr int W_NINS = 9 * COT / 16, W_PER = (W_NINS + NW - 1) / NW;
+  constexpr int D_NINS = EXT ? TI : 0, D_PER = EXT ? (D_NINS + NW - 1) / NW : 1;
+  constexpr int W2_NINS = EXT ? COT / 16 : 0, W2_PER = EXT ? (W2_NINS + NW - 1) / NW : 1;
+  unsigned hoff[H_PER], woff[W_PER], doff[D_PER], woff2[W2_PER];
+#pragma unroll
+  for (int k = 0; k < H_PER; ++k) {
+    const int hp = (wave + k * NW) * 16 + (lane >> 2);
+    const int lchunk = (lane & 3) ^ ((hp >> 1) & 2);
+    const int hr = hp / kHW, hc = hp - hr * kHW;
+    const int ih = i0 + hr, iw = j0 + hc;
+    const bool ok = hp < HR * kHW && ih < a.H && iw < a.W;
+    hoff[k] = ok ? (unsigned)(((((size_t)n * a.H + ih) * a.W + iw) * a.ldx + lchunk * 8) * 2) : kOOB;
+  }
+#pragma unroll
+  for (int k = 0; k < W_PER; ++k) {
+    const int rowg = (wave + k * NW) * 16 + (lane >> 2);
+    const int co = rowg % COT, tap = rowg / COT;
+    const int lchunk = (lane & 3) ^ ((co >> 1) & 2);
+    woff[k] = (unsigned)(((co0 + co) * 9 * a.C + tap * a.C + lchunk * 8) * 2);
+  }
+#pragma unroll
+  for (int k = 0; k < D_PER; ++k) {  // dY_ds tile row (class row) = instruction index
+    const int dp = (wave + k * NW) * 16 + (lane >> 2);
+    const int lchunk = (lane & 3) ^ ((dp >> 1) & 2);
+    const int ih = i0 + (dp >> 4), iw = j0 + (dp & 15);
+    doff[k] = EXT ? (unsigned)(((((size_t)n * a.H + ih) * a.W + iw) * a.ldx2 + lchunk * 8) * 2) : kOOB;
+  }
+#pragma unroll
+  for (int k = 0; k < W2_PER; ++k) {
+    const int co = (wave + k * NW) * 16 + (lane >> 2);
+    const int lchunk = (lane & 3) ^ ((co >> 1) & 2);
+    woff2[k] = EXT ? (unsigned)(((co0 + co) * a.C2 + lchunk * 8) * 2) : kOOB;
+  }
+  auto issue = [&](int kt, int b) {
+    char* S = smem + b * STAGE;
+    const unsigned so = (unsigned)kt * 64u;
+#pragma unroll
+    for (int k = 0; k < H_PER; ++k)
+      if (wave + k * NW < H_NINS) glds16s(xr, S + (wave + k * NW) * 1024, hoff[k], so);
+#pragma unroll
+    for (int k = 0; k < W_PER; ++k)
+      if (wave + k * NW < W_NINS) glds16s(wr, S + HBYTES + (wave + k * NW) * 1024, woff[k], so);
+    if constexpr (EXT) {
+#pragma unroll
+      for (int k = 0; k < D_PER; ++k)
+        if (wave + k * NW < D_NINS) glds16s(x2r, S + HBYTES + WBYTES + (wave + k * NW) * 1024, doff[k], so);
+#pragma unroll
+      for (int k = 0; k < W2_PER; ++k)
+        if (wave + k * NW < W2_NINS)
+          glds16s(w2r, S + HBYTES + WBYTES + DBYTES + (wave + k * NW) * 1024, woff2[k], so);
+    }
+  };
+  issue(0, 0);
+  load_epi_constants<COT>(a, cst, co0, tid, NW * 64);
+
+  const int aoff = ws_off(lane & 15, lane >> 4);
+  int boff[RW + 1][2], doffl[RW];
+#pragma unroll
+  for (int h = 0; h < RW + 1; ++h)
+#pragma unroll
+    for (int d = 0; d < 2; ++d) boff[h][d] = ws_off((wave * RW + h) * kHW + d + (lane & 15), lane >> 4);
+#pragma unroll
+  for (int j = 0; j < RW; ++j) doffl[j] = ws_off((wave * RW + j) * 16 + (lane & 15), lane >> 4);
+
+  f32x4 acc[4 * RW][FN];
+#pragma unroll
+  for (int q = 0; q < 4 * RW; ++q)
+#pragma unroll
+    for (int i = 0; i < FN; ++i) acc[q][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // one tap of class c: weight tap (r, s), halo shift (dr, ds)
+  auto tap_mfma = [&](const char* W, const char* Hh, int c, int r, int dr, int s, int ds) {
+    bf16x8 A[FN];
+#pragma unroll
+    for (int i = 0; i < FN; ++i) A[i] = *reinterpret_cast<const bf16x8*>(W + (r * 3 + s) * COT * 64 + i * 1024 + aoff);
+#pragma unroll
+    for (int j = 0; j < RW; ++j) {
+      const bf16x8 B = *reinterpret_cast<const bf16x8*>(Hh + boff[j + dr][ds]);
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+        acc[c * RW + j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B, acc[c * RW + j][i], 0, 0, 0);
+    }
+  };
+  for (int kt = 0; kt < KC; ++kt) {
+    wait_vmcnt<0>();               // stage kt landed (this wave's part) ...
+    __builtin_amdgcn_s_barrier();  // ... everyone's; and stage kt-1 is no longer read
+    if (kt + 1 < KC) issue(kt + 1, (kt + 1) & 1);
+    const char* S = smem + (kt & 1) * STAGE;
+    const char* W = S + HBYTES;
+    tap_mfma(W, S, 0, 1, 0, 1, 0);                                 // (0, 0)
+    tap_mfma(W, S, 1, 1, 0, 0, 1); tap_mfma(W, S, 1, 1, 0, 2, 0);  // (0, 1)
+    tap_mfma(W, S, 2, 0, 1, 1, 0); tap_mfma(W, S, 2, 2, 0, 1, 0);  // (1, 0)
+    tap_mfma(W, S, 3, 0, 1, 0, 1); tap_mfma(W, S, 3, 0, 1, 2, 0);  // (1, 1)
+    tap_mfma(W, S, 3, 2, 0, 0, 1); tap_mfma(W, S, 3, 2, 0, 2, 0);
+    if constexpr (EXT) {  // downsample: class (0, 0), 1x1 weights, no shift
+      const char* D = S + HBYTES + WBYTES;
+      bf16x8 A[FN];
+#pragma unroll
+      for (int i = 0; i < FN; ++i) A[i] = *reinterpret_cast<const bf16x8*>(D + DBYTES + i * 1024 + aoff);
+#pragma unroll
+      for (int j = 0; j < RW; ++j) {
+        const bf16x8 B = *reinterpret_cast<const bf16x8*>(D + doffl[j]);
+#pragma unroll
+        for (int i = 0; i < FN; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B, acc[j][i], 0, 0, 0);
+      }
+    }
+  }
+  float q0[FN][4], q1[FN][4], q2[FN][4];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) q0[i][e] = q1[i][e] = q2[i][e] = 0.f;
+  // one class at a time: its epilogue operands are the only ones live
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    size_t pix[RW];
+    f32x4 ac[RW][FN];
+#pragma unroll
+    for (int j = 0; j < RW; ++j) {
+      const int oh = 2 * (i0 + wave * RW + j) + (c >> 1), ow = 2 * (j0 + (lane & 15)) + (c & 1);
+      pix[j] = ((size_t)n * a.P + oh) * a.Q + ow;
+#pragma unroll
+      for (int i = 0; i < FN; ++i) ac[j][i] = acc[c * RW + j][i];
+    }
+    TileEpi<FN, RW, true, false, false> epi;
+    epi.fetch(a, pix, co0, lane);
+    epi.store(a, ac, pix, co0, lane, cst, q0, q1, q2);
+  }
+  if (a.bb.sums) commit_stats<FN, NW, false>(a, q0, q1, q2, co0, smem);
+}
+
+template <int FN, int RW, int NW, bool EXT>
+static hipError_t launch_s2d(const ConvFwdArgs& a, hipStream_t st) {
+  constexpr int COT = FN * 16, TI = RW * NW;
+  constexpr int HPR = ((TI + 1) * kHW + 15) / 16 * 16;
+  constexpr size_t stage = (size_t)HPR * 64 + 9 * COT * 64 + (EXT ? (size_t)TI * 16 * 64 + COT * 64 : 0);
+  constexpr size_t lds = 2 * stage + kEpiConsts * COT * sizeof(float);
+  static_assert(lds <= 163840, "LDS");
+  static_assert((size_t)NW * COT * 3 * sizeof(float) + sizeof(int) <= 2 * stage, "stats scratch");
+  const int ncb = a.Cout / COT;
+  const int ntiles = a.N * (a.H / TI) * (a.W / 16);
+  char tag[96];
+  std::snprintf(tag, sizeof(tag), "conv3x3s2_dgrad_kernel<%d, %d, %d, %s>", FN, RW, NW, EXT ? "true" : "false");
+  conv_kernel_tag(tag);
+  hipLaunchKernelGGL((conv3x3s2_dgrad_kernel<FN, RW, NW, EXT>), dim3(ntiles * ncb), dim3(NW * 64), lds, st, a, ncb);
+  return hipGetLastError();
+}
+
+template <int FN, int RW, int NW>
+static hipError_t launch_s2d_ext(const ConvFwdArgs& a, hipStream_t st) {
+  return a.x2 ? launch_s2d<FN, RW, NW, true>(a, st) : launch_s2d<FN, RW, NW, false>(a, st);
+}
+
+static int g_s2_disabled = std::getenv("UNET_NO_S2HALO") != nullptr;  // A/B switch for measurements
+
+// 3x3 / stride-2 / pad-1 data gradient (+ the folded 1x1 / s2 downsample
+// dgrad) when the shape is covered; hipErrorNotSupported otherwise (the caller
+// falls back to the implicit-GEMM MODE_TRANS kernel).  a: x = dY [N,H,W,C],
+// y = dX [N,P=2H,Q=2W,Cout], w = dgrad pack [Cout][9][C].
+hipError_t launch_conv3x3s2_dgrad(const ConvFwdArgs& a, hipStream_t st) {
+  if (g_s2_disabled || a.ysplit || a.fold_on || a.stats || a.bias) return hipErrorNotSupported;
+  if (a.R != 3 || a.S != 3 || a.stride != 2 || a.pad != 1) return hipErrorNotSupported;
+  if (a.P != 2 * a.H || a.Q != 2 * a.W || a.W % 16 || a.C % 32 || a.Cout % 64) return hipErrorNotSupported;
+  if (a.ldx % 8 || a.ldy % 4 || (a.x2 && (a.C2 != a.C || a.ldx2 % 8))) return hipErrorNotSupported;
+  if ((a.add && a.ldadd % 4) || (a.bb.sums && (a.bb.y2 || a.bb.ldact % 4 || a.bb.ldy % 4)))
+    return hipErrorNotSupported;
+  if ((size_t)a.N * a.H * a.W * a.ldx * 2 >= 0x80000000ull) return hipErrorNotSupported;
+  if (a.x2 && (size_t)a.N * a.H * a.W * a.ldx2 * 2 >= 0x80000000ull) return hipErrorNotSupported;
+  if ((size_t)a.Cout * 9 * a.C * 2 >= 0x80000000ull) return hipErrorNotSupported;
+  static const int forced = std::getenv("UNET_S2CFG") ? std::atoi(std::getenv("UNET_S2CFG")) : 0;  // tuning
+  auto fits = [&](int ti) { return a.H % ti == 0; };
+  switch (forced) {
+    case 1: if (fits(16)) return launch_s2d_ext<4, 2, 8>(a, st); break;
+    case 2: if (fits(8)) return launch_s2d_ext<4, 1, 8>(a, st); break;
+    case 3: if (fits(4)) return launch_s2d_ext<4, 1, 4>(a, st); break;
+    case 4: if (fits(8)) return launch_s2d_ext<2, 1, 8>(a, st); break;
+    case 5: if (fits(8)) return launch_s2d_ext<2, 2, 4>(a, st); break;
+    case 6: if (fits(4)) return launch_s2d_ext<2, 1, 4>(a, st); break;
+    default: break;
+  }
+  const long long ncb = a.Cout / 64;
+  auto blocks = [&](int ti) { return (long long)a.N * (a.H / ti) * (a.W / 16) * ncb; };
+  // measured (16 x 512^2 Base, UNET_S2CFG sweep): 16-row tiles while they fill
+  // the chip (enc2.0: 51 us, was 79 on the implicit-GEMM kernel), else 32-channel
+  // blocks of 8 rows (enc3.0 36 us, was 49; enc4.0 33 us, was 52)
+  if (fits(16) && blocks(16) >= 256) return launch_s2d_ext<4, 2, 8>(a, st);
+  if (fits(8)) return launch_s2d_ext<2, 1, 8>(a, st);
+  if (fits(4)) return launch_s2d_ext<2, 1, 4>(a, st);
+  return hipErrorNotSupported;
+}
+
+// ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
 template <int NP, int FN, int TH, int NW, bool FLIP>

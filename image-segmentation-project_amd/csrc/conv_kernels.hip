@@ -1627,6 +1627,10 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a0, int mode, hipStream_t st) {
     }
     if (mode == MODE_TRANS) {
       if (a.P % a.stride || a.Q % a.stride) return hipErrorInvalidValue;
+      if (g_cfg_override <= 0) {
+        const hipError_t e = launch_conv3x3s2_dgrad(a, st);
+        if (e != hipErrorNotSupported) return e;
+      }
       a.Pc = a.P / a.stride;
       a.Qc = a.Q / a.stride;
       return launch_glds<MODE_TRANS>(a, a.stride * a.stride, st);

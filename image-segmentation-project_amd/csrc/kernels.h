@@ -122,6 +122,9 @@ hipError_t launch_conv_fwd_v1(const ConvFwdArgs& a, int mode, hipStream_t st);  
 // (conv_halo.hip); mode 0 conv, 1 dgrad.  hipErrorNotSupported if not covered.
 hipError_t launch_conv3x3_ws(const ConvFwdArgs& a, int mode, hipStream_t st);
 void set_conv_ws(int on);
+// 3x3 / stride-2 / pad-1 data gradient by parity class on a shared dY halo
+// (conv_halo.hip), with the optional folded downsample (x2 / w2) range
+hipError_t launch_conv3x3s2_dgrad(const ConvFwdArgs& a, hipStream_t st);
 void set_conv_impl(int glds);  // 1: LDS-DMA pipelined kernels (default), 0: register-staged v1
 void set_conv_config(int cfg);  // 0: automatic tile selection, >0: fixed tile config (tuning)
 hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st);

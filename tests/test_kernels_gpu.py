@@ -114,6 +114,11 @@ CASES_DGRAD = [  # N, Ci, H, Co, R, stride, pad  (forward geometry)
     (4, 256, 32, 256, 3, 1, 1),
     (2, 512, 16, 512, 3, 1, 1),
     (2, 128, 64, 256, 3, 1, 1),
+    # stride-2 parity-class halo dgrad (conv3x3s2_dgrad_kernel): TI = 16, 8, 4
+    (16, 64, 128, 128, 3, 2, 1),
+    (16, 128, 64, 256, 3, 2, 1),
+    (16, 256, 32, 512, 3, 2, 1),
+    (2, 128, 96, 64, 3, 2, 1),
 ]
 
 
