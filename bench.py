@@ -27,6 +27,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md)
+MFMA_FP8_PEAK_TFLOPS = 5000.0  # MI355X dense fp8 (block-scaled e4m3 MFMA, MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -119,6 +120,8 @@ def main():
                     help="use_attention=True decoder (AttentionGate + ChannelAttention, the reference default)")
     ap.add_argument("--width", type=int, default=1,
                     help="channel multiplier: 1 = Base (configs[1]), 2 = Wide 128->1024 (configs[4], bf16 here)")
+    ap.add_argument("--fp8", action="store_true",
+                    help="forward convs with >= 128 input channels in fp8 e4m3 (configs[4] Wide fp8); bwd bf16")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the CPU oracle legs (baseline + mIoU parity)")
@@ -145,7 +148,7 @@ def main():
 
     torch.manual_seed(0)
     model = pkg.UNetWithBackbone(n_classes=1, backbone="resnet34", pretrained=False,
-                                  use_attention=args.attention, width=args.width).to(dev)
+                                  use_attention=args.attention, width=args.width, fp8=args.fp8).to(dev)
     if world > 1:
         ddp.enable_data_parallel(model)
     use_graph = args.graph if args.graph is not None else world == 1
@@ -222,6 +225,7 @@ def main():
     dom = max(by_kernel, key=lambda k: by_kernel[k][0])
     dom_ms, dom_fl, dom_n = by_kernel[dom]
     achieved_tflops = dom_fl / 1e9 / dom_ms
+    dom_peak = MFMA_FP8_PEAK_TFLOPS if dom.startswith("conv_f8_kernel") else MFMA_BF16_PEAK_TFLOPS
     traffic = pmc_traffic(dom)
     line = {
         "metric": "images/sec + mIoU, 512x512 U-Net bf16 at 1/2/4/8 MI355X",
@@ -234,7 +238,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": "fp8-e4m3 fwd convs (C>=128) + bf16" if args.fp8 else "bf16",
         "data": "synthetic (Gaussian cells, seed 1234+rank), random-init weights",
         "miou": round(miou, 6),
         "miou_step0": None if parity is None else round(parity[0], 6),
@@ -244,9 +248,9 @@ def main():
                    + " U-Net resnet34 " + ("attention" if args.attention else "no-attention")
                    + " train step (fwd+bce+bwd+Adam)",
                    "global_batch": args.batch * world, "image": f"{args.size}x{args.size}",
-                   "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "achieved": round(achieved_tflops, 2), "peak": MFMA_BF16_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(achieved_tflops / MFMA_BF16_PEAK_TFLOPS, 4),
+                   "parallelism": f"dp{world}", "fp8": bool(args.fp8)},
+        "roofline": {"bound": "mfma", "achieved": round(achieved_tflops, 2), "peak": dom_peak,
+                     "unit": "TFLOP/s", "frac": round(achieved_tflops / dom_peak, 4),
                      "traffic": traffic,
                      "kernel": dom, "launches_per_step": dom_n,
                      "avg_launch_us": round(dom_ms / dom_n * 1e3, 2),

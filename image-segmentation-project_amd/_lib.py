@@ -23,7 +23,8 @@ c_int, c_int64, c_float, c_double, c_void_p, c_char_p = (
 
 class UnetConfig(ctypes.Structure):
     _fields_ = [("N", c_int), ("H", c_int), ("W", c_int), ("width", c_int), ("n_classes", c_int),
-                ("bn_eps", c_float), ("bn_momentum", c_float), ("attention", c_int), ("backbone", c_int)]
+                ("bn_eps", c_float), ("bn_momentum", c_float), ("attention", c_int), ("backbone", c_int),
+                ("fp8", c_int)]
 
 
 # name -> (restype, argtypes); every exported symbol of include/unet_hip.h
@@ -60,6 +61,11 @@ SIGNATURES = {
     "unet_conv_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]
                       + [c_int] * 12 + [c_void_p]),
     "unet_conv_wgrad": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p] + [c_int] * 12 + [c_void_p]),
+    "unet_f8_quantize": (c_int, [c_void_p, c_int, c_int, c_int64, c_void_p, c_void_p, c_int, c_void_p]),
+    "unet_f8_pack_weight": (c_int, [c_void_p] + [c_int] * 4 + [c_void_p, c_void_p, c_int, c_void_p]),
+    "unet_f8_roll": (c_int, [c_void_p, c_int, c_void_p]),
+    "unet_conv_fwd_f8": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                                 c_int, c_void_p] + [c_int] * 11 + [c_void_p]),
     "unet_conv_wgrad_slab": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int64]
                              + [c_int] * 12 + [c_void_p]),
     "unet_convt_wgrad_slab": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int64]

@@ -99,9 +99,10 @@ class _ChannelAttention(nn.Module):
 class _Plan:
     """Owns one native plan (per input shape) and its persistent workspace."""
 
-    def __init__(self, n, h, w, width, n_classes, device, attention=False, backbone=34):
+    def __init__(self, n, h, w, width, n_classes, device, attention=False, backbone=34, fp8=False):
         lib = _lib.load()
-        cfg = _lib.UnetConfig(n, h, w, width, n_classes, 1e-5, 0.1, 1 if attention else 0, backbone)
+        cfg = _lib.UnetConfig(n, h, w, width, n_classes, 1e-5, 0.1, 1 if attention else 0, backbone,
+                              1 if fp8 else 0)
         handle = ctypes.c_void_p()
         _lib.check(lib.unet_plan_create(ctypes.byref(cfg), ctypes.byref(handle)), "unet_plan_create")
         self.lib, self.handle = lib, handle
@@ -208,10 +209,17 @@ class UNetWithBackbone(nn.Module):
     runnable in the reference and raises
     ``NotImplementedError``.  ``use_attention=True`` (the reference default)
     adds the AttentionGate / ChannelAttention decoder (advanced_models.py:7-61).
+    ``fp8=True`` (build extension, BASELINE configs[4] "Wide fp8"; resnet34
+    without attention): forward convs with >= 128 input channels run on the
+    fp8 e4m3 block-scaled MFMA with per-tensor delayed scaling; BN, the loss
+    and the whole backward stay bf16/fp32.
     """
 
-    def __init__(self, n_classes=1, backbone="resnet34", pretrained=True, use_attention=True, width=1):
+    def __init__(self, n_classes=1, backbone="resnet34", pretrained=True, use_attention=True, width=1, fp8=False):
         super().__init__()
+        if fp8 and (backbone != "resnet34" or use_attention):
+            raise NotImplementedError("fp8=True is built for the resnet34 U-Net without attention")
+        self.fp8 = bool(fp8)
         if backbone not in ("resnet34", "resnet50"):
             raise NotImplementedError(f"backbone={backbone!r}: 'resnet34' and 'resnet50' are built for MI355X "
                                       "(densenet121 is broken in the reference, SURVEY.md §2 row 1)")
@@ -289,7 +297,7 @@ class UNetWithBackbone(nn.Module):
         key = (n, h, w, x.device)
         plan = self._plans.get(key)
         if plan is None:
-            plan = _Plan(n, h, w, self.width, 1, x.device, self.use_attention, self._backbone_id)
+            plan = _Plan(n, h, w, self.width, 1, x.device, self.use_attention, self._backbone_id, self.fp8)
             names = [k for k, _ in self.named_parameters()]
             if names != plan.param_names:
                 raise RuntimeError("native parameter table does not match the module's named_parameters()")
@@ -360,7 +368,8 @@ class UNetWithBackbone(nn.Module):
         """Algorithmic FLOPs of one step at input shape [N,1,H,W]."""
         n, _, h, w = x_shape
         lib = _lib.load()
-        cfg = _lib.UnetConfig(n, h, w, self.width, 1, 1e-5, 0.1, 1 if self.use_attention else 0, self._backbone_id)
+        cfg = _lib.UnetConfig(n, h, w, self.width, 1, 1e-5, 0.1, 1 if self.use_attention else 0, self._backbone_id,
+                              1 if self.fp8 else 0)
         handle = ctypes.c_void_p()
         _lib.check(lib.unet_plan_create(ctypes.byref(cfg), ctypes.byref(handle)), "unet_plan_create")
         try:

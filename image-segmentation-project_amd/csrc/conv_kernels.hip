@@ -649,6 +649,153 @@ conv_glds_kernel(ConvFwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// fp8 (OCP e4m3) implicit-GEMM forward conv (BASELINE configs[4]).  The
+// MODE_FWD LDS-DMA pipeline with 128-channel fp8 K tiles: a tile row is 128 B,
+// the same byte image and swizzle as a 64-channel bf16 tile, so staging,
+// padding (kOOB zero-fill, also for the channel tail of C % 128) and the
+// epilogue are unchanged.  v_mfma_scale_f32_16x16x128_f8f6f4 (format 0 = e4m3
+// for both operands): each lane feeds 32 consecutive K bytes of its row (two
+// 16-B chunks, 2g and 2g+1 for lane group g) — the same k assignment for A
+// and B, so the dot product covers the K tile whatever the hardware's internal
+// k order — at 2x the bf16 MFMA rate; the per-tensor power-of-two scales are
+// its e8m0 block scales (fp8.hip), so the accumulators hold the fp32 conv.
+// ---------------------------------------------------------------------------
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+template <int BM, int BN, int NS, int WM, int WN>
+__global__ void __launch_bounds__(WM * WN * 64)
+conv_f8_kernel(ConvFwdArgs a) {
+  constexpr int BK = 128;              // e4m3 elements (= bytes) per K tile row
+  constexpr int NW = WM * WN;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  static_assert((NW == 4 || NW == 8) && FM >= 1 && FN >= 1, "tiling");
+  constexpr int CPR = 8;               // 16-B chunks per row
+  constexpr int RPI = 8;               // rows per wave instruction
+  constexpr int A_INS = BM / RPI / NW;
+  constexpr int B_INS = (BN / RPI + NW - 1) / NW;
+  static_assert(BM % (RPI * NW) == 0, "A rows per wave");
+  constexpr int LPS = A_INS + B_INS;
+  constexpr int A_BYTES = BM * BK;
+  constexpr int B_BYTES = ((BN + RPI * NW - 1) / (RPI * NW)) * RPI * NW * BK;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % WM, wn = wave / WM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int nblk = bid % a.nblocks, mblk = bid / a.nblocks;
+  const int Mtot = a.N * a.P * a.Q;
+  const int m0 = mblk * BM, n0 = nblk * BN;
+  const int cchunks = (a.C + BK - 1) / BK;
+  const int KT = a.R * a.S * cchunks;
+  const int Ktot = a.R * a.S * a.C;
+  const int sx = a.f8x->code, sw = a.f8w->code;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx));
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (unsigned)((size_t)a.Cout * Ktot));
+
+  const int lrow = lane / CPR, lslot = lane % CPR;
+  int an[A_INS], aa[A_INS], ab[A_INS], ach[A_INS];
+#pragma unroll
+  for (int j = 0; j < A_INS; ++j) {
+    const int row = (wave * A_INS + j) * RPI + lrow;
+    ach[j] = swz_chunk<64>(row, lslot);
+    const int m = m0 + row;
+    if (m < Mtot) {
+      const int n = m / (a.P * a.Q);
+      const int rem = m - n * (a.P * a.Q);
+      an[j] = n;
+      aa[j] = rem / a.Q;
+      ab[j] = rem - aa[j] * a.Q;
+    } else {
+      an[j] = -1; aa[j] = 0; ab[j] = 0;
+    }
+  }
+  int bch[B_INS];
+  unsigned bbase[B_INS];
+#pragma unroll
+  for (int j = 0; j < B_INS; ++j) {
+    const int row = (wave * B_INS + j) * RPI + lrow;
+    bch[j] = swz_chunk<64>(row, lslot);
+    const bool ok = row < BN && n0 + row < a.Cout;
+    bbase[j] = ok ? (unsigned)((n0 + row) * Ktot) : kOOB;
+  }
+
+  auto issue = [&](int kt, int buf) {
+    const int cc = kt % cchunks;
+    const int tap = kt / cchunks;
+    const int r = tap / a.S, s = tap - r * a.S;
+    const int c0 = cc * BK;
+    char* As = smem + buf * STAGE;
+    char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int j = 0; j < A_INS; ++j) {
+      const int ih = aa[j] * a.stride - a.pad + r;
+      const int iw = ab[j] * a.stride - a.pad + s;
+      const int c = c0 + ach[j] * 16;
+      unsigned off = kOOB;
+      if (an[j] >= 0 && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W && c < a.C)
+        off = (unsigned)(((an[j] * a.H + ih) * a.W + iw) * a.ldx + c);
+      glds16(xr, As + (wave * A_INS + j) * 1024, off);
+    }
+#pragma unroll
+    for (int j = 0; j < B_INS; ++j) {
+      const int c = c0 + bch[j] * 16;
+      const unsigned off = (bbase[j] == kOOB || c >= a.C) ? kOOB : bbase[j] + (unsigned)((r * a.S + s) * a.C + c);
+      glds16(wr, Bs + (wave * B_INS + j) * 1024, off);
+    }
+  };
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int st = 0; st < NS - 1; ++st)
+    if (st < KT) issue(st, st);
+
+  const int g = lane >> 4;
+  for (int kt = 0; kt < KT; ++kt) {
+    const int ahead = KT - 1 - kt;
+    if (ahead >= NS - 2) wait_vmcnt<(NS - 2) * LPS>();
+    else if (NS > 3 && ahead == 1) wait_vmcnt<LPS>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (kt + NS - 1 < KT) issue(kt + NS - 1, (kt + NS - 1) % NS);
+    const char* As = smem + (kt % NS) * STAGE;
+    const char* Bs = As + A_BYTES;
+    i32x8 wf[FN], xf[FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+      const int row = wn * WTN + i * 16 + (lane & 15);
+      const uint4 lo = *reinterpret_cast<const uint4*>(Bs + frag_off<64>(row, 2 * g));
+      const uint4 hi = *reinterpret_cast<const uint4*>(Bs + frag_off<64>(row, 2 * g + 1));
+      wf[i] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+    }
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      const int row = wm * WTM + j * 16 + (lane & 15);
+      const uint4 lo = *reinterpret_cast<const uint4*>(As + frag_off<64>(row, 2 * g));
+      const uint4 hi = *reinterpret_cast<const uint4*>(As + frag_off<64>(row, 2 * g + 1));
+      xf[j] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+    }
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wf[i], xf[j], acc[i][j], 0, 0, 0, sw, 0, sx);
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+  ConvFwdArgs e = a;
+  e.Pc = a.P; e.Qc = a.Q;
+  conv_epilogue<MODE_FWD, BN, WM, WN, FM, FN>(e, acc, smem, m0, n0, Mtot, 0, 0);
+}
+
+// ---------------------------------------------------------------------------
 // weight gradient
 // ---------------------------------------------------------------------------
 // [pixel][channel] tile, 32-B units XOR-swizzled per row so that every
@@ -1591,6 +1738,35 @@ static hipError_t launch_glds(const ConvFwdArgs& a, int classes, hipStream_t st)
   if (bk64 && nblk(256, 64) >= 512) return launch_glds_cfg<MODE, 256, 64, 64, 2, 4, 2>(a, classes, st);
   return bk64 ? launch_glds_cfg<MODE, 128, 64, 64, 2, 2, 2>(a, classes, st)
               : launch_glds_cfg<MODE, 128, 64, 32, 3, 2, 2>(a, classes, st);
+}
+
+template <int BM, int BN, int NS, int WM, int WN>
+static hipError_t launch_f8_cfg(const ConvFwdArgs& a0, hipStream_t st) {
+  ConvFwdArgs a = a0;
+  a.nblocks = (a.Cout + BN - 1) / BN;
+  const int M = a.N * a.P * a.Q;
+  a.mblocks = (M + BM - 1) / BM;
+  a.Pc = a.P; a.Qc = a.Q;
+  constexpr int NW = WM * WN, RPI = 8;
+  constexpr size_t B_ROWS = ((BN + RPI * NW - 1) / (RPI * NW)) * RPI * NW;
+  size_t lds = (size_t)NS * (BM + B_ROWS) * 128;
+  const size_t red = (size_t)WM * BN * 3 * sizeof(float) + 16;
+  if (red > lds) lds = red;
+  set_kernel_tag("conv_f8_kernel<%d, %d, %d, %d, %d>", BM, BN, NS, WM, WN);
+  hipLaunchKernelGGL((conv_f8_kernel<BM, BN, NS, WM, WN>), dim3(a.mblocks * a.nblocks), dim3(NW * 64), lds, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_conv_fwd_f8(const ConvFwdArgs& a, hipStream_t st) {
+  if (!a.f8x || !a.f8w || a.C % 16 || a.ldx % 16 || a.ysplit || a.bb.sums || a.x2) return hipErrorInvalidValue;
+  if ((size_t)a.N * a.H * a.W * a.ldx >= 0x80000000ull) return hipErrorInvalidValue;
+  if ((size_t)a.Cout * a.R * a.S * a.C >= 0x80000000ull) return hipErrorInvalidValue;
+  const long long M = (long long)a.N * a.P * a.Q;
+  auto nblk = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((a.Cout + bn - 1) / bn); };
+  if (a.Cout <= 64) return launch_f8_cfg<256, 64, 3, 4, 2>(a, st);
+  if (nblk(256, 128) >= 512) return launch_f8_cfg<256, 128, 2, 4, 2>(a, st);
+  if (nblk(128, 128) >= 256) return launch_f8_cfg<128, 128, 3, 2, 2>(a, st);
+  return launch_f8_cfg<64, 128, 3, 2, 2>(a, st);
 }
 
 static bool g_use_glds = std::getenv("UNET_CONV_V1") == nullptr;  // A/B switch for measurements

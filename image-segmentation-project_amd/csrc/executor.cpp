@@ -65,6 +65,17 @@ struct Conv {
   int kind, Ci, Co, R, S, stride, pad;
   size_t pk_fwd = 0, pk_dgrad = 0, wacc = 0;  // ws offsets
   size_t bias_acc = 0;                        // fp64 [kStatRep][Co] (convT bias grads)
+  bool f8 = false;                            // forward in fp8 e4m3 (cfg.fp8, C >= 128)
+  size_t f8w = 0;                             // ws offset: e4m3 [Co][R*S*Ci]
+  int f8st = -1;                              // F8State index of the weight
+};
+
+// fp8 forward: the e4m3 copy of one conv input activation (quantized once per
+// forward, before its first fp8 consumer)
+struct F8Act {
+  size_t src = 0; int C = 0;  // the bf16 activation (ws offset, channels)
+  size_t q = 0;               // ws offset: dense e4m3 [npix][C]
+  int st = -1;                // F8State index
 };
 
 // BasicBlock (resnet34): conv1 3x3/s - bn1 - relu - conv2 3x3 - bn2 (+ skip) - relu.
@@ -174,6 +185,13 @@ struct unet_plan {
   // eval forward: BN folded into the conv epilogues (UNET_NO_EVAL_FOLD=1: separate BN passes, A/B only)
   bool eval_fold = std::getenv("UNET_NO_EVAL_FOLD") == nullptr;
   double flops_fwd = 0, flops_train = 0;
+  // fp8 forward (cfg.fp8): per-tensor delayed-amax states (fp8.hip) for the
+  // conv weights and activations; the first forward calibrates
+  std::vector<F8Act> f8acts;
+  std::vector<char> f8_done;  // per F8Act: quantized in the current forward
+  size_t f8st = 0;            // ws offset of the F8State array
+  int f8n = 0;
+  bool f8_calibrated = false;
   std::vector<std::pair<std::string, Act>> named;  // debug / test introspection
   // per-launch HIP-event profiler (unet_profile_*): one record per kernel
   struct ProfRec { std::string name; double flops; int e0, e1; std::string kernel; };
@@ -289,6 +307,10 @@ static int build_plan(unet_plan* p) {
     return 1;
   }
   if (r50 && w != 1) { set_err("unet_plan_create: resnet50 is built at width 1 only"); return 1; }
+  if (c.fp8 && (r50 || c.attention)) {
+    set_err("unet_plan_create: the fp8 forward is built for the resnet34 U-Net without attention (Wide / Base)");
+    return 1;
+  }
   // stage output channels (x2..x5): resnet34 64..512, resnet50 (expansion 4) 256..2048
   const int c0 = 64 * w, c1 = 128 * w, c2 = 256 * w, c3 = 512 * w;
   const int chan[4] = {r50 ? 256 : c0, r50 ? 512 : c1, r50 ? 1024 : c2, r50 ? 2048 : c3};
@@ -559,6 +581,35 @@ static int build_plan(unet_plan* p) {
     p->atts[3].x = p->x1;
   }
 
+  // fp8 forward: e4m3 weight packs and input copies of every conv with C >= 128
+  if (c.fp8) {
+    auto f8_input = [&](int ci, const Act& in) {
+      Conv& cv = p->convs[ci];
+      if (cv.kind != L_CONV || cv.Ci < 128 || cv.Ci % 16 || in.ld % 8) return;
+      cv.f8 = true;
+      cv.f8w = A.take((size_t)cv.Co * cv.Ci * cv.R * cv.S);
+      cv.f8st = p->f8n++;
+      for (auto& f : p->f8acts)
+        if (f.src == in.off && f.C == in.C) return;
+      F8Act f;
+      f.src = in.off; f.C = in.C;
+      f.q = A.take((size_t)N * in.H * in.W * in.C);
+      f.st = p->f8n++;
+      p->f8acts.push_back(f);
+    };
+    for (auto& b : p->blocks) {
+      f8_input(b.conv1, b.in);
+      f8_input(b.conv2, b.h);
+      if (b.ds >= 0) f8_input(b.ds, b.in);
+    }
+    for (auto& d : p->decs) {
+      f8_input(d.conv1, d.cat);
+      f8_input(d.conv2, d.h);
+    }
+    p->f8st = A.take((size_t)p->f8n * sizeof(F8State));
+    p->f8_done.assign(p->f8acts.size(), 0);
+  }
+
   // backward gradient tensors
   for (int l = 3; l >= 0; --l) {
     Dec& d = p->decs[l];
@@ -790,6 +841,26 @@ int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for
   a.N = x.p->cfg.N; a.H = in.H; a.W = in.W; a.C = cv.Ci;
   a.P = out.H; a.Q = out.W; a.Cout = cv.Co;
   a.R = cv.R; a.S = cv.S; a.stride = cv.stride; a.pad = cv.pad;
+  if (cv.f8) {  // e4m3 operands: quantize the input once per forward, block-scaled MFMA
+    unet_plan* p = x.p;
+    int fi = -1;
+    for (int i = 0; i < (int)p->f8acts.size(); ++i)
+      if (p->f8acts[i].src == in.off && p->f8acts[i].C == in.C) fi = i;
+    if (fi < 0) { set_err("fp8 conv without a registered input"); return 1; }
+    const F8Act& f = p->f8acts[fi];
+    F8State* sts = x.W<F8State>(p->f8st);
+    if (!p->f8_done[fi]) {
+      ProfScope pq(p, x.st, "f8_quant " + pname(x, cv.w), 0);
+      CK(launch_f8_quant_act(x.A(in), in.ld, in.C, (int64_t)a.N * in.H * in.W, x.W<uint8_t>(f.q), sts + f.st,
+                             p->f8_calibrated ? 0 : 1, x.st));
+      p->f8_done[fi] = 1;
+    }
+    a.x = reinterpret_cast<const bf16_t*>(x.W<uint8_t>(f.q)); a.ldx = in.C;
+    a.w = reinterpret_cast<const bf16_t*>(x.W<uint8_t>(cv.f8w));
+    a.f8x = sts + f.st; a.f8w = sts + cv.f8st;
+    CK(launch_conv_fwd_f8(a, x.st));
+    return 0;
+  }
   CK(launch_conv_fwd(a, cv.kind == L_CONVT ? MODE_SHUF : MODE_FWD, x.st));
   return 0;
 }
@@ -1046,6 +1117,17 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
   Ctx x{p, ws, prm, buf, st, training};
   const int N = p->cfg.N;
   CK(hipMemsetAsync(ws + p->zero_fwd_off, 0, p->zero_fwd_bytes, st));
+  if (p->f8n) {  // fp8 scale states: calibrate on the plan's first forward, else roll
+    if (!p->f8_calibrated) CK(hipMemsetAsync(ws + p->f8st, 0, (size_t)p->f8n * sizeof(F8State), st));
+    else CK(launch_f8_roll(x.W<F8State>(p->f8st), p->f8n, st));
+    std::fill(p->f8_done.begin(), p->f8_done.end(), 0);
+    for (auto& cv : p->convs)
+      if (cv.f8) {
+        ProfScope ps(p, st, "f8_pack " + pname(x, cv.w), 0);
+        CK(launch_f8_pack_w(prm[cv.w], cv.Co, cv.Ci, cv.R, cv.S, x.W<uint8_t>(cv.f8w), x.W<F8State>(p->f8st) + cv.f8st,
+                            p->f8_calibrated ? 0 : 1, st));
+      }
+  }
   // pack weights (fp32 torch layout -> bf16 kernel layouts)
   {
     PackTable t;
@@ -1060,7 +1142,7 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
       if (cv.kind == L_STEM) {
         t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_fwd), PK_STEM, cv.Co, 1, 7, 7};
       } else if (cv.kind == L_CONV) {
-        t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_fwd), PK_CONV_FWD, cv.Co, cv.Ci, cv.R, cv.S};
+        if (!cv.f8) t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_fwd), PK_CONV_FWD, cv.Co, cv.Ci, cv.R, cv.S};
         if (t.n == kMaxPack) RUN(flush());
         if (training) t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_dgrad), PK_CONV_DGRAD, cv.Co, cv.Ci, cv.R, cv.S};
       } else {
@@ -1520,7 +1602,9 @@ int unet_forward(unet_plan* p, const float* image, const float* const* params, f
                  void* workspace, float* logits, int training, hipStream_t stream) {
   API_GUARD({
     if (!p || !image || !params || !buffers || !workspace || !logits) { set_err("null argument"); return 1; }
-    return run_forward(p, image, params, buffers, reinterpret_cast<char*>(workspace), logits, training, stream);
+    const int r = run_forward(p, image, params, buffers, reinterpret_cast<char*>(workspace), logits, training, stream);
+    if (r == 0 && p->f8n) p->f8_calibrated = true;
+    return r;
   })
 }
 
@@ -1616,6 +1700,36 @@ int unet_conv_fwd(const void* x, int ldx, const void* w, void* y, int ldy, const
   a.R = R; a.S = S; a.stride = stride; a.pad = pad;
   if (mode < 0 || mode > 2) { set_err("bad mode"); return 1; }
   CK(launch_conv_fwd(a, mode, stream));
+  return 0;
+}
+
+int unet_f8_quantize(const void* x, int ld, int C, int64_t npix, void* q, void* state, int calibrate,
+                     hipStream_t stream) {
+  CK(launch_f8_quant_act((const bf16_t*)x, ld, C, npix, (uint8_t*)q, (F8State*)state, calibrate, stream));
+  return 0;
+}
+
+int unet_f8_pack_weight(const float* w, int Co, int Ci, int R, int S, void* dst, void* state, int calibrate,
+                        hipStream_t stream) {
+  CK(launch_f8_pack_w(w, Co, Ci, R, S, (uint8_t*)dst, (F8State*)state, calibrate, stream));
+  return 0;
+}
+
+int unet_f8_roll(void* states, int n, hipStream_t stream) {
+  CK(launch_f8_roll((F8State*)states, n, stream));
+  return 0;
+}
+
+int unet_conv_fwd_f8(const void* xq, int ldx, const void* wq, const void* state_x, const void* state_w, void* y,
+                     int ldy, const float* bias, const void* addend, int ldadd, double* stats, int N, int H, int W,
+                     int C, int P, int Q, int Cout, int R, int S, int stride, int pad, hipStream_t stream) {
+  ConvFwdArgs a = {};
+  a.x = (const bf16_t*)xq; a.ldx = ldx; a.w = (const bf16_t*)wq; a.y = (bf16_t*)y; a.ldy = ldy;
+  a.f8x = (const F8State*)state_x; a.f8w = (const F8State*)state_w;
+  a.bias = bias; a.add = (const bf16_t*)addend; a.ldadd = ldadd; a.stats = stats;
+  a.N = N; a.H = H; a.W = W; a.C = C; a.P = P; a.Q = Q; a.Cout = Cout;
+  a.R = R; a.S = S; a.stride = stride; a.pad = pad;
+  CK(launch_conv_fwd_f8(a, stream));
   return 0;
 }
 

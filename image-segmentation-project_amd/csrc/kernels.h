@@ -55,6 +55,10 @@ struct BnBwdArgs {
   float* coef;                       // [5][C]: k1, mean dZ, mean dZ*xhat, k1b, mean dZ*xhat2
   int64_t npix; int C; int relu;
 };
+// fp8 per-tensor scale state (fp8.hip): amax of the previous step (the scale
+// in use), amax accumulating this step (float bits), e8m0 dequant code 127 - e
+struct F8State { unsigned prev_bits; unsigned cur_bits; int code; int pad; };
+
 struct ConvFwdArgs {
   const bf16_t* x; int ldx;      // input NHWC bf16, channel stride ldx (stem: fp32 [N,H,W])
   const bf16_t* w;               // packed weights [Cout][R*S*C] (stem: [64][64])
@@ -81,6 +85,9 @@ struct ConvFwdArgs {
   // channel from the running statistics of `fold` (BnLaunch, training = 0);
   // act = ReLU when fold_relu.  `add` (forward) is the block's residual.
   BnLaunch fold; int fold_on; int fold_relu;
+  // fp8 forward (launch_conv_fwd_f8): x / w are e4m3 bytes (x dense, ldx = C;
+  // w packed [Cout][R*S*C]) whose dequant codes the kernel reads from f8x / f8w
+  const F8State* f8x; const F8State* f8w;
   int N, H, W, C;                // input geometry (C = GEMM reduction channels)
   int P, Q, Cout;                // output geometry
   int R, S, stride, pad;
@@ -128,6 +135,15 @@ hipError_t launch_conv3x3s2_dgrad(const ConvFwdArgs& a, hipStream_t st);
 void set_conv_impl(int glds);  // 1: LDS-DMA pipelined kernels (default), 0: register-staged v1
 void set_conv_config(int cfg);  // 0: automatic tile selection, >0: fixed tile config (tuning)
 hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st);
+// fp8 e4m3 implicit-GEMM forward conv (MODE_FWD geometry, any R/S/stride/pad,
+// C % 16 == 0), block-scaled MFMA dequantizing with the F8State codes
+hipError_t launch_conv_fwd_f8(const ConvFwdArgs& a, hipStream_t st);
+// fp8.hip: delayed-amax quantization of activations / conv weights
+hipError_t launch_f8_roll(F8State* s, int n, hipStream_t st);
+hipError_t launch_f8_quant_act(const bf16_t* x, int ld, int C, int64_t npix, uint8_t* q, F8State* s, int calibrate,
+                               hipStream_t st);
+hipError_t launch_f8_pack_w(const float* w, int Co, int Ci, int R, int S, uint8_t* dst, F8State* s, int calibrate,
+                            hipStream_t st);
 // ConvTranspose2d(k2,s2) weight gradient (XLOAD_SHUF): dy = X [N,P,Q,Ci] (Cout = Ci),
 // x = dY [N,H=2P,W=2Q,Co] with C = 4*Co; dw [Ci][4][Co]
 hipError_t launch_convt_wgrad(const ConvWgradArgs& a, hipStream_t st);

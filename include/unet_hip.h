@@ -46,6 +46,10 @@ typedef struct unet_config {
                      /*    (use_attention=True, advanced_models.py:7-61,163-172) */
   int backbone;      /* 34: resnet34 (BasicBlock encoder, advanced_models.py:72-100);     */
                      /* 50: resnet50 (Bottleneck encoder 256..2048, :102-130,158-159)     */
+  int fp8;           /* 1: forward convs with >= 128 input channels in fp8 e4m3 (per-tensor */
+                     /*    delayed scaling, block-scaled MFMA); backward stays bf16.        */
+                     /*    Build extension for BASELINE configs[4] (Wide fp8); resnet34,   */
+                     /*    no attention.  The reference trains in fp32 only.               */
 } unet_config;
 
 const char* unet_last_error(void);
@@ -128,6 +132,25 @@ int unet_conv_wgrad_slab(const void* dy, int lddy, const void* x, int ldx, float
                          int S, int stride, int pad, int stem, hipStream_t stream);
 int unet_convt_wgrad_slab(const void* dy, int lddy, const void* x, int ldx, float* dw, void* slab,
                           int64_t slab_bytes, int N, int H, int W, int Ci, int Co, hipStream_t stream);
+/* ---- fp8 e4m3 forward conv (BASELINE.json configs[4]; no reference counterpart:
+ * the reference's convs are fp32 torch.nn.Conv2d, advanced_models.py:72-100) ----
+ * state: 16-B scale state {amax prev (float bits), amax this step, e8m0 code,
+ * pad}, zeroed before first use; calibrate=1 measures amax before quantizing.
+ * q = sat448(v * 2^e) with 2 * amax_prev * 2^e <= 448, code = 127 - e.
+ * unet_f8_quantize: bf16 [npix][C] (stride ld) -> dense e4m3 [npix][C].
+ * unet_f8_pack_weight: fp32 [Co][Ci][R][S] -> e4m3 [Co][R][S][Ci].
+ * unet_f8_roll: prev <- this step's amax (if any), this step's amax <- 0.
+ * unet_conv_fwd_f8: y = conv(dequant(xq), dequant(wq)) (+bias, +addend, BN
+ * sums) as unet_conv_fwd mode 0, K = R*S*C in e4m3 on the block-scaled MFMA. */
+int unet_f8_quantize(const void* x, int ld, int C, int64_t npix, void* q, void* state, int calibrate,
+                     hipStream_t stream);
+int unet_f8_pack_weight(const float* w, int Co, int Ci, int R, int S, void* dst, void* state, int calibrate,
+                        hipStream_t stream);
+int unet_f8_roll(void* states, int n, hipStream_t stream);
+int unet_conv_fwd_f8(const void* xq, int ldx, const void* wq, const void* state_x, const void* state_w, void* y,
+                     int ldy, const float* bias, const void* addend, int ldadd, double* stats, int N, int H,
+                     int W, int C, int P, int Q, int Cout, int R, int S, int stride, int pad,
+                     hipStream_t stream);
 /* tile configuration of the implicit-GEMM conv kernels: 0 automatic (default),
  * >0 a fixed configuration from the tuning table (scripts/tune_conv.py) */
 int unet_set_conv_config(int cfg);
