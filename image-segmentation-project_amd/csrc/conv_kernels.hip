@@ -767,14 +767,8 @@ conv_f8_kernel(ConvFwdArgs a) {
     if (kt + NS - 1 < KT) issue(kt + NS - 1, (kt + NS - 1) % NS);
     const char* As = smem + (kt % NS) * STAGE;
     const char* Bs = As + A_BYTES;
-    i32x8 wf[FN], xf[FM];
-#pragma unroll
-    for (int i = 0; i < FN; ++i) {
-      const int row = wn * WTN + i * 16 + (lane & 15);
-      const uint4 lo = *reinterpret_cast<const uint4*>(Bs + frag_off<64>(row, 2 * g));
-      const uint4 hi = *reinterpret_cast<const uint4*>(Bs + frag_off<64>(row, 2 * g + 1));
-      wf[i] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
-    }
+    // all FM pixel fragments, then one weight fragment at a time (register budget)
+    i32x8 xf[FM];
 #pragma unroll
     for (int j = 0; j < FM; ++j) {
       const int row = wm * WTM + j * 16 + (lane & 15);
@@ -783,10 +777,15 @@ conv_f8_kernel(ConvFwdArgs a) {
       xf[j] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
     }
 #pragma unroll
-    for (int i = 0; i < FN; ++i)
+    for (int i = 0; i < FN; ++i) {
+      const int row = wn * WTN + i * 16 + (lane & 15);
+      const uint4 lo = *reinterpret_cast<const uint4*>(Bs + frag_off<64>(row, 2 * g));
+      const uint4 hi = *reinterpret_cast<const uint4*>(Bs + frag_off<64>(row, 2 * g + 1));
+      const i32x8 wf = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
 #pragma unroll
       for (int j = 0; j < FM; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wf[i], xf[j], acc[i][j], 0, 0, 0, sw, 0, sx);
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wf, xf[j], acc[i][j], 0, 0, 0, sw, 0, sx);
+    }
   }
   wait_vmcnt<0>();
   __syncthreads();
@@ -1763,7 +1762,18 @@ hipError_t launch_conv_fwd_f8(const ConvFwdArgs& a, hipStream_t st) {
   if ((size_t)a.Cout * a.R * a.S * a.C >= 0x80000000ull) return hipErrorInvalidValue;
   const long long M = (long long)a.N * a.P * a.Q;
   auto nblk = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((a.Cout + bn - 1) / bn); };
+  static const int forced = std::getenv("UNET_F8CFG") ? std::atoi(std::getenv("UNET_F8CFG")) : 0;  // tuning
+  switch (forced) {
+    case 1: return launch_f8_cfg<256, 64, 3, 4, 2>(a, st);
+    case 2: return launch_f8_cfg<256, 128, 2, 4, 2>(a, st);
+    case 3: return launch_f8_cfg<128, 128, 3, 2, 2>(a, st);
+    case 4: return launch_f8_cfg<256, 256, 2, 2, 4>(a, st);
+    case 5: return launch_f8_cfg<128, 256, 2, 2, 4>(a, st);
+    default: break;
+  }
   if (a.Cout <= 64) return launch_f8_cfg<256, 64, 3, 4, 2>(a, st);
+  if (a.Cout >= 256 && nblk(256, 256) >= 256) return launch_f8_cfg<256, 256, 2, 2, 4>(a, st);
+  if (a.Cout >= 256 && nblk(128, 256) >= 256) return launch_f8_cfg<128, 256, 2, 2, 4>(a, st);
   if (nblk(256, 128) >= 512) return launch_f8_cfg<256, 128, 2, 4, 2>(a, st);
   if (nblk(128, 128) >= 256) return launch_f8_cfg<128, 128, 3, 2, 2>(a, st);
   return launch_f8_cfg<64, 128, 3, 2, 2>(a, st);

@@ -85,14 +85,14 @@ __global__ void __launch_bounds__(256) f8_quant_act_kernel(const bf16_t* x, int 
                                                            uint8_t* q, F8State* s) {
   const int e = f8_exponent(s->prev_bits);
   if (blockIdx.x == 0 && threadIdx.x == 0) s->code = 127 - e;
-  const int cpr = C >> 3;
-  const int64_t units = npix * cpr;
+  const unsigned cpr = (unsigned)C >> 3;
+  const unsigned units = (unsigned)(npix * cpr);  // < 2^31 (launcher)
   float m = 0.f;
-  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t px = u / cpr;
-    const int c = (int)(u - px * cpr) << 3;
+  for (unsigned u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += gridDim.x * blockDim.x) {
+    const unsigned px = u / cpr;
+    const unsigned c = (u - px * cpr) << 3;
     float f[8];
-    unpack8(*reinterpret_cast<const uint4*>(x + px * ld + c), f);
+    unpack8(*reinterpret_cast<const uint4*>(x + (size_t)px * ld + c), f);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       m = fmaxf(m, fabsf(f[k]));
@@ -101,34 +101,30 @@ __global__ void __launch_bounds__(256) f8_quant_act_kernel(const bf16_t* x, int 
     uint2 o;
     o.x = f8_pack4(f[0], f[1], f[2], f[3]);
     o.y = f8_pack4(f[4], f[5], f[6], f[7]);
-    *reinterpret_cast<uint2*>(q + px * C + c) = o;
+    *reinterpret_cast<uint2*>(q + (size_t)px * C + c) = o;
   }
   f8_amax_commit(m, &s->cur_bits);
 }
 
 // conv weights fp32 [Co][Ci][RS] -> e4m3 [Co][RS][Ci] (the forward pack layout
-// of PK_CONV_FWD); 4 input channels per thread
+// of PK_CONV_FWD): one thread per (co, ci) reads its RS taps (a contiguous run;
+// neighbouring threads' runs are adjacent) and writes one byte per tap
+// (neighbouring threads: neighbouring bytes)
 __global__ void __launch_bounds__(256) f8_pack_w_kernel(const float* w, int Co, int Ci, int RS, uint8_t* dst,
                                                         F8State* s) {
   const int e = f8_exponent(s->prev_bits);
   if (blockIdx.x == 0 && threadIdx.x == 0) s->code = 127 - e;
-  const int cq = Ci >> 2;
-  const int64_t units = (int64_t)Co * RS * cq;
+  const unsigned units = (unsigned)Co * Ci;
   float m = 0.f;
-  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += (int64_t)gridDim.x * blockDim.x) {
-    const int ci = (int)(u % cq) << 2;
-    const int64_t r = u / cq;
-    const int t = (int)(r % RS);
-    const int co = (int)(r / RS);
-    const float* src = w + ((int64_t)co * Ci + ci) * RS + t;
-    float f[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      f[k] = src[(int64_t)k * RS];
-      m = fmaxf(m, fabsf(f[k]));
+  for (unsigned u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += gridDim.x * blockDim.x) {
+    const unsigned co = u / Ci, ci = u - co * Ci;
+    const float* src = w + (size_t)u * RS;
+    uint8_t* d = dst + (size_t)co * RS * Ci + ci;
+    for (int t = 0; t < RS; ++t) {
+      const float v = src[t];
+      m = fmaxf(m, fabsf(v));
+      d[(size_t)t * Ci] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(f8_sat(ldexpf(v, e)), 0.f, 0, false) & 0xff);
     }
-    *reinterpret_cast<unsigned*>(dst + ((int64_t)co * RS + t) * Ci + ci) =
-        f8_pack4(ldexpf(f[0], e), ldexpf(f[1], e), ldexpf(f[2], e), ldexpf(f[3], e));
   }
   f8_amax_commit(m, &s->cur_bits);
 }
@@ -147,7 +143,7 @@ hipError_t launch_f8_roll(F8State* s, int n, hipStream_t st) {
 
 hipError_t launch_f8_quant_act(const bf16_t* x, int ld, int C, int64_t npix, uint8_t* q, F8State* s, int calibrate,
                                hipStream_t st) {
-  if (C % 16 || ld % 8) return hipErrorInvalidValue;
+  if (C % 16 || ld % 8 || npix * (C >> 3) >= 0x7fffffffLL) return hipErrorInvalidValue;
   const int g = grid_for(npix * (C >> 3));
   if (calibrate) {
     hipLaunchKernelGGL(f8_amax_act_kernel, dim3(g), dim3(256), 0, st, x, ld, C, npix, s);
@@ -162,12 +158,13 @@ hipError_t launch_f8_pack_w(const float* w, int Co, int Ci, int R, int S, uint8_
                             hipStream_t st) {
   if (Ci % 16) return hipErrorInvalidValue;
   const int64_t n = (int64_t)Co * Ci * R * S;
+  if (n >= 0x7fffffffLL) return hipErrorInvalidValue;
   if (calibrate) {
     hipLaunchKernelGGL(f8_amax_f32_kernel, dim3(grid_for(n)), dim3(256), 0, st, w, n, s);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(f8_pack_w_kernel, dim3(grid_for(n / 4)), dim3(256), 0, st, w, Co, Ci, R * S, dst, s);
+  hipLaunchKernelGGL(f8_pack_w_kernel, dim3(grid_for((int64_t)Co * Ci)), dim3(256), 0, st, w, Co, Ci, R * S, dst, s);
   return hipGetLastError();
 }
 

@@ -16,10 +16,13 @@ ap.add_argument("--size", type=int, default=512)
 ap.add_argument("--top", type=int, default=40)
 ap.add_argument("--all", action="store_true")
 ap.add_argument("--attention", action="store_true")
+ap.add_argument("--width", type=int, default=1)
+ap.add_argument("--fp8", action="store_true")
 args = ap.parse_args()
 
 torch.manual_seed(0)
-m = pkg.UNetWithBackbone(pretrained=False, use_attention=args.attention).cuda().train()
+m = pkg.UNetWithBackbone(pretrained=False, use_attention=args.attention, width=args.width,
+                         fp8=args.fp8).cuda().train()
 xs, ms = pkg.synthetic_cells(args.batch, args.size, args.size, seed=1234)
 x, y = torch.from_numpy(xs).cuda(), torch.from_numpy(ms).cuda()
 opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-5)
