@@ -1244,9 +1244,9 @@ __device__ __forceinline__ long long slab_dw_index(const SlabLayout& L, long lon
     if (c >= L.cmax || co >= L.Cout) return -1;
     return (long long)co * L.Krow + (long long)tap * L.C + c;
   }
-  // SLAB_STEM: one block per split, 4 waves of 32 co x 32 k
+  // SLAB_STEM: one block per (split, 64-channel group blk), 4 waves of 32 co x 32 k
   const int i = frag >> 1, j = frag & 1, wm = wave & 1, wn = wave >> 1;
-  return (long long)(wm * 32 + i * 16 + 4 * g + e) * 64 + wn * 32 + j * 16 + li;
+  return (long long)(blk * 64 + wm * 32 + i * 16 + 4 * g + e) * 64 + wn * 32 + j * 16 + li;
 }
 
 // dW = sum over the splits of the slab, bit-reproducible: a block covers
@@ -1364,8 +1364,9 @@ __global__ void __launch_bounds__(256, 2) stem_fwd_kernel(ConvFwdArgs a, int row
   const int total_rows = a.N * a.P * ((a.Q + 255) >> 8);  // units
   const int r0 = xcd_remap(blockIdx.x, gridDim.x) * rows_per_block;
   const int r1 = min(total_rows, r0 + rows_per_block);
-  {  // packed weights [64][64] bf16 -> swizzled LDS rows
-    const uint4* wsrc = reinterpret_cast<const uint4*>(a.w);
+  const int cg = blockIdx.y * 64;  // 64-channel output group (Wide stem: 2 groups)
+  {  // packed weights [64][64] bf16 of the group -> swizzled LDS rows
+    const uint4* wsrc = reinterpret_cast<const uint4*>(a.w + (size_t)cg * 64);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int i = tid + j * 256, co = i >> 3, ch = i & 7;
@@ -1424,7 +1425,7 @@ __global__ void __launch_bounds__(256, 2) stem_fwd_kernel(ConvFwdArgs a, int row
     for (int j = 0; j < 4; ++j) {
       const int px = wave * 64 + j * 16 + (lane & 15);
       if (px < t.Qs) {
-        bf16_t* yrow = a.y + (t.row * a.Q + t.q0 + px) * a.ldy;
+        bf16_t* yrow = a.y + (t.row * a.Q + t.q0 + px) * a.ldy + cg;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int co = i * 16 + ((lane >> 4) << 2);
@@ -1466,13 +1467,13 @@ __global__ void __launch_bounds__(256, 2) stem_fwd_kernel(ConvFwdArgs a, int row
     float s0 = 0.f, s1 = 0.f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) { s0 += red[(w * 64 + tid) * 2]; s1 += red[(w * 64 + tid) * 2 + 1]; }
-    double* rep = a.stats + (size_t)(blockIdx.x % kStatRep) * 2 * 64;
+    double* rep = a.stats + (size_t)(blockIdx.x % kStatRep) * 2 * a.Cout + cg;
     atomicAdd(rep + tid, (double)s0);
-    atomicAdd(rep + 64 + tid, (double)s1);
+    atomicAdd(rep + a.Cout + tid, (double)s1);
   }
   if (a.bn.ticket) {
     int* flag = reinterpret_cast<int*>(smem + 4 * 64 * 2 * sizeof(float));
-    if (last_block_arrive(a.bn.ticket, gridDim.x, flag, tid < 64)) bn_finalize(a.bn);
+    if (last_block_arrive(a.bn.ticket, gridDim.x * gridDim.y, flag, tid < 64)) bn_finalize(a.bn);
   }
 }
 
@@ -1490,6 +1491,7 @@ __global__ void __launch_bounds__(256, 2) stem_wgrad_kernel(ConvWgradArgs a, int
   const int total_rows = a.N * a.P * ((a.Q + 255) >> 8);  // units (stem_unit)
   const int r0 = xcd_remap(blockIdx.x, gridDim.x) * rows_per_block;
   const int r1 = min(total_rows, r0 + rows_per_block);
+  const int cg = blockIdx.y * 64;  // 64-channel output group (Wide stem: 2 groups)
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1501,7 +1503,7 @@ __global__ void __launch_bounds__(256, 2) stem_wgrad_kernel(ConvWgradArgs a, int
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int i = tid + j * 256, px = i >> 3, c8 = i & 7;
-      dyv[j] = px < t.Qs ? *reinterpret_cast<const uint4*>(a.dy + (t.row * a.Q + t.q0 + px) * a.lddy + c8 * 8)
+      dyv[j] = px < t.Qs ? *reinterpret_cast<const uint4*>(a.dy + (t.row * a.Q + t.q0 + px) * a.lddy + cg + c8 * 8)
                          : make_uint4(0, 0, 0, 0);
     }
     stem_fetch(img, t, a.H, a.W, pf);
@@ -1550,8 +1552,9 @@ __global__ void __launch_bounds__(256, 2) stem_wgrad_kernel(ConvWgradArgs a, int
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
   }
-  if (a.slab && gridDim.x > 1) {  // one split per block (SLAB_STEM), summed by the reduce
-    f32x4* dst = reinterpret_cast<f32x4*>(a.slab) + (size_t)blockIdx.x * 1024 + (size_t)wave * 256 + lane;
+  if (a.slab && gridDim.x > 1) {  // one split per block row (SLAB_STEM), summed by the reduce
+    f32x4* dst = reinterpret_cast<f32x4*>(a.slab) + ((size_t)blockIdx.x * gridDim.y + blockIdx.y) * 1024 +
+                 (size_t)wave * 256 + lane;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1566,7 +1569,7 @@ __global__ void __launch_bounds__(256, 2) stem_wgrad_kernel(ConvWgradArgs a, int
       const int k = wn * 32 + j * 16 + li;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int co = wm * 32 + i * 16 + 4 * g + e;
+        const int co = cg + wm * 32 + i * 16 + 4 * g + e;
         if (a.slab) a.dw[co * 64 + k] = acc[i][j][e];
         else atomicAdd(a.dw + co * 64 + k, acc[i][j][e]);
       }
@@ -1586,30 +1589,31 @@ static long long slab_split_cap(const ConvWgradArgs& a, long long bytes_per_spli
 }
 
 hipError_t launch_stem_fwd(const ConvFwdArgs& a, hipStream_t st) {
-  if (a.Cout != 64 || a.R != 7 || a.stride != 2 || a.pad != 3) return hipErrorInvalidValue;
+  if (a.Cout % 64 || a.R != 7 || a.stride != 2 || a.pad != 3 || a.ldy % 4) return hipErrorInvalidValue;
   const int rows = a.N * a.P * ((a.Q + 255) / 256);  // 256-pixel units
   const int per = std::max(1, (rows + 511) / 512);  // ~2 blocks per CU
   const size_t lds = 64 * 128 + 256 * 128 + 7 * kStemPatchW * 2;
   set_kernel_tag("stem_fwd_kernel");
-  hipLaunchKernelGGL(stem_fwd_kernel, dim3((rows + per - 1) / per), dim3(256), lds, st, a, per);
+  hipLaunchKernelGGL(stem_fwd_kernel, dim3((rows + per - 1) / per, a.Cout / 64), dim3(256), lds, st, a, per);
   return hipGetLastError();
 }
 
 hipError_t launch_stem_wgrad(const ConvWgradArgs& a, hipStream_t st) {
-  if (a.Cout != 64 || a.R != 7 || a.stride != 2 || a.pad != 3) return hipErrorInvalidValue;
+  if (a.Cout % 64 || a.R != 7 || a.stride != 2 || a.pad != 3 || a.lddy % 8) return hipErrorInvalidValue;
+  const int groups = a.Cout / 64;
   const int rows = a.N * a.P * ((a.Q + 255) / 256);  // 256-pixel units
-  int per = std::max(1, (rows + 511) / 512);  // ~2 blocks per CU
+  int per = std::max(1, (rows * groups + 511) / 512);  // ~2 blocks per CU
   // one register-native 64x64 partial (16 KiB) per block
-  const long long cap = slab_split_cap(a, 1024 * 16);
+  const long long cap = slab_split_cap(a, 1024 * 16 * groups);
   while ((rows + per - 1) / per > cap) ++per;
   const int blocks = (rows + per - 1) / per;
   const size_t lds = 2 * 256 * 128 + 7 * kStemPatchW * 2;
   set_kernel_tag("stem_wgrad_kernel");
-  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(blocks), dim3(256), lds, st, a, per);
+  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(blocks, groups), dim3(256), lds, st, a, per);
   if (a.slab && blocks > 1) {
     SlabLayout L = {};
-    L.kind = SLAB_STEM; L.splits = blocks; L.blocks = 1; L.nw = 4; L.nf = 4; L.units = 1024;
-    L.Cout = 64; L.C = 64; L.Krow = 64; L.cmax = 64;
+    L.kind = SLAB_STEM; L.splits = blocks; L.blocks = groups; L.nw = 4; L.nf = 4; L.units = 1024LL * groups;
+    L.Cout = a.Cout; L.C = 64; L.Krow = 64; L.cmax = 64;
     g_pending = PendingReduce{a.slab, a.dw, L};
   }
   return hipGetLastError();
@@ -1792,7 +1796,7 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a0, int mode, hipStream_t st) {
   if (a0.fold_on && (mode != MODE_FWD || a0.stats || a0.bb.sums || !g_use_glds)) return hipErrorInvalidValue;
   // dedicated stem kernel: 64 output channels (Base); the Wide stem (128) takes
   // the generic implicit-GEMM path below
-  if (g_use_glds && mode == MODE_STEM && a0.Cout == 64) return launch_stem_fwd(a0, st);
+  if (g_use_glds && mode == MODE_STEM && a0.Cout % 64 == 0) return launch_stem_fwd(a0, st);
   if (mode == MODE_SHUF) {  // convT k2s2 forward: a0 holds the transposed-conv geometry
     if (!g_use_glds || a0.R != 2 || a0.S != 2 || a0.stride != 2 || a0.pad != 0 || a0.Cout % 4 || a0.C % 32 ||
         a0.P != 2 * a0.H || a0.Q != 2 * a0.W || a0.stats || a0.add || a0.bb.sums)
@@ -1973,7 +1977,7 @@ hipError_t launch_convt_wgrad(const ConvWgradArgs& a0, hipStream_t st) {
 
 hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st) {
   if (stem)
-    return g_use_glds && a.Cout == 64 ? launch_stem_wgrad(a, st) : launch_wgrad_cfg<XLOAD_STEM, 64, 64, 64, 2, 2>(a, st);
+    return g_use_glds && a.Cout % 64 == 0 ? launch_stem_wgrad(a, st) : launch_wgrad_cfg<XLOAD_STEM, 64, 64, 64, 2, 2>(a, st);
   if (g_use_glds && a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.C % 32 == 0 && a.P == a.H &&
       a.Q == a.W && (size_t)a.N * a.H * a.W * a.ldx * 2 < 0x80000000ull &&
       (size_t)a.N * a.P * a.Q * a.lddy * 2 < 0x80000000ull) {

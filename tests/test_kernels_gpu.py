@@ -207,9 +207,8 @@ def test_convT_wgrad(L, cuda):
     close(out, w.grad, rel=2e-3)
 
 
-@pytest.mark.parametrize("N,H", [(2, 64), (1, 1024)])
-def test_stem_fwd_and_wgrad(L, N, H, cuda):
-    Co = 64
+@pytest.mark.parametrize("N,H,Co", [(2, 64, 64), (1, 1024, 64), (2, 64, 128)])  # 128: Wide stem (2 groups)
+def test_stem_fwd_and_wgrad(L, N, H, Co, cuda):
     g = torch.Generator().manual_seed(6)
     img = torch.rand(N, 1, H, H, generator=g)
     w = torch.randn(Co, 1, 7, 7, generator=g) / 7.0
@@ -358,6 +357,7 @@ SLAB_CASES = [  # N, Ci, H, Co, R, stride, pad, stem  -- every wgrad kernel fami
     (2, 64, 32, 128, 3, 2, 1, 0),    # implicit-GEMM wgrad, stride 2
     (2, 64, 32, 128, 1, 2, 0, 0),    # 1x1 downsample
     (4, 1, 128, 64, 7, 2, 3, 1),     # 7x7 stem (one partial per block)
+    (4, 1, 128, 128, 7, 2, 3, 1),    # Wide 7x7 stem (two channel groups per split)
 ]
 
 
