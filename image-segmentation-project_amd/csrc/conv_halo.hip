@@ -481,9 +481,11 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
       mfma_panel<FN, RW, NP * COT * 64, FLIP>(acc, wl + p * COT * 64, H + p * PANEL, aoff, boff);
     if (!PREF) epi.fetch(a, pix, co0, lane);
     epi.landed();
-    epi.store(a, acc, pix, co0, lane, cst, q0, q1, q2);
-    wait_vmcnt<0>();               // the next tile's halo has landed (this wave's part)
+    wait_vmcnt<0>();               // the next tile's halo (issued before this tile's MFMAs) has landed ...
     __builtin_amdgcn_s_barrier();  // ... everyone's part; buffer b is free for reuse
+    // the stores go out AFTER the wait: they drain under the next tile's MFMAs
+    // instead of being waited for here (vmcnt counts stores too)
+    epi.store(a, acc, pix, co0, lane, cst, q0, q1, q2);
   }
   if (a.stats || a.bb.sums) commit_stats<FN, NW, false>(a, q0, q1, q2, co0, smem);
 }
