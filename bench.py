@@ -56,14 +56,15 @@ def pmc_traffic(kernel: str):
     return None
 
 
-def cpu_baseline(batch: int, h: int, steps: int, threads: int, width: int = 1, attention: bool = False):
+def cpu_baseline(batch: int, h: int, steps: int, threads: int, width: int = 1, attention: bool = False,
+                 backbone: str = "resnet34"):
     """Time the oracle (fp32 torch-CPU restatement of the reference path) on host cores."""
     import oracle
     torch.set_num_threads(threads)
     pkg = importlib.import_module("image-segmentation-project_amd")
     xs, ms = pkg.synthetic_cells(batch, h, h, seed=1234)
     x, y = torch.from_numpy(xs), torch.from_numpy(ms)
-    m = oracle.ReferenceUNet(width=width, use_attention=attention)
+    m = oracle.ReferenceUNet(width=width, use_attention=attention, backbone=backbone)
     m.load_state_dict(oracle.closed_form_state_dict(m))
     m.train()
     opt = oracle.make_adam(m)
@@ -76,6 +77,56 @@ def cpu_baseline(batch: int, h: int, steps: int, threads: int, width: int = 1, a
     return {"value": round(batch * steps / dt, 3), "unit": "images/sec", "cores": threads, "kind": "port",
             "sample": f"{steps} fp32 train steps (fwd+bce+bwd+Adam) of batch {batch} at {h}x{h}, "
                       f"oracle/unet_ref.py on {threads} host threads"}
+
+
+def cpu_baseline_data(frames, masks, size: int, n: int):
+    """The reference's per-image host preprocessing (dataset.py:30-66) as restated
+    by the numpy oracle, timed on one host thread over a bounded sample."""
+    import oracle.dataset_ref as dref
+    t0 = time.perf_counter()
+    for i in range(n):
+        dref.preprocess(frames[i], masks[i], (size, size))
+    dt = (time.perf_counter() - t0) / n
+    return {"value": round(1.0 / dt, 2), "unit": "frames/sec", "cores": 1, "kind": "port",
+            "sample": f"{n} frames through oracle/dataset_ref.py (numpy, one thread)"}
+
+
+def data_bench(args):
+    """--data: throughput of the on-GPU data pipeline (SURVEY.md §8(f) row 3,
+    dataset.py:30-66,147-151) on decoded uint8 frames resident in HBM: resize
+    (INTER_AREA / INTER_NEAREST), percentile clip + CLAHE + min-max, mask
+    binarisation; and the RandomRotate90 / VerticalFlip augmentation."""
+    import numpy as np
+    pkg = importlib.import_module("image-segmentation-project_amd")
+    rng = np.random.default_rng(0)
+    n, src = args.batch, args.data_src
+    frames = rng.integers(0, 256, (n, src, src), dtype=np.uint8)
+    masks = (rng.random((n, src, src)) < 0.3).astype(np.uint8) * 255
+    x, m = torch.from_numpy(frames).cuda(), torch.from_numpy(masks).cuda()
+    aug = pkg.CellAugmenter(augmentations_per_image=1, seed=0)
+    for _ in range(args.warmup):
+        pkg.preprocess(x, m, (args.size, args.size))
+        aug.augment_training_data(x, m)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pkg.preprocess(x, m, (args.size, args.size))
+    torch.cuda.synchronize()
+    dt_pre = (time.perf_counter() - t0) / args.steps
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        aug.augment_training_data(x, m)
+    torch.cuda.synchronize()
+    dt_aug = (time.perf_counter() - t0) / args.steps
+    line = {"metric": f"preprocessed frames/sec (uint8 {src}x{src} -> float32 {args.size}x{args.size}, "
+                      "clip+CLAHE+min-max+mask)",
+            "value": round(n / dt_pre, 1), "unit": "frames/sec", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "higher_is_better": True, "data": "synthetic uint8 frames",
+            "config": {"workload": "dataset.py preprocessing on GPU", "batch": n},
+            "augment_frames_per_sec": round(n / dt_aug, 1)}
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline_data(frames, masks, args.size, args.cpu_frames)
+    print(json.dumps(line), flush=True)
 
 
 def launch_ranks(n: int) -> int:
@@ -92,13 +143,13 @@ def launch_ranks(n: int) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
-def miou_parity(model, x, y, width: int, attention: bool):
+def miou_parity(model, x, y, width: int, attention: bool, backbone: str = "resnet34"):
     """North-star parity on the bench batch: foreground IoU of the HIP train-mode
     forward vs the oracle (fp32 CPU restatement of the reference) on the same
     weights and images, reference aggregation (utils.py:120-151)."""
     import oracle
     pkg = importlib.import_module("image-segmentation-project_amd")
-    ref = oracle.ReferenceUNet(width=width, use_attention=attention)
+    ref = oracle.ReferenceUNet(width=width, use_attention=attention, backbone=backbone)
     ref.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()})
     ref.train()
     with torch.no_grad():
@@ -120,6 +171,12 @@ def main():
                     help="use_attention=True decoder (AttentionGate + ChannelAttention, the reference default)")
     ap.add_argument("--width", type=int, default=1,
                     help="channel multiplier: 1 = Base (configs[1]), 2 = Wide 128->1024 (configs[4], bf16 here)")
+    ap.add_argument("--data", action="store_true",
+                    help="bench the on-GPU data pipeline instead of the training step (--batch frames)")
+    ap.add_argument("--data-src", type=int, default=1024, help="--data: source frame size")
+    ap.add_argument("--cpu-frames", type=int, default=8, help="--data: frames in the CPU oracle sample")
+    ap.add_argument("--backbone", default="resnet34", choices=["resnet34", "resnet50"],
+                    help="encoder (advanced_models.py:72-130); resnet50 = Bottleneck 256..2048")
     ap.add_argument("--fp8", action="store_true",
                     help="forward convs with >= 128 input channels in fp8 e4m3 (configs[4] Wide fp8); bwd bf16")
     ap.add_argument("--cpu-steps", type=int, default=2)
@@ -132,6 +189,8 @@ def main():
                     help="torch.optim.Adam (foreach) instead of the fused HIP Adam (optim.py)")
     args = ap.parse_args()
 
+    if args.data:
+        return data_bench(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -147,7 +206,7 @@ def main():
     ddp = importlib.import_module("image-segmentation-project_amd.ddp")
 
     torch.manual_seed(0)
-    model = pkg.UNetWithBackbone(n_classes=1, backbone="resnet34", pretrained=False,
+    model = pkg.UNetWithBackbone(n_classes=1, backbone=args.backbone, pretrained=False,
                                   use_attention=args.attention, width=args.width, fp8=args.fp8).to(dev)
     if world > 1:
         ddp.enable_data_parallel(model)
@@ -164,7 +223,7 @@ def main():
     model.train()
     parity = None
     if rank == 0 and not args.no_cpu_baseline:
-        parity = miou_parity(model, x, y, args.width, args.attention)  # step-0 weights, before any update
+        parity = miou_parity(model, x, y, args.width, args.attention, args.backbone)  # step-0 weights
     if world > 1:
         dist.barrier()
 
@@ -245,7 +304,7 @@ def main():
         "miou_ref": None if parity is None else round(parity[1], 6),
         "miou_abs_diff": None if parity is None else float(f"{abs(parity[0] - parity[1]):.3e}"),
         "config": {"workload": ("Base" if args.width == 1 else f"Wide (x{args.width} channels)")
-                   + " U-Net resnet34 " + ("attention" if args.attention else "no-attention")
+                   + f" U-Net {args.backbone} " + ("attention" if args.attention else "no-attention")
                    + " train step (fwd+bce+bwd+Adam)",
                    "global_batch": args.batch * world, "image": f"{args.size}x{args.size}",
                    "parallelism": f"dp{world}", "fp8": bool(args.fp8)},
@@ -264,7 +323,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.batch, args.size, args.cpu_steps, args.cpu_threads, args.width,
-                                            args.attention)
+                                            args.attention, args.backbone)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -1,4 +1,4 @@
-"""Measure end-to-end deviation of the HIP path from the fp32 oracle at several
+"""(Test tooling, not collected by pytest: may import the oracle.)  Measure end-to-end deviation of the HIP path from the fp32 oracle at several
 input sizes (prints one line per size).  Used to state the tolerances of
 tests/test_model_gpu.py."""
 import importlib
