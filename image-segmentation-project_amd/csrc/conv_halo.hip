@@ -878,6 +878,11 @@ static hipError_t launch_halo_shape(const ConvFwdArgs& a, hipStream_t st) {
   // the halo-streamed kernel with the two-BN epilogue
   if (FLIP && a.bb.sums && a.bb.y2) {
     if (!(C % 32 == 0 && C >= 128 && Co % 64 == 0)) return hipErrorNotSupported;
+    static const int tcfg = std::getenv("UNET_HSTWO") ? std::atoi(std::getenv("UNET_HSTWO")) : 0;  // tuning
+    if (tcfg == 1 && a.P % 16 == 0) return launch_hs<2, 16, 4, true, true>(a, st);
+    // 32-channel blocks, 8 waves (two blocks per CU): enc2-4 downsample-block
+    // dgrads 63 / 49 / 42 -> 56 / 40 / 35 us (Base, measured)
+    if (tcfg != 9 && a.P % 16 == 0 && Co % 32 == 0) return launch_hs<2, 16, 8, true, true>(a, st);
     const long long t16 = (long long)a.N * (a.P / 16) * (a.Q / 16) * (Co / 64);
     if (a.P % 16 == 0 && t16 >= 256) return launch_hs<4, 16, 8, true, true>(a, st);
     if (a.P % 8 == 0) return launch_hs<4, 8, 4, true, true>(a, st);
@@ -895,6 +900,17 @@ static hipError_t launch_halo_shape(const ConvFwdArgs& a, hipStream_t st) {
     // measured exception: a 4-chunk K loop (C = 128) over two rounds of
     // blocks (enc2 forward) is faster as a 128x128 im2col tile
     if (!FLIP && C == 128 && t16 > 256 && t16 <= 512) return hipErrorNotSupported;
+    static const int hcfg = std::getenv("UNET_HSCFG") ? std::atoi(std::getenv("UNET_HSCFG")) : 0;  // tuning
+    if (hcfg == 9 && a.P % 16 == 0 && t16 >= 256) return launch_hs<4, 16, 8, FLIP, false>(a, st);  // round-1 choice
+    // 32-channel output blocks (80 KB of LDS: two blocks per CU, so one
+    // block's epilogue overlaps the other's MFMAs; measured on the Base
+    // config: enc3/decoder4 dgrads -5..-7 %, enc4 -11..-19 %): 8 waves when
+    // the grid is one round, else 4 waves with 4 rows each
+    if (a.P % 16 == 0 && Co % 32 == 0) {
+      const long long b32 = (long long)a.N * (a.P / 16) * (a.Q / 16) * (Co / 32);
+      if (b32 <= 256) return launch_hs<2, 16, 8, FLIP, false>(a, st);
+      return launch_hs<2, 16, 4, FLIP, false>(a, st);
+    }
     if (a.P % 16 == 0 && t16 >= 256) return launch_hs<4, 16, 8, FLIP, false>(a, st);
     if (a.P % 8 == 0) return launch_hs<4, 8, 4, FLIP, false>(a, st);
   }
