@@ -889,6 +889,10 @@ static hipError_t launch_halo_shape(const ConvFwdArgs& a, hipStream_t st) {
     return hipErrorNotSupported;
   }
   // weight-stationary: every tap of the block's channels fits in LDS
+  static const int wscfg = std::getenv("UNET_WSCFG") ? std::atoi(std::getenv("UNET_WSCFG")) : 0;  // tuning
+  if (wscfg == 1 && C == 64 && Co % 32 == 0 && a.P % 4 == 0) return launch_ws<2, 2, 4, 4, FLIP>(a, st);
+  if (wscfg == 2 && C == 64 && Co % 32 == 0 && a.P % 8 == 0) return launch_ws<2, 2, 8, 4, FLIP>(a, st);
+  if (wscfg == 3 && C == 64 && Co % 32 == 0 && a.P % 8 == 0) return launch_ws<2, 2, 8, 8, FLIP>(a, st);
   if (C == 64 && Co % 64 == 0 && a.P % 16 == 0) return launch_ws<2, 4, 16, 8, FLIP>(a, st);
   if (C == 32 && Co == 32 && a.P % 16 == 0) return launch_ws<1, 2, 16, 4, FLIP>(a, st);
   if (C == 32 && Co == 96 && a.P % 16 == 0) return launch_ws<1, 6, 16, 8, FLIP>(a, st);
@@ -897,9 +901,11 @@ static hipError_t launch_halo_shape(const ConvFwdArgs& a, hipStream_t st) {
   // halo-streamed: 256-pixel tiles while they still give >= ~1 block per CU
   if (C % 32 == 0 && C >= 128 && Co % 64 == 0) {
     const long long t16 = (long long)a.N * (a.P / 16) * (a.Q / 16) * (Co / 64);
-    // measured exception: a 4-chunk K loop (C = 128) over two rounds of
-    // blocks (enc2 forward) is faster as a 128x128 im2col tile
-    if (!FLIP && C == 128 && t16 > 256 && t16 <= 512) return hipErrorNotSupported;
+    // round 1 ran the C = 128 forwards (enc2, decoder3.3) as a 128x128 im2col
+    // tile (faster than the 64-channel halo blocks then); the 32-channel
+    // halo blocks below beat it (37-43 -> 31 us).  UNET_C128GLDS=1: old choice
+    static const bool c128_glds = std::getenv("UNET_C128GLDS") != nullptr;  // A/B
+    if (c128_glds && !FLIP && C == 128 && t16 > 256 && t16 <= 512) return hipErrorNotSupported;
     static const int hcfg = std::getenv("UNET_HSCFG") ? std::atoi(std::getenv("UNET_HSCFG")) : 0;  // tuning
     if (hcfg == 9 && a.P % 16 == 0 && t16 >= 256) return launch_hs<4, 16, 8, FLIP, false>(a, st);  // round-1 choice
     // 32-channel output blocks (80 KB of LDS: two blocks per CU, so one

@@ -1918,7 +1918,7 @@ static void halo_geometry(const ConvWgradArgs& a, int& blocks_xy, int& tiles, in
   splits = (tiles + per - 1) / per;
 }
 
-template <int TW, int CI, bool CO32 = false>
+template <int TW, int CI, bool CO32 = false, int NSO = 0>
 static hipError_t launch_wgrad_halo(const ConvWgradArgs& a0, hipStream_t st) {
   ConvWgradArgs a = a0;
   a.co_blocks = CO32 ? a.Cout / 32 : (a.Cout + 63) / 64;
@@ -1933,7 +1933,7 @@ static hipError_t launch_wgrad_halo(const ConvWgradArgs& a0, hipStream_t st) {
     per = (tiles + splits - 1) / splits;
     splits = (tiles + per - 1) / per;
   }
-  constexpr int NS = CI == 64 ? 3 : 4;
+  constexpr int NS = NSO ? NSO : (CI == 64 ? 3 : 4);
   const size_t lds = (size_t)NS * (128 * 128 + 256 * CI * 2);
   if (CO32) set_kernel_tag("wgrad3x3_halo_kernel<%d, %d, %d, true>", TW, NS, CI);
   else set_kernel_tag("wgrad3x3_halo_kernel<%d, %d, %d>", TW, NS, CI);
@@ -1981,6 +1981,12 @@ hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st) {
   if (g_use_glds && a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.C % 32 == 0 && a.P == a.H &&
       a.Q == a.W && (size_t)a.N * a.H * a.W * a.ldx * 2 < 0x80000000ull &&
       (size_t)a.N * a.P * a.Q * a.lddy * 2 < 0x80000000ull) {
+    static const int wcfg = std::getenv("UNET_WGCFG") ? std::atoi(std::getenv("UNET_WGCFG")) : 0;  // tuning
+    if (a.Q % 32 == 0 && a.P % 4 == 0) {
+      if (wcfg == 1 && a.C % 64 == 0) return launch_wgrad_halo<32, 64, false, 2>(a, st);
+      if (wcfg == 2) return launch_wgrad_halo<32, 32, false, 2>(a, st);
+      if (wcfg == 3) return launch_wgrad_halo<32, 32, false, 3>(a, st);
+    }
     if (a.C % 64 == 0) {
       if (a.Q % 32 == 0 && a.P % 4 == 0) return launch_wgrad_halo<32, 64>(a, st);
       if (a.Q % 16 == 0 && a.P % 8 == 0) return launch_wgrad_halo<16, 64>(a, st);
