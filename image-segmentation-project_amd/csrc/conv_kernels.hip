@@ -1477,6 +1477,7 @@ __global__ void __launch_bounds__(256, 2) stem_fwd_kernel(ConvFwdArgs a, int row
   }
 }
 
+template <bool FUSE>
 __global__ void __launch_bounds__(256, 2) stem_wgrad_kernel(ConvWgradArgs a, int rows_per_block) {
   // LDS: dY [256 px][64 co] | im2col [256 px][64 k] (pixel-major tr tiles) | patch
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1495,16 +1496,57 @@ __global__ void __launch_bounds__(256, 2) stem_wgrad_kernel(ConvWgradArgs a, int
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // fused stem BN-backward apply: this thread's 8 channels (c8 = tid & 7 for
+  // every j below) get dY = A dZ + B y + C (bn_bwd_apply_kernel's coefficients)
+  float cA[FUSE ? 8 : 1], cB[FUSE ? 8 : 1], cC[FUSE ? 8 : 1];
+  if constexpr (FUSE) {
+    float* coef = reinterpret_cast<float*>(smem + 2 * 256 * 128 + 7 * kStemPatchW * 2);  // [3][64]
+    if (tid < 64) {
+      const BnBwdArgs& b = a.bn;
+      const int ch = cg + tid;
+      double s1 = 0.0, s2 = 0.0;
+      for (int r = 0; r < kStatRep; ++r) {
+        s1 += b.sums[(size_t)r * 2 * b.C + ch];
+        s2 += b.sums[(size_t)r * 2 * b.C + b.C + ch];
+      }
+      const double inv_n = 1.0 / (double)b.npix;
+      const float k1 = b.gamma[ch] * b.invstd[ch];
+      const float m1 = (float)(s1 * inv_n), m2 = (float)(s2 * inv_n);
+      const float is = b.invstd[ch], mu = b.mean[ch];
+      coef[tid] = k1;
+      coef[64 + tid] = -k1 * is * m2;
+      coef[128 + tid] = k1 * (is * m2 * mu - m1);
+      if (blockIdx.x == 0) {
+        b.dgamma[ch] = (float)s2;
+        b.dbeta[ch] = (float)s1;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = ((tid & 7) << 3) + k;
+      cA[k] = coef[c]; cB[k] = coef[64 + c]; cC[k] = coef[128 + c];
+    }
+  }
   // register prefetch of the next row: dY (8 x 16 B per thread) + input patch
-  uint4 dyv[8];
+  // (fused: dZ and y, combined at the LDS store)
+  uint4 dyv[8], yv[FUSE ? 8 : 1];
   StemPatch pf;
   auto fetch = [&](int u) {
     const StemUnit t = stem_unit(u, a.P, a.Q);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int i = tid + j * 256, px = i >> 3, c8 = i & 7;
-      dyv[j] = px < t.Qs ? *reinterpret_cast<const uint4*>(a.dy + (t.row * a.Q + t.q0 + px) * a.lddy + cg + c8 * 8)
-                         : make_uint4(0, 0, 0, 0);
+      const size_t pix = t.row * a.Q + t.q0 + px;
+      if constexpr (FUSE) {
+        dyv[j] = px < t.Qs ? *reinterpret_cast<const uint4*>(a.bn.da + pix * a.bn.ldda + cg + c8 * 8)
+                           : make_uint4(0, 0, 0, 0);
+        yv[j] = px < t.Qs ? *reinterpret_cast<const uint4*>(a.bn.y + pix * a.bn.ldy + cg + c8 * 8)
+                          : make_uint4(0, 0, 0, 0);
+      } else {
+        dyv[j] = px < t.Qs ? *reinterpret_cast<const uint4*>(a.dy + pix * a.lddy + cg + c8 * 8)
+                           : make_uint4(0, 0, 0, 0);
+      }
     }
     stem_fetch(img, t, a.H, a.W, pf);
   };
@@ -1515,7 +1557,20 @@ __global__ void __launch_bounds__(256, 2) stem_wgrad_kernel(ConvWgradArgs a, int
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int i = tid + j * 256, px = i >> 3, c8 = i & 7;
-      *reinterpret_cast<uint4*>(Ds + TT::off(px, c8 * 8)) = dyv[j];
+      uint4 v = dyv[j];
+      if constexpr (FUSE) {
+        if (px < t.Qs) {
+          float dz[8], y[8], o[8];
+          unpack8(dyv[j], dz);
+          unpack8(yv[j], y);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] = fmaf(cA[k], dz[k], fmaf(cB[k], y[k], cC[k]));
+          v = pack8(o);
+        } else {
+          v = make_uint4(0, 0, 0, 0);
+        }
+      }
+      *reinterpret_cast<uint4*>(Ds + TT::off(px, c8 * 8)) = v;
     }
     stem_store_patch(pf, t.Qs, patch);
     if (row + 1 < r1) fetch(row + 1);
@@ -1607,9 +1662,11 @@ hipError_t launch_stem_wgrad(const ConvWgradArgs& a, hipStream_t st) {
   const long long cap = slab_split_cap(a, 1024 * 16 * groups);
   while ((rows + per - 1) / per > cap) ++per;
   const int blocks = (rows + per - 1) / per;
-  const size_t lds = 2 * 256 * 128 + 7 * kStemPatchW * 2;
+  const size_t lds = 2 * 256 * 128 + 7 * kStemPatchW * 2 + (a.bn_fuse ? 3 * 64 * sizeof(float) : 0);
+  if (a.bn_fuse && (a.bn.C != a.Cout || a.bn.ldda % 8 || a.bn.ldy % 8 || !a.bn.sums)) return hipErrorInvalidValue;
   set_kernel_tag("stem_wgrad_kernel");
-  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(blocks, groups), dim3(256), lds, st, a, per);
+  if (a.bn_fuse) hipLaunchKernelGGL(stem_wgrad_kernel<true>, dim3(blocks, groups), dim3(256), lds, st, a, per);
+  else hipLaunchKernelGGL(stem_wgrad_kernel<false>, dim3(blocks, groups), dim3(256), lds, st, a, per);
   if (a.slab && blocks > 1) {
     SlabLayout L = {};
     L.kind = SLAB_STEM; L.splits = blocks; L.blocks = groups; L.nw = 4; L.nf = 4; L.units = 1024LL * groups;

@@ -184,6 +184,9 @@ struct unet_plan {
   bool bn_ticket = std::getenv("UNET_BN_TICKET") && std::getenv("UNET_BN_TICKET")[0] == '1';
   // eval forward: BN folded into the conv epilogues (UNET_NO_EVAL_FOLD=1: separate BN passes, A/B only)
   bool eval_fold = std::getenv("UNET_NO_EVAL_FOLD") == nullptr;
+  // stem BN-backward apply fused into the stem weight gradient's dY load
+  // (UNET_NO_STEM_FUSE=1: separate apply pass writing dY, A/B only)
+  bool stem_bn_fuse = std::getenv("UNET_NO_STEM_FUSE") == nullptr;
   double flops_fwd = 0, flops_train = 0;
   // fp8 forward (cfg.fp8): per-tensor delayed-amax states (fp8.hip) for the
   // conv weights and activations; the first forward calibrates
@@ -672,7 +675,8 @@ static int build_plan(unet_plan* p) {
   // named views for tests: forward activations and their gradients
   auto& nm = p->named;
   nm.push_back({"y0", p->y0}); nm.push_back({"x1", p->x1}); nm.push_back({"p0", p->p0});
-  nm.push_back({"d.x1", p->d_x1}); nm.push_back({"d.y0", p->d_y0}); nm.push_back({"d.p0", p->d_p0});
+  nm.push_back({"d.x1", p->d_x1}); nm.push_back({"d.p0", p->d_p0});
+  if (!(p->fuse_bwd && p->stem_bn_fuse)) nm.push_back({"d.y0", p->d_y0});  // else never stored
   {
     int bi = 0;
     for (int s = 0; s < 4; ++s)
@@ -1499,11 +1503,14 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
       ProfScope ps(p, st, "maxpool_bwd", 0);
       CK(launch_maxpool_bwd(m, st));
     }
-    RUN(bn_backward(x, p->stem_bn, sb, fz));
-    RUN(fork());
     const Conv& cv = p->convs[p->stem_conv];
+    // fused: the stem wgrad forms dY from dZ and y itself (no apply pass, dY never stored)
+    const bool stem_fuse = fz && p->stem_bn_fuse && cv.Co % 64 == 0;
+    if (!stem_fuse) RUN(bn_backward(x, p->stem_bn, sb, fz));
+    RUN(fork());
     ConvWgradArgs a = {};
     a.dy = x.A(p->d_y0); a.lddy = p->d_y0.ld;
+    if (stem_fuse) { a.bn = sb; a.bn_fuse = 1; }
     a.dw = x.W<float>(cv.wacc);
     a.N = N; a.H = p->cfg.H; a.W = p->cfg.W; a.C = 1;
     a.P = p->y0.H; a.Q = p->y0.W; a.Cout = cv.Co;

@@ -119,6 +119,12 @@ struct ConvWgradArgs {
   // without one (single-op C ABI) the kernels add into a zeroed dW with fp32
   // atomics.
   float* slab; size_t slab_bytes;
+  // stem only (bn_fuse != 0): dY is not stored; the kernel forms it while
+  // loading, dY = A dZ + B y + C per channel, from the stem BN's backward sums
+  // (bn.sums, reduced by the fused maxpool backward), bn.da = dZ, bn.y = the raw
+  // stem conv output — the expression of bn_bwd_apply_kernel, so dY is bit-
+  // identical — and writes the BN's dgamma / dbeta (block (0, group))
+  BnBwdArgs bn; int bn_fuse;
   int N, H, W, C, P, Q, Cout, R, S, stride, pad;
   int px_per_split, co_blocks, c_blocks;  // filled by the launcher
 };
