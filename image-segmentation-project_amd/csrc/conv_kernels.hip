@@ -1704,7 +1704,15 @@ static hipError_t launch_glds_cfg(const ConvFwdArgs& a0, int classes, hipStream_
   a.mblocks = (M + BM - 1) / BM;
   constexpr int NW = WM * WN, ROWB = BK * 2, RPI = 1024 / ROWB;
   constexpr size_t B_ROWS = ((BN + RPI * NW - 1) / (RPI * NW)) * RPI * NW;
-  size_t lds = (size_t)NS * (BM + B_ROWS) * ROWB;
+  // a K loop shorter than the pipeline (1x1 convs, the convT forward as one
+  // GEMM) only ever touches its first KT stage buffers: allocate just those,
+  // so more blocks fit per CU
+  int stages = NS;
+  if ((MODE == MODE_FWD || MODE == MODE_SHUF) && a.C % BK == 0) {
+    const int kt = a.R * a.S * (a.C / BK);
+    if (kt >= 1 && kt < stages) stages = kt;
+  }
+  size_t lds = (size_t)stages * (BM + B_ROWS) * ROWB;
   const size_t red = (size_t)WM * BN * 3 * sizeof(float) + 16;
   if (red > lds) lds = red;
   dim3 grid(a.mblocks * a.nblocks, 1, classes);
@@ -2048,7 +2056,11 @@ hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st) {
       if (a.Q % 32 == 0 && a.P % 4 == 0) return launch_wgrad_halo<32, 64>(a, st);
       if (a.Q % 16 == 0 && a.P % 8 == 0) return launch_wgrad_halo<16, 64>(a, st);
     }
-    if (a.Cout == 32 && a.Q % 32 == 0 && a.P % 4 == 0) return launch_wgrad_halo<32, 32, true>(a, st);
+    if (a.Cout == 32 && a.Q % 32 == 0 && a.P % 4 == 0) {
+      if (wcfg == 4) return launch_wgrad_halo<32, 32, true, 2>(a, st);
+      if (wcfg == 5) return launch_wgrad_halo<32, 32, true, 3>(a, st);
+      return launch_wgrad_halo<32, 32, true>(a, st);
+    }
     if (a.Q % 32 == 0 && a.P % 4 == 0) return launch_wgrad_halo<32, 32>(a, st);
     if (a.Q % 16 == 0 && a.P % 8 == 0) return launch_wgrad_halo<16, 32>(a, st);
   }
