@@ -32,13 +32,14 @@ HBM_PEAK_GBS = 8000.0
 
 
 def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (scripts/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md
-    HBM section), or None when that kernel was not profiled."""
+    """(HBM bytes per launch of `kernel`, source file) from the newest committed
+    rocprofv3 PMC summary (scripts/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE,
+    MI355X_MICROARCH.md HBM section; PMC passes cannot run inside the timed
+    bench), or (None, None) when that kernel was not profiled."""
     import glob
     found = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "*", "pmc_traffic.json")))
     if not found:
-        return None
+        return None, None
     path = found[-1]  # newest profiling session of the newest round
     with open(path) as f:
         table = json.load(f)
@@ -52,8 +53,8 @@ def pmc_traffic(kernel: str):
     want = canon(kernel)
     for key, ent in table.items():
         if canon(key) == want:
-            return ent["bytes_per_launch"]
-    return None
+            return ent["bytes_per_launch"], os.path.relpath(path, REPO)
+    return None, None
 
 
 def cpu_baseline(batch: int, h: int, steps: int, threads: int, width: int = 1, attention: bool = False,
@@ -285,7 +286,8 @@ def main():
     dom_ms, dom_fl, dom_n = by_kernel[dom]
     achieved_tflops = dom_fl / 1e9 / dom_ms
     dom_peak = MFMA_FP8_PEAK_TFLOPS if dom.startswith("conv_f8_kernel") else MFMA_BF16_PEAK_TFLOPS
-    traffic = pmc_traffic(dom)
+    traffic, traffic_src = pmc_traffic(dom)
+    dom_us = dom_ms / dom_n * 1e3
     line = {
         "metric": "images/sec + mIoU, 512x512 U-Net bf16 at 1/2/4/8 MI355X",
         "value": round(imgs / dt, 3),
@@ -311,8 +313,13 @@ def main():
         "roofline": {"bound": "mfma", "achieved": round(achieved_tflops, 2), "peak": dom_peak,
                      "unit": "TFLOP/s", "frac": round(achieved_tflops / dom_peak, 4),
                      "traffic": traffic,
+                     # PMC bytes per launch (committed profile named here) over this
+                     # run's measured average launch time: the kernel's HBM rate
+                     "traffic_source": traffic_src,
+                     "hbm_gbs": None if traffic is None else round(traffic / dom_us / 1e3, 1),
+                     "hbm_peak_gbs": HBM_PEAK_GBS,
                      "kernel": dom, "launches_per_step": dom_n,
-                     "avg_launch_us": round(dom_ms / dom_n * 1e3, 2),
+                     "avg_launch_us": round(dom_us, 2),
                      "kernel_ms_per_step": round(dom_ms, 3),
                      "conv_family_tflops": round(conv_tflops, 2), "conv_ms_per_step": round(conv_ms, 3),
                      "all_kernels_ms_per_step": round(kernel_ms_total, 3),

@@ -1189,9 +1189,12 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
   // (SLAB_HALO: 18 fragments per wave, 16 B per lane per store), or -- one
   // split -- the block's dW tile with plain stores, or fp32 atomics (no slab)
   if (a.slab && nsplit > 1) {
-    const size_t units = (size_t)combos * NW * 18 * 64;  // per split (grid = combos x splits)
+    // CO32: only the wm = 0 waves hold a partial (the slab has NW / 2 wave slots)
+    constexpr int SW = CO32 ? NW / 2 : NW;
+    const int sw = CO32 ? wn : wave;
+    const size_t units = (size_t)combos * SW * 18 * 64;  // per split (grid = combos x splits)
     f32x4* dst = reinterpret_cast<f32x4*>(a.slab) + (size_t)split * units +
-                 ((size_t)combo * NW + wave) * (18 * 64) + lane;
+                 ((size_t)combo * SW + sw) * (18 * 64) + lane;
 #pragma unroll
     for (int t = 0; t < 9; ++t)
 #pragma unroll
@@ -1226,8 +1229,8 @@ __device__ __forceinline__ long long slab_dw_index(const SlabLayout& L, long lon
   const int blk = (int)(r / L.nw);
   const int g = lane >> 4, li = lane & 15;
   if (L.kind == SLAB_HALO) {
-    const int t = frag >> 1, i = frag & 1, wm = wave & 1, wn = wave >> 1;
-    if (L.co32 && wm) return -1;
+    // CO32 slabs hold only the wm = 0 waves (wave slot = wn)
+    const int t = frag >> 1, i = frag & 1, wm = L.co32 ? 0 : (wave & 1), wn = L.co32 ? wave : (wave >> 1);
     const int cob = blk % L.co_blocks, cib = blk / L.co_blocks;
     const int co = cob * (L.co32 ? 32 : 64) + (L.co32 ? 0 : wm * 32) + i * 16 + 4 * g + e;
     const int c = cib * L.ci + wn * 16 + li;
@@ -1991,7 +1994,8 @@ static hipError_t launch_wgrad_halo(const ConvWgradArgs& a0, hipStream_t st) {
   int blocks_xy, tiles, per, splits;
   halo_geometry<TW, CI, CO32>(a, blocks_xy, tiles, per, splits);
   constexpr int NW = CI / 8;
-  const long long units = (long long)blocks_xy * NW * 18 * 64;
+  constexpr int SW = CO32 ? NW / 2 : NW;  // wave slots per block in the slab
+  const long long units = (long long)blocks_xy * SW * 18 * 64;
   const long long cap = slab_split_cap(a, units * 16);
   if (splits > cap) {
     splits = (int)cap;
@@ -2006,7 +2010,7 @@ static hipError_t launch_wgrad_halo(const ConvWgradArgs& a0, hipStream_t st) {
                      a, tiles, per);
   if (a.slab && splits > 1) {
     SlabLayout L = {};
-    L.kind = SLAB_HALO; L.splits = splits; L.blocks = blocks_xy; L.nw = NW; L.nf = 18; L.units = units;
+    L.kind = SLAB_HALO; L.splits = splits; L.blocks = blocks_xy; L.nw = SW; L.nf = 18; L.units = units;
     L.Cout = a.Cout; L.C = a.C; L.Krow = 9 * a.C; L.cmax = a.C;
     L.co_blocks = a.co_blocks; L.c_blocks = a.c_blocks; L.ci = CI; L.co32 = CO32 ? 1 : 0;
     g_pending = PendingReduce{a.slab, a.dw, L};
