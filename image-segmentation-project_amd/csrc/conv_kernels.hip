@@ -1035,23 +1035,45 @@ conv_wgrad_kernel(ConvWgradArgs a) {
 // channels (no MFMA on the absent channels 32..63), and their partial dW are
 // summed through LDS before the store.  The dY DMA still moves 128-B rows
 // (pixel p's 32 channels + pixel p+1's, unused).
-template <int TW, int NS, int CI, bool CO32 = false>
+//
+// SD = 2 (3x3 / stride 2 / pad 1, the first conv of encoder stages 2-4): the
+// output tile TH x TW reads a (2TH+1) x (2TW+1) input halo (CI = 32 only: 561
+// rows of 64 B), tap (r, s) of output pixel (y, x) is halo row (2y + r, 2x + s);
+// the same 9-tap reuse of each staged input pixel as the stride-1 kernel
+// (the implicit-GEMM wgrad stages an im2col tile per tap).
+template <int TW, int CI, int SD>
+constexpr int wgrad_halo_rows() {  // LDS halo capacity (rows), a multiple of one DMA round
+  constexpr int TH = 128 / TW;
+  constexpr int rows = (SD * TH + (SD == 1 ? 2 : 1)) * (SD * TW + (SD == 1 ? 2 : 1));
+  constexpr int round = (1024 / (CI * 2)) * (CI / 8);
+  return SD == 1 ? 256 : (rows + round - 1) / round * round;
+}
+
+// DSF (SD = 2): the block's downsample weight gradient rides in the same
+// stages: a dY2 tile beside dY, one more A fragment pair at the centre tap,
+// two more accumulator fragments (slab frags 18, 19).
+template <int TW, int NS, int CI, bool CO32 = false, int SD = 1, bool DSF = false>
 __global__ void __launch_bounds__(CI * 8)
 wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
   constexpr int NW = CI / 8;            // waves
   constexpr int TH = 128 / TW;
-  constexpr int HW2 = TW + 2;
-  constexpr int HROWS = (TH + 2) * HW2;
+  constexpr int HW2 = SD * TW + (SD == 1 ? 2 : 1);
+  constexpr int HROWS = (SD * TH + (SD == 1 ? 2 : 1)) * HW2;
+  constexpr int HCAP = wgrad_halo_rows<TW, CI, SD>();
   constexpr int HROWB = CI * 2;         // halo row bytes
   constexpr int HCPR = HROWB / 16;      // 16-B chunks per halo row
   constexpr int HRPI = 1024 / HROWB;    // halo rows per wave instruction
-  constexpr int H_INS = 256 / HRPI / NW;
+  constexpr int H_INS = HCAP / HRPI / NW;
   constexpr int A_INS = 16 / NW;        // dY: 128 rows of 128 B = 16 instructions
   constexpr int A_BYTES = 128 * 128;
-  constexpr int B_BYTES = 256 * HROWB;  // halo capacity: 256 rows
-  static_assert(HROWS <= 256, "halo rows");
-  constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int LPS = A_INS + H_INS;    // glds per wave per stage
+  constexpr int B_BYTES = HCAP * HROWB;
+  static_assert(HROWS <= HCAP && HCAP % (HRPI * NW) == 0, "halo rows");
+  static_assert(SD == 1 || (CI == 32 && !CO32 && TW % 8 == 0), "stride-2 variant");
+  static_assert(!DSF || SD == 2, "downsample fold: stride-2 kernel only");
+  constexpr int D_BYTES = DSF ? A_BYTES : 0;  // dY2 tile
+  constexpr int STAGE = A_BYTES + B_BYTES + D_BYTES;
+  constexpr int NF = DSF ? 20 : 18;           // accumulator fragments per wave
+  constexpr int LPS = A_INS * (DSF ? 2 : 1) + H_INS;  // glds per wave per stage
   extern __shared__ __attribute__((aligned(16))) char smem[];
   typedef TrTile<64, 64, 128> TA;
 
@@ -1075,6 +1097,8 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
   const int tq = a.Q / TW, tp = a.P / TH;
   const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, (unsigned)((size_t)a.N * a.P * a.Q * a.lddy * 2));
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
+  const __amdgpu_buffer_rsrc_t dy2r =
+      make_rsrc(DSF ? a.dy2 : a.dy, DSF ? (unsigned)((size_t)a.N * a.P * a.Q * a.lddy2 * 2) : 0u);
 
   // per-lane constant parts of the loads
   const int arow = lane >> 3, aslot = lane & 7;                // dY: 8 rows of 128 B per instruction
@@ -1084,13 +1108,14 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
   // contiguous rows of one image, so its offset is a per-lane part plus the
   // tile's (wave-uniform, non-negative) origin passed as the scalar offset;
   // the halo keeps a per-stage bounds test on precomputed (row, col).
-  unsigned arel[A_INS];
+  unsigned arel[A_INS], arel2[DSF ? A_INS : 1];
 #pragma unroll
   for (int j = 0; j < A_INS; ++j) {
     const int row = (wave * A_INS + j) * 8 + arow;  // pixel in tile
     const int f = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
     const int lchunk = ((((aslot >> 1) ^ f)) << 1) | (aslot & 1);
     arel[j] = (unsigned)((((row / TW) * a.Q + row % TW) * a.lddy) + co0 + lchunk * 8) * 2u;
+    if constexpr (DSF) arel2[j] = (unsigned)((((row / TW) * a.Q + row % TW) * a.lddy2) + co0 + lchunk * 8) * 2u;
   }
   int hrr[H_INS], hcc[H_INS], hch[H_INS];
 #pragma unroll
@@ -1117,9 +1142,15 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
     const unsigned abase = (unsigned)(((n * a.P + oh0) * a.Q + ow0) * a.lddy) * 2u;
 #pragma unroll
     for (int j = 0; j < A_INS; ++j) glds16s(dyr, As + (wave * A_INS + j) * 1024, arel[j], abase);
+    if constexpr (DSF) {
+      const unsigned abase2 = (unsigned)(((n * a.P + oh0) * a.Q + ow0) * a.lddy2) * 2u;
+#pragma unroll
+      for (int j = 0; j < A_INS; ++j)
+        glds16s(dy2r, As + A_BYTES + B_BYTES + (wave * A_INS + j) * 1024, arel2[j], abase2);
+    }
 #pragma unroll
     for (int j = 0; j < H_INS; ++j) {
-      const int ih = oh0 + hrr[j], iw = ow0 + hcc[j];
+      const int ih = SD * oh0 + hrr[j], iw = SD * ow0 + hcc[j];
       unsigned off = kOOB;
       if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
         off = (unsigned)((((n * a.H + ih) * a.W + iw) * a.ldx) + hch[j]) * 2u;
@@ -1127,9 +1158,11 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
     }
   };
 
-  f32x4 acc[9][2];
+  f32x4 acc[9][2], acc2[DSF ? 2 : 1];
 #pragma unroll
   for (int t = 0; t < 9; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < (DSF ? 2 : 1); ++i) acc2[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
@@ -1160,11 +1193,22 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
       for (int r = 0; r < 3; ++r)
 #pragma unroll
         for (int s = 0; s < 3; ++s) {
-          const int hr = (ty + r) * HW2 + tx + s;
-          const bf16x8 bfr = tr_read8(Bs + tr_off<CI>(hr, col), Bs + tr_off<CI>(hr + 4, col));
+          const int hr = (SD * ty + r) * HW2 + SD * tx + s;
+          const bf16x8 bfr = tr_read8(Bs + tr_off<CI>(hr, col), Bs + tr_off<CI>(hr + 4 * SD, col));
 #pragma unroll
           for (int i = 0; i < 2; ++i)
             acc[r * 3 + s][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[r * 3 + s][i], 0, 0, 0);
+          if constexpr (DSF) {
+            if (r == 1 && s == 1) {  // centre tap = the downsample's input pixel (2y, 2x)
+              const char* Ds = Bs + B_BYTES;
+#pragma unroll
+              for (int i = 0; i < 2; ++i) {
+                const int cl = wm * 32 + i * 16 + 4 * trp;
+                const bf16x8 a2 = tr_read8(Ds + TA::off(p_lo, cl), Ds + TA::off(p_lo + 4, cl));
+                acc2[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, bfr, acc2[i], 0, 0, 0);
+              }
+            }
+          }
         }
     }
   }
@@ -1192,13 +1236,17 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
     // CO32: only the wm = 0 waves hold a partial (the slab has NW / 2 wave slots)
     constexpr int SW = CO32 ? NW / 2 : NW;
     const int sw = CO32 ? wn : wave;
-    const size_t units = (size_t)combos * SW * 18 * 64;  // per split (grid = combos x splits)
+    const size_t units = (size_t)combos * SW * NF * 64;  // per split (grid = combos x splits)
     f32x4* dst = reinterpret_cast<f32x4*>(a.slab) + (size_t)split * units +
-                 ((size_t)combo * SW + sw) * (18 * 64) + lane;
+                 ((size_t)combo * SW + sw) * (NF * 64) + lane;
 #pragma unroll
     for (int t = 0; t < 9; ++t)
 #pragma unroll
       for (int i = 0; i < 2; ++i) dst[(t * 2 + i) * 64] = acc[t][i];
+    if constexpr (DSF) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) dst[(18 + i) * 64] = acc2[i];
+    }
     return;
   }
   const int Krow = 9 * a.C;
@@ -1216,6 +1264,19 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
           else atomicAdd(d, acc[t][i][e]);
         }
       }
+  if constexpr (DSF) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = co0 + wm * 32 + i * 16 + 4 * g + e;
+        if (co < a.Cout) {
+          float* d = a.dw2 + (size_t)co * a.C + c;
+          if (a.slab) *d = acc2[i][e];
+          else atomicAdd(d, acc2[i][e]);
+        }
+      }
+  }
 }
 
 // dW index of element e of slab unit u (SlabLayout), -1 if that accumulator
@@ -1232,6 +1293,11 @@ __device__ __forceinline__ long long slab_dw_index(const SlabLayout& L, long lon
     // CO32 slabs hold only the wm = 0 waves (wave slot = wn)
     const int t = frag >> 1, i = frag & 1, wm = L.co32 ? 0 : (wave & 1), wn = L.co32 ? wave : (wave >> 1);
     const int cob = blk % L.co_blocks, cib = blk / L.co_blocks;
+    if (frag >= 18) {  // folded downsample: dW2 [Cout][C]
+      const int co = cob * 64 + wm * 32 + i * 16 + 4 * g + e;
+      if (co >= L.Cout) return -1;
+      return L.dw2_off + (long long)co * L.C + cib * L.ci + wn * 16 + li;
+    }
     const int co = cob * (L.co32 ? 32 : 64) + (L.co32 ? 0 : wm * 32) + i * 16 + 4 * g + e;
     const int c = cib * L.ci + wn * 16 + li;
     if (co >= L.Cout) return -1;
@@ -1981,12 +2047,13 @@ static void halo_geometry(const ConvWgradArgs& a, int& blocks_xy, int& tiles, in
   constexpr int TH = 128 / TW;
   blocks_xy = (CO32 ? a.Cout / 32 : (a.Cout + 63) / 64) * (a.C / CI);
   tiles = a.N * (a.P / TH) * (a.Q / TW);
-  splits = std::max(1, std::min(tiles, 256 / blocks_xy));
+  static const int target = std::getenv("UNET_WG_TARGET") ? std::atoi(std::getenv("UNET_WG_TARGET")) : 256;  // tuning
+  splits = std::max(1, std::min(tiles, target / blocks_xy));
   per = (tiles + splits - 1) / splits;
   splits = (tiles + per - 1) / per;
 }
 
-template <int TW, int CI, bool CO32 = false, int NSO = 0>
+template <int TW, int CI, bool CO32 = false, int NSO = 0, int SD = 1, bool DSF = false>
 static hipError_t launch_wgrad_halo(const ConvWgradArgs& a0, hipStream_t st) {
   ConvWgradArgs a = a0;
   a.co_blocks = CO32 ? a.Cout / 32 : (a.Cout + 63) / 64;
@@ -1995,7 +2062,8 @@ static hipError_t launch_wgrad_halo(const ConvWgradArgs& a0, hipStream_t st) {
   halo_geometry<TW, CI, CO32>(a, blocks_xy, tiles, per, splits);
   constexpr int NW = CI / 8;
   constexpr int SW = CO32 ? NW / 2 : NW;  // wave slots per block in the slab
-  const long long units = (long long)blocks_xy * SW * 18 * 64;
+  constexpr int NF = DSF ? 20 : 18;
+  const long long units = (long long)blocks_xy * SW * NF * 64;
   const long long cap = slab_split_cap(a, units * 16);
   if (splits > cap) {
     splits = (int)cap;
@@ -2003,16 +2071,20 @@ static hipError_t launch_wgrad_halo(const ConvWgradArgs& a0, hipStream_t st) {
     splits = (tiles + per - 1) / per;
   }
   constexpr int NS = NSO ? NSO : (CI == 64 ? 3 : 4);
-  const size_t lds = (size_t)NS * (128 * 128 + 256 * CI * 2);
-  if (CO32) set_kernel_tag("wgrad3x3_halo_kernel<%d, %d, %d, true>", TW, NS, CI);
+  constexpr size_t lds = (size_t)NS * (128 * 128 * (DSF ? 2 : 1) + wgrad_halo_rows<TW, CI, SD>() * CI * 2);
+  static_assert(lds <= 163840, "LDS");
+  if (DSF) set_kernel_tag("wgrad3x3_halo_kernel<%d, %d, %d, false, 2, true>", TW, NS, CI);
+  else if (SD == 2) set_kernel_tag("wgrad3x3_halo_kernel<%d, %d, %d, false, 2>", TW, NS, CI);
+  else if (CO32) set_kernel_tag("wgrad3x3_halo_kernel<%d, %d, %d, true>", TW, NS, CI);
   else set_kernel_tag("wgrad3x3_halo_kernel<%d, %d, %d>", TW, NS, CI);
-  hipLaunchKernelGGL((wgrad3x3_halo_kernel<TW, NS, CI, CO32>), dim3(blocks_xy * splits), dim3(CI * 8), lds, st,
-                     a, tiles, per);
+  hipLaunchKernelGGL((wgrad3x3_halo_kernel<TW, NS, CI, CO32, SD, DSF>), dim3(blocks_xy * splits), dim3(CI * 8), lds,
+                     st, a, tiles, per);
   if (a.slab && splits > 1) {
     SlabLayout L = {};
-    L.kind = SLAB_HALO; L.splits = splits; L.blocks = blocks_xy; L.nw = SW; L.nf = 18; L.units = units;
+    L.kind = SLAB_HALO; L.splits = splits; L.blocks = blocks_xy; L.nw = SW; L.nf = NF; L.units = units;
     L.Cout = a.Cout; L.C = a.C; L.Krow = 9 * a.C; L.cmax = a.C;
     L.co_blocks = a.co_blocks; L.c_blocks = a.c_blocks; L.ci = CI; L.co32 = CO32 ? 1 : 0;
+    L.dw2_off = DSF ? (long long)(a.dw2 - a.dw) : 0;
     g_pending = PendingReduce{a.slab, a.dw, L};
   }
   return hipGetLastError();
@@ -2044,6 +2116,16 @@ hipError_t launch_convt_wgrad(const ConvWgradArgs& a0, hipStream_t st) {
   return launch_wgrad_cfg<XLOAD_SHUF, 32, 32, 64, 2, 2>(a, st);
 }
 
+// UNET_NO_S2WG=1: stride-2 weight gradients on the implicit GEMM (A/B)
+bool wgrad_s2_fold_ok(const ConvWgradArgs& a) {
+  static const bool s2wg = std::getenv("UNET_NO_S2WG") == nullptr;
+  return g_use_glds && s2wg && a.R == 3 && a.S == 3 && a.stride == 2 && a.pad == 1 && a.C % 32 == 0 &&
+         a.Cout % 64 == 0 && a.H == 2 * a.P && a.W == 2 * a.Q && a.Q % 16 == 0 && a.P % 8 == 0 &&
+         (!a.dy2 || a.lddy2 % 8 == 0) && a.lddy % 8 == 0 && a.ldx % 8 == 0 &&
+         (size_t)a.N * a.H * a.W * a.ldx * 2 < 0x80000000ull &&
+         (size_t)a.N * a.P * a.Q * (a.lddy > a.lddy2 ? a.lddy : a.lddy2) * 2 < 0x80000000ull;
+}
+
 hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st) {
   if (stem)
     return g_use_glds && a.Cout % 64 == 0 ? launch_stem_wgrad(a, st) : launch_wgrad_cfg<XLOAD_STEM, 64, 64, 64, 2, 2>(a, st);
@@ -2068,6 +2150,13 @@ hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st) {
     if (a.Q % 32 == 0 && a.P % 4 == 0) return launch_wgrad_halo<32, 32>(a, st);
     if (a.Q % 16 == 0 && a.P % 8 == 0) return launch_wgrad_halo<16, 32>(a, st);
   }
+  // 3x3 / stride 2 / pad 1 (encoder stages 2-4, first conv): the halo kernel
+  // with a (2TH+1) x (2TW+1) input halo, the downsample folded in when a.dy2
+  if (wgrad_s2_fold_ok(a)) {
+    if (a.dy2) return launch_wgrad_halo<16, 32, false, 2, 2, true>(a, st);
+    return launch_wgrad_halo<16, 32, false, 3, 2>(a, st);
+  }
+  if (a.dy2) return hipErrorInvalidValue;
   if (a.C % 32 || a.Cout % 32) return hipErrorInvalidValue;
   const bool co64 = a.Cout % 64 == 0, c64 = a.C % 64 == 0;
   if (a.Cout >= 128 && a.C >= 128)

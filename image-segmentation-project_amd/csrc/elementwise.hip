@@ -1080,6 +1080,8 @@ __global__ void __launch_bounds__(256) unpack_kernel(UnpackTable t) {
       const int aa = (int)(q % R); q /= R;
       const int co = (int)(q % Co); const int ci = (int)(q / Co);
       v = e.acc[(((int)ci * R + aa) * S + b) * Co + co];
+    } else if (e.kind == UP_ZERO) {  // a gradient that is exactly 0 (bias feeding a training-mode BN)
+      v = 0.f;
     } else {  // UP_STEM: dst[co][0][r][s] <- acc[co][r*8+s] (row length 64)
       const int k = (int)(i % 49), co = (int)(i / 49);
       const int r = k / 7, ss = k - r * 7;

@@ -187,6 +187,9 @@ struct unet_plan {
   // stem BN-backward apply fused into the stem weight gradient's dY load
   // (UNET_NO_STEM_FUSE=1: separate apply pass writing dY, A/B only)
   bool stem_bn_fuse = std::getenv("UNET_NO_STEM_FUSE") == nullptr;
+  // BasicBlock downsample (1x1 / s2) weight gradient folded into the conv1
+  // (3x3 / s2) halo weight gradient (UNET_NO_DS_FOLD=1: separate launch, A/B)
+  bool ds_wgrad_fold = std::getenv("UNET_NO_DS_FOLD") == nullptr;
   double flops_fwd = 0, flops_train = 0;
   // fp8 forward (cfg.fp8): per-tensor delayed-amax states (fp8.hip) for the
   // conv weights and activations; the first forward calibrates
@@ -935,7 +938,9 @@ int wgrad_and_reduce(const Ctx& x, ConvWgradArgs& a, int mode, const std::string
   return 0;
 }
 
-int conv_wgrad(const Ctx& x, int ci, const Act& dy, const Act& in) {
+// ds >= 0: the block's 1x1 / stride-2 downsample weight gradient (dY = *dyds,
+// same input) folded into this 3x3 / stride-2 conv's launch (ds_fold_ok)
+int conv_wgrad(const Ctx& x, int ci, const Act& dy, const Act& in, int ds = -1, const Act* dyds = nullptr) {
   const Conv& cv = x.p->convs[ci];
   ConvWgradArgs a = {};
   a.N = x.p->cfg.N;
@@ -954,7 +959,32 @@ int conv_wgrad(const Ctx& x, int ci, const Act& dy, const Act& in) {
   a.x = x.A(in); a.ldx = in.ld;
   a.H = in.H; a.W = in.W; a.C = cv.Ci;
   a.P = dy.H; a.Q = dy.W; a.Cout = cv.Co;
-  return wgrad_and_reduce(x, a, 0, pname(x, cv.w), conv_flops(x.p, cv, dy));
+  double fl = conv_flops(x.p, cv, dy);
+  std::string name = pname(x, cv.w);
+  if (ds >= 0) {
+    const Conv& dv = x.p->convs[ds];
+    a.dy2 = x.A(*dyds); a.lddy2 = dyds->ld;
+    a.dw2 = x.W<float>(dv.wacc);
+    fl += conv_flops(x.p, dv, *dyds);
+    name += " +ds";
+  }
+  return wgrad_and_reduce(x, a, 0, name, fl);
+}
+
+// the downsample's weight gradient can ride in conv1's stride-2 halo wgrad
+bool ds_fold_ok(const Ctx& x, const Block& b) {
+  if (b.ds < 0 || b.bottleneck()) return false;
+  const Conv& c1 = x.p->convs[b.conv1];
+  const Conv& dv = x.p->convs[b.ds];
+  if (dv.R != 1 || dv.stride != 2 || dv.pad != 0 || dv.Co != c1.Co || dv.Ci != c1.Ci) return false;
+  ConvWgradArgs a = {};
+  a.N = x.p->cfg.N;
+  a.R = c1.R; a.S = c1.S; a.stride = c1.stride; a.pad = c1.pad;
+  a.lddy = b.dy1.ld; a.ldx = b.in.ld; a.lddy2 = b.dyds.ld;
+  a.dy2 = x.A(b.dyds);
+  a.H = b.in.H; a.W = b.in.W; a.C = c1.Ci;
+  a.P = b.dy1.H; a.Q = b.dy1.W; a.Cout = c1.Co;
+  return b.dyds.H == b.dy1.H && b.dyds.W == b.dy1.W && wgrad_s2_fold_ok(a);
 }
 
 int bn_apply(const Ctx& x, int bi, const Act& y, const Act& out, int res_mode, const Act* res, int bi2,
@@ -1020,6 +1050,26 @@ int unpack_bucket(const Ctx& x, int bk, float* grads) {
   ProfScope ps(x.p, x.wst, "unpack", 0);
   UnpackTable t;
   t.n = 0;
+  if (bk == 0) {
+    // decoder (and attention W_g / W_x / psi) conv biases feed a training-mode
+    // BN: their exact gradient is sum(dY) = 0 (BN removes the mean); written
+    // here instead of one memset launch each
+    auto zero = [&](int param) -> int {
+      t.e[t.n++] = UnpackEntry{nullptr, grads + x.p->params[param].flat, UP_ZERO,
+                               (int)x.p->params[param].numel, 1, 1, 1};
+      if (t.n == kMaxPack) { CK(launch_unpack(t, x.wst)); t.n = 0; }
+      return 0;
+    };
+    for (const Dec& d : x.p->decs) {
+      RUN(zero(x.p->convs[d.conv1].b));
+      RUN(zero(x.p->convs[d.conv2].b));
+    }
+    for (const Att& a : x.p->atts) {
+      RUN(zero(x.p->convs[a.wg].b));
+      RUN(zero(x.p->convs[a.wx].b));
+      RUN(zero(a.psi_b));
+    }
+  }
   for (int ci : x.p->bucket_convs[bk]) {
     const Conv& cv = x.p->convs[ci];
     UnpackEntry& e = t.e[t.n++];
@@ -1371,10 +1421,7 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     RUN(fork());
     RUN(conv_wgrad(x, d.conv1, d.dy1, d.cat));
     RUN(conv_dgrad(x, d.conv1, d.dy1, d.dcat, nullptr, nullptr, -1, nullptr, d.split ? &d.dcat_up : nullptr));
-    // decoder conv biases feed a training-mode BN: their exact gradient is
-    // sum(dY) = 0 (BN removes the mean); write it explicitly.
-    CK(hipMemsetAsync(grads + p->params[p->convs[d.conv1].b].flat, 0, sizeof(float) * p->convs[d.conv1].Co, st));
-    CK(hipMemsetAsync(grads + p->params[p->convs[d.conv2].b].flat, 0, sizeof(float) * p->convs[d.conv2].Co, st));
+    // (decoder conv bias gradients: exactly 0, written by bucket 0's unpack)
     // up-conv: dU = dcat[:, skip:]; its dgrad is dA of the previous decoder's
     // (or enc4's) last BN
     if (att) {  // AttentionGate backward (skip gradient -> dskip, g-path gradient added into du)
@@ -1396,10 +1443,7 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
       RUN(conv_wgrad(x, t.wx, t.dxa, t.x));
       RUN(conv_dgrad(x, t.wg, t.dg1, t.du, &d.dcat_up));
       RUN(conv_dgrad(x, t.wx, t.dxa, t.dskip, &t.dxpsi));
-      // W_g / W_x / psi conv biases feed a training-mode BN: exact gradient 0
-      for (int ci : {t.wg, t.wx})
-        CK(hipMemsetAsync(grads + p->params[p->convs[ci].b].flat, 0, sizeof(float) * p->convs[ci].Co, st));
-      CK(hipMemsetAsync(grads + p->params[t.psi_b].flat, 0, sizeof(float), st));
+      // (W_g / W_x / psi conv bias gradients: exactly 0, written by bucket 0's unpack)
     }
     const Conv& up = p->convs[d.up];
     const Act du = att ? p->atts[l].du : d.dcat_up;
@@ -1461,12 +1505,13 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     RUN(bn_backward(x, b.bn2, blk_bn2(i), fz));
     RUN(fork());
     RUN(conv_wgrad(x, b.conv2, b.dy2, b.h));
-    if (b.ds >= 0) RUN(conv_wgrad(x, b.ds, b.dyds, b.in));
+    const bool dsfold = p->ds_wgrad_fold && ds_fold_ok(x, b);
+    if (b.ds >= 0 && !dsfold) RUN(conv_wgrad(x, b.ds, b.dyds, b.in));
     const BnBwdArgs f1 = blk_bn1(i);
     RUN(conv_dgrad(x, b.conv2, b.dy2, b.dh, nullptr, fz ? &f1 : nullptr));
     RUN(bn_backward(x, b.bn1, f1, fz));
     RUN(fork());
-    RUN(conv_wgrad(x, b.conv1, b.dy1, b.in));
+    RUN(conv_wgrad(x, b.conv1, b.dy1, b.in, dsfold ? b.ds : -1, &b.dyds));
     // the last writer of d_in produces dA of the previous block's bn2
     BnBwdArgs fp = {};
     const BnBwdArgs* fprev = nullptr;

@@ -108,6 +108,7 @@ struct SlabLayout {
   int co_blocks, c_blocks;         // blk -> (co block, c block[, tap])
   int bmo, bnc, wm, wn, fn;        // GEMM tile (BMO x BNC, WM x WN waves, FN column frags)
   int ci, co32;                    // HALO: channels per block, 32-output-channel variant
+  long long dw2_off;               // HALO + folded downsample: its dW [Cout][C] at dw + dw2_off (frags 18, 19)
 };
 
 struct ConvWgradArgs {
@@ -127,7 +128,13 @@ struct ConvWgradArgs {
   BnBwdArgs bn; int bn_fuse;
   int N, H, W, C, P, Q, Cout, R, S, stride, pad;
   int px_per_split, co_blocks, c_blocks;  // filled by the launcher
+  // stride-2 halo kernel only: the block's 1x1 / stride-2 downsample weight
+  // gradient folded in (its input pixels are the centre tap's): dW2[co][c] =
+  // sum dY2[px][co] x[2p][2q][c], dY2 with the same Cout (wgrad_s2_fold_ok)
+  const bf16_t* dy2; int lddy2; float* dw2;
 };
+// the stride-2 halo weight gradient covers this shape (and then folds a.dy2)
+bool wgrad_s2_fold_ok(const ConvWgradArgs& a);
 
 hipError_t launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st);
 hipError_t launch_conv_fwd_v1(const ConvFwdArgs& a, int mode, hipStream_t st);  // register-staged
@@ -224,7 +231,7 @@ hipError_t launch_d2f_strided(const double* src, float* dst, int n, int stride, 
 // weight (un)packing between torch fp32 layouts and kernel bf16 layouts
 enum { PK_CONV_FWD = 0, PK_CONV_DGRAD = 1, PK_CONVT_FWD = 2, PK_CONVT_DGRAD = 3, PK_STEM = 4 };
 struct PackEntry { const float* src; bf16_t* dst; int kind, Co, Ci, R, S; };
-enum { UP_CONV = 0, UP_CONVT = 1, UP_STEM = 2 };
+enum { UP_CONV = 0, UP_CONVT = 1, UP_STEM = 2, UP_ZERO = 3 };  // UP_ZERO: dst[0 .. Co) = 0
 struct UnpackEntry { const float* acc; float* dst; int kind, Co, Ci, R, S; };
 constexpr int kMaxPack = 48;
 struct PackTable { int n; PackEntry e[kMaxPack]; };

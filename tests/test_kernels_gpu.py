@@ -354,7 +354,10 @@ SLAB_CASES = [  # N, Ci, H, Co, R, stride, pad, stem  -- every wgrad kernel fami
     (4, 32, 64, 32, 3, 1, 1, 0),     # halo CO32 (decoder1 shape)
     (2, 96, 64, 32, 3, 1, 1, 0),     # halo 32-channel blocks, CO32
     (2, 512, 16, 512, 3, 1, 1, 0),   # halo, one split (block owns its tile)
-    (2, 64, 32, 128, 3, 2, 1, 0),    # implicit-GEMM wgrad, stride 2
+    (2, 64, 32, 128, 3, 2, 1, 0),    # stride-2 halo wgrad (2TH+1 x 2TW+1 input halo), many splits
+    (2, 128, 64, 256, 3, 2, 1, 0),   # stride-2 halo, enc3.0 shape family
+    (4, 256, 32, 512, 3, 2, 1, 0),   # stride-2 halo, enc4.0 shape family (16x16 output)
+    (2, 64, 24, 128, 3, 2, 1, 0),    # implicit-GEMM wgrad, stride 2 (12x12 output: no halo tiling)
     (2, 64, 32, 128, 1, 2, 0, 0),    # 1x1 downsample
     (4, 1, 128, 64, 7, 2, 3, 1),     # 7x7 stem (one partial per block)
     (4, 1, 128, 128, 7, 2, 3, 1),    # Wide 7x7 stem (two channel groups per split)
