@@ -2073,10 +2073,9 @@ static hipError_t launch_wgrad_halo(const ConvWgradArgs& a0, hipStream_t st) {
   constexpr int NS = NSO ? NSO : (CI == 64 ? 3 : 4);
   constexpr size_t lds = (size_t)NS * (128 * 128 * (DSF ? 2 : 1) + wgrad_halo_rows<TW, CI, SD>() * CI * 2);
   static_assert(lds <= 163840, "LDS");
-  if (DSF) set_kernel_tag("wgrad3x3_halo_kernel<%d, %d, %d, false, 2, true>", TW, NS, CI);
-  else if (SD == 2) set_kernel_tag("wgrad3x3_halo_kernel<%d, %d, %d, false, 2>", TW, NS, CI);
-  else if (CO32) set_kernel_tag("wgrad3x3_halo_kernel<%d, %d, %d, true>", TW, NS, CI);
-  else set_kernel_tag("wgrad3x3_halo_kernel<%d, %d, %d>", TW, NS, CI);
+  // the full template argument list, as rocprofv3 spells the kernel
+  set_kernel_tag("wgrad3x3_halo_kernel<%d, %d, %d, %s, %d, %s>", TW, NS, CI, CO32 ? "true" : "false", SD,
+                 DSF ? "true" : "false");
   hipLaunchKernelGGL((wgrad3x3_halo_kernel<TW, NS, CI, CO32, SD, DSF>), dim3(blocks_xy * splits), dim3(CI * 8), lds,
                      st, a, tiles, per);
   if (a.slab && splits > 1) {
