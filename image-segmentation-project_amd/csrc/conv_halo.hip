@@ -888,15 +888,6 @@ static hipError_t launch_halo_shape(const ConvFwdArgs& a, hipStream_t st) {
     if (a.P % 8 == 0) return launch_hs<4, 8, 4, true, true>(a, st);
     return hipErrorNotSupported;
   }
-  // UNET_HS_SMALL (A/B): the halo-streamed kernel (one tile per block, 32-channel
-  // output blocks, two blocks per CU) also for C < 128; 1 = every such layer,
-  // 2 = the full-resolution ones (P >= 256: decoder1)
-  static const int hs_small = std::getenv("UNET_HS_SMALL") ? std::atoi(std::getenv("UNET_HS_SMALL")) : 0;
-  if (hs_small && C % 32 == 0 && C < 128 && Co % 32 == 0 && a.P % 16 == 0 && (hs_small == 1 || a.P >= 256)) {
-    const long long b32 = (long long)a.N * (a.P / 16) * (a.Q / 16) * (Co / 32);
-    if (b32 <= 256) return launch_hs<2, 16, 8, FLIP, false>(a, st);
-    return launch_hs<2, 16, 4, FLIP, false>(a, st);
-  }
   // weight-stationary: every tap of the block's channels fits in LDS
   static const int wscfg = std::getenv("UNET_WSCFG") ? std::atoi(std::getenv("UNET_WSCFG")) : 0;  // tuning
   if (wscfg == 1 && C == 64 && Co % 32 == 0 && a.P % 4 == 0) return launch_ws<2, 2, 4, 4, FLIP>(a, st);
