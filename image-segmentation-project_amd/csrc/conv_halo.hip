@@ -388,6 +388,7 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
   char* wl = smem;
   char* hl = smem + WBYTES;
   float* cst = reinterpret_cast<float*>(hl + 2 * HBUF);  // [kEpiConsts][COT]
+  float* xss = cst + kEpiConsts * COT;                   // xform: [2][NP*32] scale | shift
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -400,6 +401,13 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
 
   issue_weight_dma<COT, NW>(a, wr, wl, co0, 0, NP, wave, lane);  // all 9 taps, once
   load_epi_constants<COT>(a, cst, co0, tid, NW * 64);
+  if (!FLIP && a.xform) {  // the previous BN's affine map (bn_apply's coefficients)
+    for (int c = tid; c < NP * 32; c += NW * 64) {
+      float m, is, var;
+      bn_scale_shift(a.xbn, c, xss[c], xss[NP * 32 + c], m, is, var);
+    }
+    if (blockIdx.x == 0) bn_finalize(a.xbn);  // saved mean / invstd, running statistics
+  }
   float q0[FN][4], q1[FN][4], q2[FN][4];
 #pragma unroll
   for (int i = 0; i < FN; ++i)
@@ -470,6 +478,32 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
     for (int j = 0; j < RW; ++j) pix[j] = ((size_t)n * a.P + oh0 + wave * RW + j) * a.Q + ow0 + (lane & 15);
     TileEpi<FN, RW, FLIP, PREF, false> epi;
     if (PREF) epi.fetch(a, pix, co0, lane);
+    if (!FLIP && a.xform) {
+      // relu(y * scale + shift) of every in-image halo pixel, in place (the
+      // zero-filled conv padding stays 0); the interior is the stored activation
+      char* Hb = hl + b * HBUF;
+      for (int idx = tid; idx < NP * HPR * 4; idx += NW * 64) {
+        const int p = idx / (HPR * 4), rem = idx - p * (HPR * 4);
+        const int row = rem >> 2, ch = rem & 3;
+        if (row >= (TH + 2) * kHW) continue;
+        const int hr = row / kHW, hc = row - hr * kHW;
+        const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
+        if ((unsigned)ih >= (unsigned)a.H || (unsigned)iw >= (unsigned)a.W) continue;
+        uint4* q = reinterpret_cast<uint4*>(Hb + p * PANEL + ws_off(row, ch));
+        const int c0 = p * 32 + ch * 8;
+        float v[8];
+        unpack8(*q, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = v[k] * xss[c0 + k] + xss[NP * 32 + c0 + k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
+        const uint4 o = pack8(v);
+        *q = o;
+        if (cg == 0 && hr >= 1 && hr <= TH && hc >= 1 && hc <= 16)
+          *reinterpret_cast<uint4*>(a.xh + (((size_t)n * a.H + ih) * a.W + iw) * a.ldxh + c0) = o;
+      }
+      lds_barrier();  // transformed halo visible to every wave (DMA / h stores stay in flight)
+    }
     const char* H = hl + b * HBUF;
     f32x4 acc[RW][FN];
 #pragma unroll
@@ -837,7 +871,8 @@ template <int NP, int FN, int TH, int NW, bool FLIP>
 static hipError_t launch_ws(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int COT = FN * 16;
   constexpr int HPR = ((TH + 2) * kHW + 15) / 16 * 16;
-  constexpr size_t lds = (size_t)9 * NP * COT * 64 + 2 * (size_t)NP * HPR * 64 + kEpiConsts * COT * sizeof(float);
+  constexpr size_t lds = (size_t)9 * NP * COT * 64 + 2 * (size_t)NP * HPR * 64 + kEpiConsts * COT * sizeof(float) +
+                         (FLIP ? 0 : 2 * NP * 32 * sizeof(float));
   static_assert(lds <= 163840, "LDS");
   const int ncg = (a.Cout + COT - 1) / COT;
   const int ntiles = a.N * (a.P / TH) * (a.Q / 16);
@@ -924,6 +959,22 @@ static hipError_t launch_halo_shape(const ConvFwdArgs& a, hipStream_t st) {
 }
 
 static int g_halo_disabled = std::getenv("UNET_NO_HALO") != nullptr;  // A/B switch for measurements
+
+// the default weight-stationary selections of launch_halo_shape<false> (the
+// launcher checks the same; xform is only supported there)
+static bool ws_fwd_shape(const ConvFwdArgs& a) {
+  const int C = a.C, Co = a.Cout;
+  return (C == 64 && Co % 64 == 0 && a.P % 16 == 0) || (C == 32 && Co == 32 && a.P % 16 == 0) ||
+         (C == 32 && Co == 96 && a.P % 16 == 0) || (C == 32 && Co % 64 == 0 && a.P % 16 == 0) ||
+         (C == 96 && Co == 32 && a.P % 8 == 0);
+}
+
+bool conv3x3_ws_xform_ok(const ConvFwdArgs& a) {
+  static const bool wscfg = std::getenv("UNET_WSCFG") != nullptr;
+  return !g_halo_disabled && !wscfg && a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.H == a.P &&
+         a.W == a.Q && a.Q % 16 == 0 && a.ldx % 8 == 0 && a.ldy % 4 == 0 && !a.x2 && !a.fold_on && !a.add &&
+         !a.bb.sums && a.ldxh % 8 == 0 && ws_fwd_shape(a) && (size_t)a.N * a.H * a.W * a.ldx * 2 < 0x80000000ull;
+}
 void set_conv_ws(int on) { g_halo_disabled = on ? 0 : 1; }
 
 // 3x3 / s1 / p1 conv (mode 0) or its data gradient (mode 1, dgrad weight pack)
@@ -942,6 +993,7 @@ hipError_t launch_conv3x3_ws(const ConvFwdArgs& a, int mode, hipStream_t st) {
   // forward epilogue: bias, BN sums, or the eval-folded BN (+ residual addend, ReLU)
   if (mode == 0 && (a.bb.sums || (a.add && !a.fold_on))) return hipErrorNotSupported;
   if (mode == 1 && a.fold_on) return hipErrorNotSupported;
+  if (a.xform && (mode != 0 || !conv3x3_ws_xform_ok(a))) return hipErrorInvalidValue;
   return mode == 0 ? launch_halo_shape<false>(a, st) : launch_halo_shape<true>(a, st);
 }
 

@@ -1949,6 +1949,7 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a0, int mode, hipStream_t st) {
       const hipError_t e = launch_conv3x3_ws(a, mode == MODE_TRANS ? 1 : 0, st);
       if (e != hipErrorNotSupported) return e;
     }
+    if (a.xform) return hipErrorInvalidValue;  // the BN-apply prologue exists in the weight-stationary kernel only
     if (mode == MODE_TRANS) {
       if (a.P % a.stride || a.Q % a.stride) return hipErrorInvalidValue;
       if (g_cfg_override <= 0) {

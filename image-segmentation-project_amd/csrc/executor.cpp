@@ -187,6 +187,10 @@ struct unet_plan {
   // stem BN-backward apply fused into the stem weight gradient's dY load
   // (UNET_NO_STEM_FUSE=1: separate apply pass writing dY, A/B only)
   bool stem_bn_fuse = std::getenv("UNET_NO_STEM_FUSE") == nullptr;
+  // BN1 + ReLU of a block / decoder level applied in the staging of the next
+  // (weight-stationary) conv, which also stores the activation: no bn_apply
+  // pass (UNET_NO_BN_XFORM=1: separate pass, A/B only)
+  bool bn_xform = std::getenv("UNET_NO_BN_XFORM") == nullptr;
   // BasicBlock downsample (1x1 / s2) weight gradient folded into the conv1
   // (3x3 / s2) halo weight gradient (UNET_NO_DS_FOLD=1: separate launch, A/B)
   bool ds_wgrad_fold = std::getenv("UNET_NO_DS_FOLD") == nullptr;
@@ -827,10 +831,13 @@ const std::string& pname(const Ctx& x, int param) { return x.p->params[param].na
 // fold_bn >= 0 (eval only): that BN (running statistics) is applied in the
 // conv epilogue, then `res` is added and ReLU applied (relu), so the BN pass
 // after the conv disappears (§8(f) row 4)
+// xbn >= 0 (training): `in` is the RAW output of the previous conv; BN xbn +
+// ReLU is applied while staging and the activation is stored to *xh by the
+// conv itself (ConvFwdArgs::xform), replacing that BN's bn_apply pass
 int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for_stats, int fold_bn = -1,
-                 bool relu = false, const Act* res = nullptr) {
+                 bool relu = false, const Act* res = nullptr, int xbn = -1, const Act* xh = nullptr) {
   const Conv& cv = x.p->convs[ci];
-  ProfScope ps(x.p, x.st, "fwd " + pname(x, cv.w), conv_flops(x.p, cv, out));
+  ProfScope ps(x.p, x.st, "fwd " + pname(x, cv.w) + (xbn >= 0 ? " +bn" : ""), conv_flops(x.p, cv, out));
   ConvFwdArgs a = {};
   a.x = x.A(in); a.ldx = in.ld;
   a.w = x.W<bf16_t>(cv.pk_fwd);
@@ -848,6 +855,11 @@ int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for
   a.N = x.p->cfg.N; a.H = in.H; a.W = in.W; a.C = cv.Ci;
   a.P = out.H; a.Q = out.W; a.Cout = cv.Co;
   a.R = cv.R; a.S = cv.S; a.stride = cv.stride; a.pad = cv.pad;
+  if (xbn >= 0) {
+    a.xbn = bn_launch(x, xbn, (int64_t)x.p->cfg.N * in.H * in.W);
+    a.xh = x.A(*xh); a.ldxh = xh->ld;
+    a.xform = 1;
+  }
   if (cv.f8) {  // e4m3 operands: quantize the input once per forward, block-scaled MFMA
     unet_plan* p = x.p;
     int fi = -1;
@@ -870,6 +882,21 @@ int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for
   }
   CK(launch_conv_fwd(a, cv.kind == L_CONVT ? MODE_SHUF : MODE_FWD, x.st));
   return 0;
+}
+
+// can conv `ci` (input: raw y of BN bi's conv, output `out`) apply that BN +
+// ReLU in its staging and store the activation `h` itself?
+bool xform_ok(const Ctx& x, int ci, const Act& yraw, const Act& h, const Act& out) {
+  const unet_plan* p = x.p;
+  if (!x.training || !p->bn_xform || p->bn_ticket) return false;
+  const Conv& cv = p->convs[ci];
+  if (cv.f8 || cv.kind != L_CONV || h.H != yraw.H || h.W != yraw.W || h.C != yraw.C) return false;
+  ConvFwdArgs a = {};
+  a.ldx = yraw.ld; a.ldy = out.ld; a.ldxh = h.ld;
+  a.N = p->cfg.N; a.H = yraw.H; a.W = yraw.W; a.C = cv.Ci;
+  a.P = out.H; a.Q = out.W; a.Cout = cv.Co;
+  a.R = cv.R; a.S = cv.S; a.stride = cv.stride; a.pad = cv.pad;
+  return conv3x3_ws_xform_ok(a);
 }
 
 // conv dgrad: dx = dgrad(dy) (+ addend).  fuse: dx is dA of that BN(+ReLU);
@@ -1268,8 +1295,12 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
       continue;
     }
     RUN(conv_forward(x, b.conv1, b.in, b.y1, b.bn1));
-    RUN(bn_apply(x, b.bn1, b.y1, b.h, 0, nullptr, -1, true));
-    RUN(conv_forward(x, b.conv2, b.h, b.y2, b.bn2));
+    if (xform_ok(x, b.conv2, b.y1, b.h, b.y2)) {  // bn1 + ReLU inside conv2's staging
+      RUN(conv_forward(x, b.conv2, b.y1, b.y2, b.bn2, -1, false, nullptr, b.bn1, &b.h));
+    } else {
+      RUN(bn_apply(x, b.bn1, b.y1, b.h, 0, nullptr, -1, true));
+      RUN(conv_forward(x, b.conv2, b.h, b.y2, b.bn2));
+    }
     if (b.ds >= 0) {
       RUN(conv_forward(x, b.ds, b.in, b.yds, b.dsbn));
       RUN(bn_apply(x, b.bn2, b.y2, b.out, 2, &b.yds, b.dsbn, true));
@@ -1287,8 +1318,12 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
       RUN(conv_forward(x, d.conv2, d.h, d.out, -1, d.bn2, true));
     } else {
       RUN(conv_forward(x, d.conv1, d.cat, d.y1, d.bn1));
-      RUN(bn_apply(x, d.bn1, d.y1, d.h, 0, nullptr, -1, true));
-      RUN(conv_forward(x, d.conv2, d.h, d.y2, d.bn2));
+      if (xform_ok(x, d.conv2, d.y1, d.h, d.y2)) {
+        RUN(conv_forward(x, d.conv2, d.y1, d.y2, d.bn2, -1, false, nullptr, d.bn1, &d.h));
+      } else {
+        RUN(bn_apply(x, d.bn1, d.y1, d.h, 0, nullptr, -1, true));
+        RUN(conv_forward(x, d.conv2, d.h, d.y2, d.bn2));
+      }
       RUN(bn_apply(x, d.bn2, d.y2, d.out, 0, nullptr, -1, true));
     }
     if (att) RUN(ch_att_forward(x, l));

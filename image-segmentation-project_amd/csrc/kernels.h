@@ -88,6 +88,14 @@ struct ConvFwdArgs {
   // fp8 forward (launch_conv_fwd_f8): x / w are e4m3 bytes (x dense, ldx = C;
   // w packed [Cout][R*S*C]) whose dequant codes the kernel reads from f8x / f8w
   const F8State* f8x; const F8State* f8w;
+  // BN(+ReLU) of the PREVIOUS conv applied while staging (xform != 0;
+  // weight-stationary 3x3 forward, training): x holds that conv's raw output y,
+  // every staged halo pixel becomes relu(y * scale + shift) of BN `xbn` (batch
+  // statistics, bn_apply's expression, so bit-identical), padding stays 0, the
+  // tile interior is stored to xh (= the BN+ReLU activation the backward
+  // needs) and block 0 finalises that BN (saved / running statistics): the
+  // standalone bn_apply pass disappears.
+  BnLaunch xbn; bf16_t* xh; int ldxh; int xform;
   int N, H, W, C;                // input geometry (C = GEMM reduction channels)
   int P, Q, Cout;                // output geometry
   int R, S, stride, pad;
@@ -141,6 +149,9 @@ hipError_t launch_conv_fwd_v1(const ConvFwdArgs& a, int mode, hipStream_t st);  
 // weight-stationary halo kernel for 3x3/s1/p1 layers with few channels
 // (conv_halo.hip); mode 0 conv, 1 dgrad.  hipErrorNotSupported if not covered.
 hipError_t launch_conv3x3_ws(const ConvFwdArgs& a, int mode, hipStream_t st);
+// the forward of this shape runs on the weight-stationary halo kernel, which
+// supports ConvFwdArgs::xform (the BN-apply prologue)
+bool conv3x3_ws_xform_ok(const ConvFwdArgs& a);
 void set_conv_ws(int on);
 // 3x3 / stride-2 / pad-1 data gradient by parity class on a shared dY halo
 // (conv_halo.hip), with the optional folded downsample (x2 / w2) range

@@ -1,0 +1,41 @@
+"""BN1 + ReLU applied inside the next weight-stationary conv's halo staging
+(ConvFwdArgs::xform) against the separate bn_apply pass it
+replaces: the stored activations h, every later tensor, the logits, the loss
+gradient path and the BN running statistics must be BIT-identical (the prologue
+evaluates bn_apply's expression with bn_apply's coefficients), at a size where
+enc1 / decoder2 / decoder1 run on the weight-stationary kernel."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(pkg, sd, x, y):
+    m = pkg.UNetWithBackbone(pretrained=False)
+    m.load_state_dict(sd)
+    m = m.cuda().train()
+    out = m(x)
+    pkg.get_loss_function({"loss_fn": "bce"})(out, y).backward()
+    torch.cuda.synchronize()
+    views = m._last_plan.tensor_views()
+    grads = {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+    bufs = {k: b.detach().clone() for k, b in m.named_buffers()}
+    return out.detach().clone(), views, grads, bufs
+
+
+def test_bn_prologue_bit_identical(pkg, cuda, monkeypatch):
+    torch.manual_seed(0)
+    sd = {k: v.detach().clone() for k, v in pkg.UNetWithBackbone(pretrained=False).state_dict().items()}
+    xs, ms = pkg.synthetic_cells(2, 128, 128, seed=21)
+    x, y = torch.from_numpy(xs).cuda(), torch.from_numpy(ms).cuda()
+    monkeypatch.delenv("UNET_NO_BN_XFORM", raising=False)
+    fused = _run(pkg, sd, x, y)
+    monkeypatch.setenv("UNET_NO_BN_XFORM", "1")  # read when the native plan is created
+    plain = _run(pkg, sd, x, y)
+    assert torch.equal(fused[0], plain[0])
+    for k in ["enc1.0.h", "enc1.1.h", "enc1.2.h", "dec2.h", "dec1.h"]:
+        assert torch.equal(fused[1][k], plain[1][k]), k
+    for k, v in plain[2].items():
+        assert torch.equal(fused[2][k], v), k
+    for k, v in plain[3].items():
+        assert torch.equal(fused[3][k], v), k
