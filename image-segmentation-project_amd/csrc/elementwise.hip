@@ -1063,36 +1063,93 @@ hipError_t launch_pack(const PackTable& t, hipStream_t st) {
   return hipGetLastError();
 }
 
+// Kernel-layout accumulators -> torch layout.  Conv [Co][T][Ci] -> [Co][Ci][T]
+// and convT [Ci][T][Co] -> [Ci][Co][T] (T = R*S) are per-row [T][K] -> [K][T]
+// transposes: a block stages <= 512 columns of a row in LDS with contiguous
+// reads and writes the transposed run contiguously (row stride 513: no bank
+// conflicts on the transposed read).  Stem [64][64] (k = r*8+s) keeps the
+// element map; UP_ZERO writes zeros.
+constexpr int kUpK = 512, kUpT = 9;
 __global__ void __launch_bounds__(256) unpack_kernel(UnpackTable t) {
   const UnpackEntry e = t.e[blockIdx.y];
-  const int Co = e.Co, Ci = e.Ci, R = e.R, S = e.S;
-  const int total = (int)Co * Ci * R * S;
-  for (int i = (int)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int)gridDim.x * blockDim.x) {
-    float v;
-    if (e.kind == UP_CONV) {  // dst[co][ci][r][s] <- acc[co][r][s][ci]
-      const int s = (int)(i % S); int q = i / S;
-      const int r = (int)(q % R); q /= R;
-      const int ci = (int)(q % Ci); const int co = (int)(q / Ci);
-      v = e.acc[(((int)co * R + r) * S + s) * Ci + ci];
-    } else if (e.kind == UP_CONVT) {  // dst W[ci][co][a][b] <- acc[ci][a][b][co]  (Ci = in ch)
-      const int b = (int)(i % S); int q = i / S;
-      const int aa = (int)(q % R); q /= R;
-      const int co = (int)(q % Co); const int ci = (int)(q / Co);
-      v = e.acc[(((int)ci * R + aa) * S + b) * Co + co];
-    } else if (e.kind == UP_ZERO) {  // a gradient that is exactly 0 (bias feeding a training-mode BN)
-      v = 0.f;
-    } else {  // UP_STEM: dst[co][0][r][s] <- acc[co][r*8+s] (row length 64)
-      const int k = (int)(i % 49), co = (int)(i / 49);
-      const int r = k / 7, ss = k - r * 7;
-      v = e.acc[(int)co * 64 + r * 8 + ss];
+  if (e.kind == UP_ZERO || e.kind == UP_STEM) {
+    const int total = e.kind == UP_ZERO ? e.Co : e.Co * 49;
+    for (int i = (int)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int)gridDim.x * blockDim.x) {
+      float v = 0.f;  // UP_ZERO: a gradient that is exactly 0 (bias feeding a training-mode BN)
+      if (e.kind == UP_STEM) {  // dst[co][0][r][s] <- acc[co][r*8+s] (row length 64)
+        const int k = i % 49, co = i / 49;
+        const int r = k / 7, ss = k - r * 7;
+        v = e.acc[co * 64 + r * 8 + ss];
+      }
+      e.dst[i] = v;
     }
-    e.dst[i] = v;
+    return;
+  }
+  __shared__ float lds[kUpT * (kUpK + 1)];
+  const bool convt = e.kind == UP_CONVT;
+  const int rows = convt ? e.Ci : e.Co, K = convt ? e.Co : e.Ci, T = e.R * e.S;
+  for (int a = blockIdx.x; a < rows; a += gridDim.x) {
+    const float* src = e.acc + (size_t)a * K * T;
+    float* dst = e.dst + (size_t)a * K * T;
+    for (int k0 = 0; k0 < K; k0 += kUpK) {
+      const int nk = min(kUpK, K - k0);
+      // 16-B loads / stores (all of a thread's loads in flight before the LDS
+      // stores) when both rows are 16-B aligned (a parameter after an odd-sized
+      // one may not be)
+      const bool v4 = (K & 3) == 0 && ((reinterpret_cast<uintptr_t>(e.acc) | reinterpret_cast<uintptr_t>(e.dst)) & 15) == 0;
+      if (v4) {
+        const int n4 = T * nk / 4, q4 = nk / 4;
+        constexpr int kPer = (kUpT * kUpK / 4 + 255) / 256;  // <= 5 float4 per thread
+        float4 v[kPer];
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+          const int i = threadIdx.x + 256 * u;
+          if (i < n4) {
+            const int tt = i / q4, k = (i - tt * q4) * 4;
+            v[u] = *reinterpret_cast<const float4*>(src + (size_t)tt * K + k0 + k);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+          const int i = threadIdx.x + 256 * u;
+          if (i < n4) {
+            const int tt = i / q4, k = (i - tt * q4) * 4;
+            float* l = lds + tt * (kUpK + 1) + k;
+            l[0] = v[u].x; l[1] = v[u].y; l[2] = v[u].z; l[3] = v[u].w;
+          }
+        }
+        __syncthreads();
+        float* d = dst + (size_t)k0 * T;  // the run [k0*T, (k0+nk)*T) is contiguous, 16-B aligned
+        for (int i = threadIdx.x; i < n4; i += blockDim.x) {
+          float o[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int j = 4 * i + c, k = j / T, tt = j - k * T;
+            o[c] = lds[tt * (kUpK + 1) + k];
+          }
+          *reinterpret_cast<float4*>(d + 4 * i) = make_float4(o[0], o[1], o[2], o[3]);
+        }
+        __syncthreads();
+        continue;
+      }
+      for (int i = threadIdx.x; i < T * nk; i += blockDim.x) {
+        const int tt = i / nk, k = i - tt * nk;
+        lds[tt * (kUpK + 1) + k] = src[(size_t)tt * K + k0 + k];
+      }
+      __syncthreads();
+      for (int i = threadIdx.x; i < T * nk; i += blockDim.x) {
+        const int k = i / T, tt = i - k * T;
+        dst[(size_t)(k0 + k) * T + tt] = lds[tt * (kUpK + 1) + k];
+      }
+      __syncthreads();
+    }
   }
 }
 
 hipError_t launch_unpack(const UnpackTable& t, hipStream_t st) {
   if (t.n <= 0) return hipSuccess;
+  for (int i = 0; i < t.n; ++i)
+    if ((t.e[i].kind == UP_CONV || t.e[i].kind == UP_CONVT) && t.e[i].R * t.e[i].S > kUpT) return hipErrorInvalidValue;
   hipLaunchKernelGGL(unpack_kernel, dim3(512, t.n), dim3(256), 0, st, t);
   return hipGetLastError();
 }
