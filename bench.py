@@ -31,18 +31,24 @@ MFMA_FP8_PEAK_TFLOPS = 5000.0  # MI355X dense fp8 (block-scaled e4m3 MFMA, MI355
 HBM_PEAK_GBS = 8000.0
 
 
-def pmc_traffic(kernel: str):
+def config_key(backbone: str, width: int, attention: bool, fp8: bool, batch: int, size: int) -> str:
+    """Workload key of a PMC profile (scripts/pmc_traffic.py --config)."""
+    return f"{backbone}/w{width}/{'attention' if attention else 'plain'}/{'fp8' if fp8 else 'bf16'}/{batch}x{size}"
+
+
+# files written before the config key existed profiled layer_profile.py's default workload
+LEGACY_CONFIG = config_key("resnet34", 1, False, False, 16, 512)
+
+
+def pmc_traffic(kernel: str, config: str):
     """(HBM bytes per launch of `kernel`, source file) from the newest committed
-    rocprofv3 PMC summary (scripts/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE,
-    MI355X_MICROARCH.md HBM section; PMC passes cannot run inside the timed
-    bench), or (None, None) when that kernel was not profiled."""
+    rocprofv3 PMC summary OF THIS WORKLOAD (scripts/pmc_traffic.py: FETCH_SIZE
+    x2 + WRITE_SIZE, MI355X_MICROARCH.md HBM section; PMC passes cannot run
+    inside the timed bench), or (None, None) when no profile of this config
+    holds that kernel: bytes measured on another config are never quoted."""
     import glob
-    found = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "*", "pmc_traffic.json")))
-    if not found:
-        return None, None
-    path = found[-1]  # newest profiling session of the newest round
-    with open(path) as f:
-        table = json.load(f)
+    found = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "*", "pmc_traffic*.json")),
+                   key=lambda p: (os.path.dirname(p), p))
     # rocprof names spell out defaulted template arguments ("..., false>")
     # that the executor's kernel tag leaves off
     def canon(name: str) -> str:
@@ -51,9 +57,16 @@ def pmc_traffic(kernel: str):
             name = name[: -len(",false>")] + ">"
         return name
     want = canon(kernel)
-    for key, ent in table.items():
-        if canon(key) == want:
-            return ent["bytes_per_launch"], os.path.relpath(path, REPO)
+    for path in reversed(found):  # newest profiling session of the newest round first
+        with open(path) as f:
+            doc = json.load(f)
+        cfg, table = (doc["config"], doc["kernels"]) if "kernels" in doc else (LEGACY_CONFIG, doc)
+        if cfg != config:
+            continue
+        for key, ent in table.items():
+            if canon(key) == want:
+                return ent["bytes_per_launch"], os.path.relpath(path, REPO)
+        return None, None  # the newest profile of this config lacks the kernel (e.g. a renamed instance)
     return None, None
 
 
@@ -286,7 +299,8 @@ def main():
     dom_ms, dom_fl, dom_n = by_kernel[dom]
     achieved_tflops = dom_fl / 1e9 / dom_ms
     dom_peak = MFMA_FP8_PEAK_TFLOPS if dom.startswith("conv_f8_kernel") else MFMA_BF16_PEAK_TFLOPS
-    traffic, traffic_src = pmc_traffic(dom)
+    traffic, traffic_src = pmc_traffic(dom, config_key(args.backbone, args.width, args.attention, args.fp8,
+                                                        args.batch, args.size))
     dom_us = dom_ms / dom_n * 1e3
     line = {
         "metric": "images/sec + mIoU, 512x512 U-Net bf16 at 1/2/4/8 MI355X",

@@ -183,7 +183,10 @@ __global__ void __launch_bounds__(1024) normalize_kernel(const uint8_t* __restri
   __syncthreads();
   const double plo = s.plo, phi = s.phi;
   // tile histograms of the clipped image, padded to a multiple of the grid by reflection
-  const int He = H + (kGrid - H % kGrid) % kGrid, We = W + (kGrid - W % kGrid) % kGrid;
+  // clahe.cpp pads BOTH sides by kGrid - size % kGrid when EITHER is not a
+  // multiple of the grid (a side that is a multiple gains a whole tile)
+  const bool pad = (H % kGrid) != 0 || (W % kGrid) != 0;
+  const int He = pad ? H + kGrid - H % kGrid : H, We = pad ? W + kGrid - W % kGrid : W;
   const int th = He / kGrid, tw = We / kGrid;
   for (int64_t i = tid; i < (int64_t)He * We; i += blockDim.x) {
     const int y = (int)(i / We), x = (int)(i % We);

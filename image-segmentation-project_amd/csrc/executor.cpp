@@ -871,7 +871,7 @@ int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for
     if (!p->f8_done[fi]) {
       ProfScope pq(p, x.st, "f8_quant " + pname(x, cv.w), 0);
       CK(launch_f8_quant_act(x.A(in), in.ld, in.C, (int64_t)a.N * in.H * in.W, x.W<uint8_t>(f.q), sts + f.st,
-                             p->f8_calibrated ? 0 : 1, x.st));
+                             (p->f8_calibrated ? 0 : F8_CALIBRATE) | (x.training ? 0 : F8_FROZEN), x.st));
       p->f8_done[fi] = 1;
     }
     a.x = reinterpret_cast<const bf16_t*>(x.W<uint8_t>(f.q)); a.ldx = in.C;
@@ -1199,14 +1199,16 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
   const int N = p->cfg.N;
   CK(hipMemsetAsync(ws + p->zero_fwd_off, 0, p->zero_fwd_bytes, st));
   if (p->f8n) {  // fp8 scale states: calibrate on the plan's first forward, else roll
+    // (training only: an eval forward quantizes with the scales in use and
+    // commits no amax, so validation never moves the training scales)
     if (!p->f8_calibrated) CK(hipMemsetAsync(ws + p->f8st, 0, (size_t)p->f8n * sizeof(F8State), st));
-    else CK(launch_f8_roll(x.W<F8State>(p->f8st), p->f8n, st));
+    else if (training) CK(launch_f8_roll(x.W<F8State>(p->f8st), p->f8n, st));
     std::fill(p->f8_done.begin(), p->f8_done.end(), 0);
     for (auto& cv : p->convs)
       if (cv.f8) {
         ProfScope ps(p, st, "f8_pack " + pname(x, cv.w), 0);
         CK(launch_f8_pack_w(prm[cv.w], cv.Co, cv.Ci, cv.R, cv.S, x.W<uint8_t>(cv.f8w), x.W<F8State>(p->f8st) + cv.f8st,
-                            p->f8_calibrated ? 0 : 1, st));
+                            (p->f8_calibrated ? 0 : F8_CALIBRATE) | (training ? 0 : F8_FROZEN), st));
       }
   }
   // pack weights (fp32 torch layout -> bf16 kernel layouts)

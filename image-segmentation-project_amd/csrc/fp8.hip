@@ -80,9 +80,10 @@ __global__ void __launch_bounds__(256) f8_amax_f32_kernel(const float* w, int64_
 }
 
 // q[px][c] = e4m3(x[px*ld + c] * 2^e), dense [npix][C]; 8 channels per thread
-// iteration; this step's amax accumulates into cur
+// iteration; this step's amax accumulates into cur (commit != 0; an eval
+// forward quantizes with the scale in use and leaves the training amax alone)
 __global__ void __launch_bounds__(256) f8_quant_act_kernel(const bf16_t* x, int ld, int C, int64_t npix,
-                                                           uint8_t* q, F8State* s) {
+                                                           uint8_t* q, F8State* s, int commit) {
   const int e = f8_exponent(s->prev_bits);
   if (blockIdx.x == 0 && threadIdx.x == 0) s->code = 127 - e;
   const unsigned cpr = (unsigned)C >> 3;
@@ -103,7 +104,7 @@ __global__ void __launch_bounds__(256) f8_quant_act_kernel(const bf16_t* x, int 
     o.y = f8_pack4(f[4], f[5], f[6], f[7]);
     *reinterpret_cast<uint2*>(q + (size_t)px * C + c) = o;
   }
-  f8_amax_commit(m, &s->cur_bits);
+  if (commit) f8_amax_commit(m, &s->cur_bits);  // kernel-uniform: the barrier inside is reached by all
 }
 
 // conv weights fp32 [Co][Ci][RS] -> e4m3 [Co][RS][Ci] (the forward pack layout
@@ -111,7 +112,7 @@ __global__ void __launch_bounds__(256) f8_quant_act_kernel(const bf16_t* x, int 
 // neighbouring threads' runs are adjacent) and writes one byte per tap
 // (neighbouring threads: neighbouring bytes)
 __global__ void __launch_bounds__(256) f8_pack_w_kernel(const float* w, int Co, int Ci, int RS, uint8_t* dst,
-                                                        F8State* s) {
+                                                        F8State* s, int commit) {
   const int e = f8_exponent(s->prev_bits);
   if (blockIdx.x == 0 && threadIdx.x == 0) s->code = 127 - e;
   const unsigned units = (unsigned)Co * Ci;
@@ -126,7 +127,7 @@ __global__ void __launch_bounds__(256) f8_pack_w_kernel(const float* w, int Co, 
       d[(size_t)t * Ci] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(f8_sat(ldexpf(v, e)), 0.f, 0, false) & 0xff);
     }
   }
-  f8_amax_commit(m, &s->cur_bits);
+  if (commit) f8_amax_commit(m, &s->cur_bits);
 }
 
 static int grid_for(int64_t units) {
@@ -145,12 +146,13 @@ hipError_t launch_f8_quant_act(const bf16_t* x, int ld, int C, int64_t npix, uin
                                hipStream_t st) {
   if (C % 16 || ld % 8 || npix * (C >> 3) >= 0x7fffffffLL) return hipErrorInvalidValue;
   const int g = grid_for(npix * (C >> 3));
-  if (calibrate) {
+  const int commit = calibrate & F8_FROZEN ? 0 : 1;
+  if (calibrate & F8_CALIBRATE) {
     hipLaunchKernelGGL(f8_amax_act_kernel, dim3(g), dim3(256), 0, st, x, ld, C, npix, s);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(f8_quant_act_kernel, dim3(g), dim3(256), 0, st, x, ld, C, npix, q, s);
+  hipLaunchKernelGGL(f8_quant_act_kernel, dim3(g), dim3(256), 0, st, x, ld, C, npix, q, s, commit);
   return hipGetLastError();
 }
 
@@ -159,12 +161,13 @@ hipError_t launch_f8_pack_w(const float* w, int Co, int Ci, int R, int S, uint8_
   if (Ci % 16) return hipErrorInvalidValue;
   const int64_t n = (int64_t)Co * Ci * R * S;
   if (n >= 0x7fffffffLL) return hipErrorInvalidValue;
-  if (calibrate) {
+  const int commit = calibrate & F8_FROZEN ? 0 : 1;
+  if (calibrate & F8_CALIBRATE) {
     hipLaunchKernelGGL(f8_amax_f32_kernel, dim3(grid_for(n)), dim3(256), 0, st, w, n, s);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(f8_pack_w_kernel, dim3(grid_for((int64_t)Co * Ci)), dim3(256), 0, st, w, Co, Ci, R * S, dst, s);
+  hipLaunchKernelGGL(f8_pack_w_kernel, dim3(grid_for((int64_t)Co * Ci)), dim3(256), 0, st, w, Co, Ci, R * S, dst, s, commit);
   return hipGetLastError();
 }
 

@@ -162,7 +162,11 @@ hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st);
 // fp8 e4m3 implicit-GEMM forward conv (MODE_FWD geometry, any R/S/stride/pad,
 // C % 16 == 0), block-scaled MFMA dequantizing with the F8State codes
 hipError_t launch_conv_fwd_f8(const ConvFwdArgs& a, hipStream_t st);
-// fp8.hip: delayed-amax quantization of activations / conv weights
+// fp8.hip: delayed-amax quantization of activations / conv weights.  `calibrate`
+// flags: F8_CALIBRATE = amax pass into prev first (a plan's first forward);
+// F8_FROZEN = quantize with the scale in use and do NOT accumulate this call's
+// amax (eval forwards: validation must not steer the next training step's scale)
+enum { F8_CALIBRATE = 1, F8_FROZEN = 2 };
 hipError_t launch_f8_roll(F8State* s, int n, hipStream_t st);
 hipError_t launch_f8_quant_act(const bf16_t* x, int ld, int C, int64_t npix, uint8_t* q, F8State* s, int calibrate,
                                hipStream_t st);

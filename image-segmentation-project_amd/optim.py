@@ -101,6 +101,10 @@ class _FlatGroup:
             for p in self.params:
                 self.state[p]["step"] = self.coef[0]
         else:
+            if self.uniform:
+                # leaving the shared counter: it is the truth (HIP-graph replays
+                # of the step advance it on the device without touching counts)
+                self.counts = [int(self.coef[0].item())] * len(self.params)
             self.pcoef[:, 0] = torch.tensor(self.counts, dtype=torch.float32)
             for i, p in enumerate(self.params):
                 self.state[p]["step"] = self.pcoef[i, 0]

@@ -135,7 +135,9 @@ int unet_convt_wgrad_slab(const void* dy, int lddy, const void* x, int ldx, floa
 /* ---- fp8 e4m3 forward conv (BASELINE.json configs[4]; no reference counterpart:
  * the reference's convs are fp32 torch.nn.Conv2d, advanced_models.py:72-100) ----
  * state: 16-B scale state {amax prev (float bits), amax this step, e8m0 code,
- * pad}, zeroed before first use; calibrate=1 measures amax before quantizing.
+ * pad}, zeroed before first use; calibrate flags: 1 measures amax before
+ * quantizing, 2 ("frozen", eval forwards) quantizes with the scale in use and
+ * does not accumulate this call's amax into the state.
  * q = sat448(v * 2^e) with 2 * amax_prev * 2^e <= 448, code = 127 - e.
  * unet_f8_quantize: bf16 [npix][C] (stride ld) -> dense e4m3 [npix][C].
  * unet_f8_pack_weight: fp32 [Co][Ci][R][S] -> e4m3 [Co][R][S][Ci].

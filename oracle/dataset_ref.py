@@ -28,7 +28,8 @@ are PARITY UNPINNED; numpy's percentile is pinned against numpy itself):
   alpha per source column / row) accumulated horizontally then vertically in
   float, ``cvRound``.  INTER_NEAREST: ``sx = min(floor(dx * (ssize/dsize)), ssize-1)``.
 * ``cv2.CLAHE`` (imgproc/src/clahe.cpp, 8-bit path): tile grid 8x8 (BORDER_REFLECT_101
-  padding to a multiple of the grid), clip limit max(int(2.0 * tileArea / 256), 1),
+  padding when either side is not a multiple of the grid: both sides by
+  ``grid - size % grid``, so a side that is a multiple gains a whole tile), clip limit max(int(2.0 * tileArea / 256), 1),
   excess redistributed as ``clipped // 256`` per bin + a residual every
   ``max(256 // residual, 1)`` bins, LUT = saturate(round(cumsum * 255 / tileArea)),
   bilinear interpolation between the 4 nearest tile LUTs in float
@@ -131,11 +132,19 @@ def resize_nearest_u8(img: np.ndarray, oh: int, ow: int) -> np.ndarray:
     return img[ys][:, xs]
 
 
+def clahe_padding(h: int, w: int, grid: int = 8):
+    """clahe.cpp: when EITHER side is not a multiple of the grid, BOTH are
+    padded (bottom / right, BORDER_REFLECT_101) by grid - size % grid, so a side
+    that already is a multiple gains a whole tile."""
+    if h % grid or w % grid:
+        return grid - h % grid, grid - w % grid
+    return 0, 0
+
+
 def clahe_u8(img: np.ndarray, clip_limit: float = 2.0, grid: int = 8) -> np.ndarray:
     """cv2.createCLAHE(clipLimit, (grid, grid)).apply(img) for uint8."""
     h, w = img.shape
-    ph = (grid - h % grid) % grid
-    pw = (grid - w % grid) % grid
+    ph, pw = clahe_padding(h, w, grid)
     ext = np.pad(img, ((0, ph), (0, pw)), mode="reflect") if (ph or pw) else img  # BORDER_REFLECT_101
     th, tw = ext.shape[0] // grid, ext.shape[1] // grid
     area = th * tw

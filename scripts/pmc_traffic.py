@@ -3,8 +3,10 @@ passes (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950), corrected as
 MI355X_MICROARCH.md's HBM section prescribes: FETCH_SIZE counts 64 B per 128-B
 request, so it is doubled; WRITE_SIZE is taken as is.  Both are in KiB.
 
-usage: python scripts/pmc_traffic.py <fetch_dir> <write_dir> [out.json]
-(scripts/profile_round.sh runs the passes and this script)."""
+usage: python scripts/pmc_traffic.py <fetch_dir> <write_dir> [out.json] [--config KEY]
+(scripts/profile_round.sh runs the passes and this script).  KEY names the
+workload the passes profiled (bench.config_key: backbone/width/decoder/dtype/
+batch x size); bench.py quotes bytes only from a file of its own config."""
 import csv
 import glob
 import json
@@ -33,8 +35,14 @@ def load(d, counter):
 
 
 def main():
-    fetch, write = load(sys.argv[1], "FETCH_SIZE"), load(sys.argv[2], "WRITE_SIZE")
-    out_path = sys.argv[3] if len(sys.argv) > 3 else "profiles/pmc_traffic.json"
+    argv = list(sys.argv[1:])
+    config = "resnet34/w1/plain/bf16/16x512"  # layer_profile.py's default workload
+    if "--config" in argv:
+        i = argv.index("--config")
+        config = argv[i + 1]
+        del argv[i:i + 2]
+    fetch, write = load(argv[0], "FETCH_SIZE"), load(argv[1], "WRITE_SIZE")
+    out_path = argv[2] if len(argv) > 2 else "profiles/pmc_traffic.json"
     table = {}
     for tag in sorted(set(fetch) & set(write)):
         f = sum(fetch[tag]) / len(fetch[tag]) * 1024 * 2
@@ -43,7 +51,7 @@ def main():
                       "launches": len(fetch[tag])}
         print(f"{tag:60s} n={len(fetch[tag]):4d} fetch {f / 1e6:9.2f} MB  write {w / 1e6:9.2f} MB")
     with open(out_path, "w") as fh:
-        json.dump(table, fh, indent=1, sort_keys=True)
+        json.dump({"config": config, "kernels": table}, fh, indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":

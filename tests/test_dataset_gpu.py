@@ -53,7 +53,7 @@ def test_resize_area_bit_exact(pkg, cuda, shape, out):
         assert np.array_equal(got[i], want), (i, int((got[i] != want).sum()))
 
 
-@pytest.mark.parametrize("hw", [(128, 128), (96, 160), (100, 100)])
+@pytest.mark.parametrize("hw", [(128, 128), (96, 160), (100, 100), (256, 250), (250, 256)])
 def test_normalize_bit_exact(pkg, cuda, hw):
     f = np.concatenate([_frames(1, 3, *hw), _frames(2, 1, *hw, kind="noise"),
                         np.full((1, *hw), 77, np.uint8)])
@@ -63,6 +63,14 @@ def test_normalize_bit_exact(pkg, cuda, hw):
         assert np.array_equal(got[i, 0], want), (i, float(np.abs(got[i, 0] - want).max()))
     raw = pkg.preprocess(f, img_size=(hw[1], hw[0]), normalize=False).cpu().numpy()
     assert np.array_equal(raw[:, 0], f.astype(np.float32) / np.float32(255.0))
+
+
+def test_preprocess_upscale_fails_early(pkg, cuda):
+    """frames smaller than img_size (cv2 INTER_AREA enlarging) are
+    rejected with a clear error before any kernel runs."""
+    f = np.zeros((1, 64, 64), np.uint8)
+    with pytest.raises(NotImplementedError, match="upscaling"):
+        pkg.preprocess(f, img_size=(128, 128))
 
 
 def test_preprocess_end_to_end_matches_dataset_getitem(pkg, cuda):

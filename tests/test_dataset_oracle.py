@@ -58,6 +58,14 @@ def test_clahe_properties():
     assert n.dtype == np.float64 and n.min() == 0.0 and abs(n.max() - 1.0) < 1e-7
 
 
+def test_clahe_padding_rule():
+    """OpenCV pads both sides when either is off the grid."""
+    assert D.clahe_padding(64, 64) == (0, 0)
+    assert D.clahe_padding(64, 60) == (8, 4)
+    assert D.clahe_padding(60, 64) == (4, 8)
+    assert D.clahe_padding(100, 100) == (4, 4)
+
+
 def test_rot90_vflip_matches_numpy():
     img = np.arange(48, dtype=np.uint8).reshape(6, 8)
     for k in range(4):

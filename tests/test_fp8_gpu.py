@@ -226,3 +226,44 @@ def test_fp8_training_and_graph_replay(pkg, cuda):
     losses += [float(step()[1]) for _ in range(8)]
     print("fp8 losses", [round(l, 4) for l in losses])
     assert all(np.isfinite(losses)) and losses[-1] < 0.8 * losses[0]
+
+
+def test_fp8_eval_forward_leaves_training_scales(pkg, cuda):
+    """an eval forward (running-statistics BN, e.g. validation
+    between epochs) quantizes with the scales in use and commits no amax, so
+    the next training forward is scaled exactly as if the eval had not run:
+    train fwd -> eval fwd (other data) -> train fwd gives bit-identical logits
+    to train fwd -> train fwd on a twin model."""
+    torch.manual_seed(0)
+    xs, ms = pkg.synthetic_cells(2, 128, 128, seed=11)
+    x = torch.from_numpy(xs).cuda()
+    x_val = 3.0 * torch.from_numpy(pkg.synthetic_cells(2, 128, 128, seed=12)[0]).cuda()  # larger amax
+    outs = []
+    for with_eval in (False, True):
+        torch.manual_seed(0)
+        m = pkg.UNetWithBackbone(pretrained=False, use_attention=False, width=1, fp8=True).cuda().train()
+        with torch.no_grad():
+            m(x)
+            if with_eval:
+                m.eval()
+                m(x_val)
+                m.train()
+            outs.append(m(x).float().cpu())
+    assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max()
+
+
+def test_fp8_quantize_frozen_commits_no_amax(L, cuda):
+    """C ABI: calibrate flag 2 (frozen) quantizes with the state's scale and
+    leaves the accumulating amax untouched."""
+    C, npix = 32, 1024
+    x = torch.randn(npix, C, device="cuda").to(torch.bfloat16)
+    q = torch.empty(npix, C, device="cuda", dtype=torch.uint8)
+    st = torch.zeros(4, device="cuda", dtype=torch.int32)
+    assert L.unet_f8_quantize(x.data_ptr(), C, C, npix, q.data_ptr(), st.data_ptr(), 1, S()) == 0
+    torch.cuda.synchronize()
+    before = st.clone()
+    assert before[1].item() != 0  # the calibrating call committed this step's amax
+    q2, x4 = torch.empty_like(q), 4 * x
+    assert L.unet_f8_quantize(x4.data_ptr(), C, C, npix, q2.data_ptr(), st.data_ptr(), 2, S()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(st.cpu(), before.cpu())
