@@ -50,6 +50,8 @@ SIGNATURES = {
     "unet_bucket_wait": (c_int, [c_void_p, c_int, c_void_p]),
     "unet_plan_use_bucket_events": (c_int, [c_void_p, c_int]),
     "unet_profile_enable": (c_int, [c_void_p, c_int]),
+    "unet_timing_enable": (c_int, [c_void_p, c_int]),
+    "unet_timing_read": (c_int64, [c_void_p, c_void_p, c_int64, ctypes.c_char_p, c_int64]),
     "unet_profile_report": (c_int, [c_void_p, ctypes.c_char_p, c_int64]),
     "unet_loss_forward": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_float, c_float, c_void_p, c_void_p,
                                   c_void_p]),

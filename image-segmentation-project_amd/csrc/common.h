@@ -11,6 +11,28 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// In-kernel phase timing (debug build, -DUNET_TIMING: `make timing` builds
+// libunet_hip_timing.so): thread 0 of block b < kTimBlocks writes the shader
+// clock (s_memtime) of phase k to T[b * kTimSlots + k] of its launch's slot of a
+// debug buffer that nothing else reads.  Compiled out of the product library.
+using unet::kTimBlocks;
+using unet::kTimSlots;
+#ifdef UNET_TIMING
+#define TSTAMP(T, k)                                                                      \
+  do {                                                                                    \
+    if ((T) && threadIdx.x == 0 && blockIdx.x < (unsigned)kTimBlocks)                     \
+      (T)[blockIdx.x * kTimSlots + (k)] = __builtin_amdgcn_s_memtime();                   \
+  } while (0)
+#define TSTAMP_RT(T, k)                                                                   \
+  do {                                                                                    \
+    if ((T) && threadIdx.x == 0 && blockIdx.x < (unsigned)kTimBlocks)                     \
+      (T)[blockIdx.x * kTimSlots + (k)] = __builtin_amdgcn_s_memrealtime();               \
+  } while (0)
+#else
+#define TSTAMP(T, k) ((void)0)
+#define TSTAMP_RT(T, k) ((void)0)
+#endif
+
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 
 __device__ __forceinline__ float bf2f(bf16_t v) {

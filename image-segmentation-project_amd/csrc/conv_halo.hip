@@ -390,6 +390,8 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
   float* cst = reinterpret_cast<float*>(hl + 2 * HBUF);  // [kEpiConsts][COT]
   float* xss = cst + kEpiConsts * COT;                   // xform: [2][NP*32] scale | shift
 
+  TSTAMP_RT(a.tim, 30);
+  TSTAMP(a.tim, 0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int cg = blockIdx.x % ncg;
@@ -463,6 +465,7 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
   }
   wait_vmcnt<0>();
   __syncthreads();
+  TSTAMP(a.tim, 1);
 
   for (int k = 0; t < ntiles; ++k, t += nslot) {
     const int b = k & 1;
@@ -513,6 +516,7 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
 #pragma unroll
     for (int p = 0; p < NP; ++p)
       mfma_panel<FN, RW, NP * COT * 64, FLIP>(acc, wl + p * COT * 64, H + p * PANEL, aoff, boff);
+    if (k < 9) TSTAMP(a.tim, 2 + 2 * k);
     if (!PREF) epi.fetch(a, pix, co0, lane);
     epi.landed();
     wait_vmcnt<0>();               // the next tile's halo (issued before this tile's MFMAs) has landed ...
@@ -520,8 +524,12 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
     // the stores go out AFTER the wait: they drain under the next tile's MFMAs
     // instead of being waited for here (vmcnt counts stores too)
     epi.store(a, acc, pix, co0, lane, cst, q0, q1, q2);
+    if (k < 9) TSTAMP(a.tim, 3 + 2 * k);
   }
+  TSTAMP(a.tim, 20);
   if (a.stats || a.bb.sums) commit_stats<FN, NW, false>(a, q0, q1, q2, co0, smem);
+  TSTAMP(a.tim, 21);
+  TSTAMP_RT(a.tim, 31);
 }
 
 // ---------------------------------------------------------------------------
@@ -541,6 +549,8 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_hs_kernel(ConvFwdArgs a, int 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* cst = reinterpret_cast<float*>(smem + 2 * STAGE);  // [kEpiConsts][COT]
 
+  TSTAMP_RT(a.tim, 30);
+  TSTAMP(a.tim, 0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -608,14 +618,17 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_hs_kernel(ConvFwdArgs a, int 
 #pragma unroll
     for (int i = 0; i < FN; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   TileEpi<FN, RW, FLIP, PREF, TWO> epi;
+  TSTAMP(a.tim, 1);
   for (int kc = 0; kc < KC; ++kc) {
     wait_vmcnt<0>();               // stage kc landed (this wave's part) ...
     __builtin_amdgcn_s_barrier();  // ... everyone's; and stage kc-1 is no longer read
+    if (kc < 16) TSTAMP(a.tim, 2 + kc);
     if (kc + 1 < KC) issue(kc + 1, (kc + 1) & 1);
     else if (PREF) epi.fetch(a, pix, co0, lane);  // epilogue operands ride beside the last chunk
     const char* S = smem + (kc & 1) * STAGE;
     mfma_panel<FN, RW, COT * 64, FLIP>(acc, S + HBYTES, S, aoff, boff);
   }
+  TSTAMP(a.tim, 20);
   if (!PREF) epi.fetch(a, pix, co0, lane);
   epi.landed();
   float q0[FN][4], q1[FN][4], q2[FN][4];
@@ -624,7 +637,10 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_hs_kernel(ConvFwdArgs a, int 
 #pragma unroll
     for (int e = 0; e < 4; ++e) q0[i][e] = q1[i][e] = q2[i][e] = 0.f;
   epi.store(a, acc, pix, co0, lane, cst, q0, q1, q2);
+  TSTAMP(a.tim, 21);
   if (a.stats || a.bb.sums) commit_stats<FN, NW, TWO>(a, q0, q1, q2, co0, smem);
+  TSTAMP(a.tim, 22);
+  TSTAMP_RT(a.tim, 31);
 }
 
 // ---------------------------------------------------------------------------

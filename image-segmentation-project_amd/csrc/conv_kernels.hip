@@ -1076,6 +1076,8 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
   constexpr int LPS = A_INS * (DSF ? 2 : 1) + H_INS;  // glds per wave per stage
   extern __shared__ __attribute__((aligned(16))) char smem[];
   typedef TrTile<64, 64, 128> TA;
+  TSTAMP_RT(a.tim, 30);
+  TSTAMP(a.tim, 0);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1168,12 +1170,14 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
   for (int s = 0; s < NS - 1; ++s)
     if (s < KT) issue(s, s);
   const int g = lane >> 4, li = lane & 15, trq = li >> 2, trp = li & 3;
+  TSTAMP(a.tim, 1);
   for (int kt = 0; kt < KT; ++kt) {
     const int ahead = KT - 1 - kt;
     if (ahead >= NS - 2) wait_vmcnt<(NS - 2) * LPS>();
     else if (NS > 3 && ahead == 1) wait_vmcnt<LPS>();
     else wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
+    if (kt < 16) TSTAMP(a.tim, 2 + kt);
     if (kt + NS - 1 < KT) issue(kt + NS - 1, (kt + NS - 1) % NS);
     const char* As = smem + (kt % NS) * STAGE;
     const char* Bs = As + A_BYTES;
@@ -1213,6 +1217,7 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
     }
   }
   wait_vmcnt<0>();
+  TSTAMP(a.tim, 20);
   if constexpr (CO32) {  // fold the wm = 1 partials into wm = 0 through LDS
     __syncthreads();     // every stage consumed: the staging LDS is free
     f32x4* red = reinterpret_cast<f32x4*>(smem) + (size_t)(wn * 18) * 64 + lane;
@@ -1247,6 +1252,8 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) dst[(18 + i) * 64] = acc2[i];
     }
+    TSTAMP(a.tim, 21);
+    TSTAMP_RT(a.tim, 31);
     return;
   }
   const int Krow = 9 * a.C;

@@ -175,6 +175,12 @@ struct unet_plan {
   std::vector<hipEvent_t> syncpool;
   int syncused = 0;
   bool want_events = false;  // DDP overlap: record one hipEvent per gradient bucket
+  // in-kernel phase timing (debug build only, unet_timing_enable): one slot of
+  // kTimBlocks x kTimSlots stamps per conv launch, in launch order
+  unsigned long long* tim_buf = nullptr;
+  int tim_n = 0;
+  bool tim_on = false;
+  std::vector<std::string> tim_names;
   // BN-backward reductions fused into the producing conv dgrad (UNET_NO_BWD_FUSE=1: off, A/B only)
   bool fuse_bwd = std::getenv("UNET_NO_BWD_FUSE") == nullptr;
   // BN coefficients recomputed by every consumer block from the replica sums
@@ -223,6 +229,13 @@ int prof_event(unet_plan* p, hipStream_t st) {
   return i;
 }
 // RAII: brackets one launch with two events when profiling is on
+// the next conv launch's phase-stamp slot (null unless timing is on)
+unsigned long long* tim_slot(unet_plan* p, const std::string& name) {
+  if (!p->tim_on || !p->tim_buf || p->tim_n >= kTimLaunches) return nullptr;
+  p->tim_names.push_back(name);
+  return p->tim_buf + (size_t)(p->tim_n++) * kTimBlocks * kTimSlots;
+}
+
 struct ProfScope {
   unet_plan* p; hipStream_t st; std::string name; double flops; int e0 = -1;
   ProfScope(unet_plan* p_, hipStream_t s, std::string n, double f) : p(p_), st(s), name(std::move(n)), flops(f) {
@@ -880,6 +893,7 @@ int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for
     CK(launch_conv_fwd_f8(a, x.st));
     return 0;
   }
+  a.tim = tim_slot(x.p, "fwd " + pname(x, cv.w));
   CK(launch_conv_fwd(a, cv.kind == L_CONVT ? MODE_SHUF : MODE_FWD, x.st));
   return 0;
 }
@@ -929,6 +943,7 @@ int conv_dgrad(const Ctx& x, int ci, const Act& dy, const Act& dx, const Act* ad
   a.R = cv.R; a.S = cv.S; a.stride = cv.stride; a.pad = cv.pad;
   a.C = cv.Co; a.Cout = cv.Ci;
   // convT: an ordinary k2s2 conv of dY; conv: the transposed gather
+  a.tim = tim_slot(x.p, "dgrad " + pname(x, cv.w));
   CK(launch_conv_fwd(a, cv.kind == L_CONVT ? MODE_FWD : MODE_TRANS, x.st));
   return 0;
 }
@@ -946,6 +961,7 @@ int wgrad_and_reduce(const Ctx& x, ConvWgradArgs& a, int mode, const std::string
   }
   a.slab = x.W<float>(p->wslab + (size_t)si * p->wslab_bytes);
   a.slab_bytes = p->wslab_bytes;
+  a.tim = tim_slot(p, "wgrad " + name);
   {
     ProfScope ps(p, x.wst, "wgrad " + name, flops);
     if (mode == 2) CK(launch_convt_wgrad(a, x.wst));
@@ -1640,6 +1656,7 @@ int unet_plan_create(const unet_config* cfg, unet_plan** out) {
 
 void unet_plan_destroy(unet_plan* p) {
   if (!p) return;
+  if (p->tim_buf) (void)hipFree(p->tim_buf);
   for (int i = 0; i < p->nevents; ++i) (void)hipEventDestroy(p->events[i]);
   for (hipEvent_t e : p->syncpool) (void)hipEventDestroy(e);
   if (p->wstream) (void)hipStreamDestroy(p->wstream);
@@ -1714,6 +1731,30 @@ int unet_plan_use_bucket_events(unet_plan* p, int on) {
   if (!p) { set_err("null plan"); return 1; }
   p->want_events = on != 0;
   return 0;
+}
+
+int unet_timing_enable(unet_plan* p, int on) {
+  if (!p) { set_err("null plan"); return 1; }
+  const size_t bytes = (size_t)kTimLaunches * kTimBlocks * kTimSlots * sizeof(unsigned long long);
+  if (on && !p->tim_buf) CK(hipMalloc(&p->tim_buf, bytes));
+  if (on) CK(hipMemset(p->tim_buf, 0, bytes));
+  p->tim_on = on != 0;
+  p->tim_n = 0;
+  p->tim_names.clear();
+  return 0;
+}
+
+int64_t unet_timing_read(unet_plan* p, unsigned long long* host, int64_t max_launches, char* names, int64_t nlen) {
+  if (!p || !p->tim_buf) { set_err("timing not enabled"); return -1; }
+  CK(hipDeviceSynchronize());
+  const int64_t n = p->tim_n < max_launches ? p->tim_n : max_launches;
+  if (host && n > 0)
+    CK(hipMemcpy(host, p->tim_buf, (size_t)n * kTimBlocks * kTimSlots * sizeof(unsigned long long),
+                 hipMemcpyDeviceToHost));
+  std::string all;
+  for (int64_t i = 0; i < n; ++i) all += p->tim_names[(size_t)i] + "\n";
+  if (names && nlen > 0) std::snprintf(names, (size_t)nlen, "%s", all.c_str());
+  return n;
 }
 
 int unet_profile_enable(unet_plan* p, int on) {

@@ -7,6 +7,9 @@ namespace unet {
 
 typedef unsigned short bf16_t;
 
+// in-kernel phase timing buffer geometry (common.h TSTAMP, debug build only)
+constexpr int kTimBlocks = 1024, kTimSlots = 32, kTimLaunches = 320;
+
 // MODE_SHUF: ConvTranspose2d(k2, s2) forward as ONE 1x1 GEMM over the input
 // pixels with 4*Cout columns (j = (a*2+b)*Cout + co) and a pixel-shuffle store
 // y[2i+a, 2j+b, co]; every input pixel is staged once instead of once per
@@ -100,6 +103,9 @@ struct ConvFwdArgs {
   int P, Q, Cout;                // output geometry
   int R, S, stride, pad;
   int mblocks, nblocks, Pc, Qc;  // filled by the launcher
+  // in-kernel phase stamps (debug build -DUNET_TIMING only, null otherwise):
+  // [block < kTimBlocks][kTimSlots] s_memtime values (scripts/conv_timing.py)
+  unsigned long long* tim;
 };
 
 // Split-K partials of the weight-gradient kernels ("register-native" slab):
@@ -140,6 +146,7 @@ struct ConvWgradArgs {
   // gradient folded in (its input pixels are the centre tap's): dW2[co][c] =
   // sum dY2[px][co] x[2p][2q][c], dY2 with the same Cout (wgrad_s2_fold_ok)
   const bf16_t* dy2; int lddy2; float* dw2;
+  unsigned long long* tim;  // phase stamps (debug build only), as ConvFwdArgs::tim
 };
 // the stride-2 halo weight gradient covers this shape (and then folds a.dy2)
 bool wgrad_s2_fold_ok(const ConvWgradArgs& a);

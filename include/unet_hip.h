@@ -86,6 +86,14 @@ int unet_plan_use_bucket_events(unet_plan* p, int on);
 int unet_bucket_wait(unet_plan* p, int bucket, hipStream_t waiter);
 /* per-launch hipEvent profiler: enable (clears records), then report lines
  * "name\tms\tflops\n" for every launch since; returns bytes needed (incl. NUL). */
+/* In-kernel phase timing of the conv launches (a debug aid; the stamps are
+ * written only by a library built with -DUNET_TIMING, `make timing`): enable
+ * zeroes a device buffer of kTimLaunches x 1024 blocks x 32 u64 stamps and gives
+ * every following conv launch of the plan the next slot; read copies the slots
+ * used so far to `host` (max_launches slots) and the launch names (one per
+ * line) to `names`, and returns the number of slots used. */
+int unet_timing_enable(unet_plan* p, int on);
+int64_t unet_timing_read(unet_plan* p, unsigned long long* host, int64_t max_launches, char* names, int64_t nlen);
 int unet_profile_enable(unet_plan* p, int on);
 int unet_profile_report(unet_plan* p, char* buf, int64_t buflen);
 

@@ -210,6 +210,11 @@ def _shared_gpu_worker(rank, world, port, q):
             want = [a / world for a in acc]
             errs.append(max(_rel(a, b) for a, b in zip(got, want) if b.norm() > 0))
             exact.append(all(torch.equal(a, b) for a, b in zip(got, want)))
+            names_ = [k for k, _ in m.named_parameters()]
+            bad = [(names_[i], round(_rel(a, b), 4)) for i, (a, b) in enumerate(zip(got, want))
+                   if b.norm() > 0 and _rel(a, b) > 1e-6]
+            if bad:
+                print(f"rank {rank} step {step}: {len(bad)} tensors differ: {bad[:10]}", flush=True)
         # oracle: the reduced head gradients (the layers the loss gradient reaches
         # before any BN) against the fp32 oracle's mean over the two chunks
         ref.load_state_dict({k: v.cpu() for k, v in sd.items()})
