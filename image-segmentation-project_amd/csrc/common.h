@@ -83,6 +83,33 @@ __device__ __forceinline__ void glds16s(__amdgpu_buffer_rsrc_t r, char* lds_wave
                                            0, 0);
 }
 
+// The same LDS-DMA as an inline-asm statement (cdna_hip_programming.md "What
+// hipcc does not do" / LDS-DMA recipe: M0 written and restored in the same
+// statement).  hipcc's waitcnt pass then never sees an LDS write on the VM
+// counter, so it cannot insert the s_waitcnt vmcnt(0) it otherwise puts in
+// front of the first ds_read_b64_tr_b16 of every k-step (draining the whole
+// multi-stage pipeline); the kernel counts its DMA completions itself.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4 make_rsrc_sgpr(const void* base, unsigned bytes) {
+  const unsigned long long p = (unsigned long long)base;  // make_rsrc's V#: base, stride 0, num_records, flags
+  i32x4 r;
+  r.x = __builtin_amdgcn_readfirstlane((int)(unsigned)p);
+  r.y = __builtin_amdgcn_readfirstlane((int)((unsigned)(p >> 32) & 0xffffu));
+  r.z = __builtin_amdgcn_readfirstlane((int)bytes);
+  r.w = 0x00020000;
+  return r;
+}
+__device__ __forceinline__ void glds16_asm(const i32x4& r, char* lds_wave_base, unsigned voff, unsigned soff) {
+  const unsigned lds = __builtin_amdgcn_readfirstlane((unsigned)(size_t)LDS_PTR(char, lds_wave_base));
+  const unsigned so = __builtin_amdgcn_readfirstlane(soff);
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(r), "s"(lds), "s"(so)
+      : "memory");
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

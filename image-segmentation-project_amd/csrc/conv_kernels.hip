@@ -1097,10 +1097,11 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
   const int nsplit = gridDim.x / combos;
   if (KT <= 0 && !(a.slab && nsplit > 1)) return;
   const int tq = a.Q / TW, tp = a.P / TH;
-  const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, (unsigned)((size_t)a.N * a.P * a.Q * a.lddy * 2));
-  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
-  const __amdgpu_buffer_rsrc_t dy2r =
-      make_rsrc(DSF ? a.dy2 : a.dy, DSF ? (unsigned)((size_t)a.N * a.P * a.Q * a.lddy2 * 2) : 0u);
+  // asm LDS-DMA (glds16_asm): hipcc would otherwise drain every stage in flight
+  // before the first transposed read of each stage
+  const i32x4 dyr = make_rsrc_sgpr(a.dy, (unsigned)((size_t)a.N * a.P * a.Q * a.lddy * 2));
+  const i32x4 xr = make_rsrc_sgpr(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
+  const i32x4 dy2r = make_rsrc_sgpr(DSF ? a.dy2 : a.dy, DSF ? (unsigned)((size_t)a.N * a.P * a.Q * a.lddy2 * 2) : 0u);
 
   // per-lane constant parts of the loads
   const int arow = lane >> 3, aslot = lane & 7;                // dY: 8 rows of 128 B per instruction
@@ -1143,12 +1144,12 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
     char* Bs = As + A_BYTES;
     const unsigned abase = (unsigned)(((n * a.P + oh0) * a.Q + ow0) * a.lddy) * 2u;
 #pragma unroll
-    for (int j = 0; j < A_INS; ++j) glds16s(dyr, As + (wave * A_INS + j) * 1024, arel[j], abase);
+    for (int j = 0; j < A_INS; ++j) glds16_asm(dyr, As + (wave * A_INS + j) * 1024, arel[j], abase);
     if constexpr (DSF) {
       const unsigned abase2 = (unsigned)(((n * a.P + oh0) * a.Q + ow0) * a.lddy2) * 2u;
 #pragma unroll
       for (int j = 0; j < A_INS; ++j)
-        glds16s(dy2r, As + A_BYTES + B_BYTES + (wave * A_INS + j) * 1024, arel2[j], abase2);
+        glds16_asm(dy2r, As + A_BYTES + B_BYTES + (wave * A_INS + j) * 1024, arel2[j], abase2);
     }
 #pragma unroll
     for (int j = 0; j < H_INS; ++j) {
@@ -1156,7 +1157,7 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
       unsigned off = kOOB;
       if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
         off = (unsigned)((((n * a.H + ih) * a.W + iw) * a.ldx) + hch[j]) * 2u;
-      glds16(xr, Bs + (wave * H_INS + j) * 1024, off);
+      glds16_asm(xr, Bs + (wave * H_INS + j) * 1024, off, 0u);
     }
   };
 

@@ -259,6 +259,98 @@ __global__ void __launch_bounds__(256) rot90_vflip_kernel(const uint8_t* __restr
   dst[i] = src[(int64_t)n * H * W + (int64_t)sy * W + sx];
 }
 
+
+// A.Affine (dataset.py:150-151) = cv2.warpAffine, OpenCV's fixed-point path
+// (imgwarp.cpp WarpAffineInvoker + remapBilinear / remapNearest, BORDER_CONSTANT
+// 0), restated in oracle/dataset_ref.py warp_affine_u8.  m: per frame the
+// dst -> src map [6] (cv::invertAffineTransform of the forward matrix, made on
+// the host); the source coordinate of output column x, row y is
+// X = cvRound((m1*y + m2)*1024) + rd + cvRound(m0*x*1024) (Y likewise), double
+// products rounded separately (no fma: this file is built -ffp-contract=off).
+// active[n] == 0: the frame is copied; vflip[n]: A.VerticalFlip, which follows
+// the affine step in the reference pipeline, folded into the output row.
+__device__ __forceinline__ long long cv_round_d(double v) {
+  double r = rint(v);
+  r = fmin(fmax(r, -2147483648.0), 2147483647.0);  // saturate_cast<int>
+  return (long long)r;
+}
+
+__global__ void __launch_bounds__(256) warp_affine_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                          int N, int H, int W, const double* __restrict__ m,
+                                                          const int* __restrict__ active,
+                                                          const int* __restrict__ vflip, int nearest) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)N * H * W) return;
+  const int n = (int)(i / ((int64_t)H * W));
+  const int64_t r = i - (int64_t)n * H * W;
+  const int y = (int)(r / W), x = (int)(r - (int64_t)(r / W) * W);
+  const int yy = vflip[n] ? H - 1 - y : y;  // the warp's output row stored at row y
+  const uint8_t* S = src + (int64_t)n * H * W;
+  if (!active[n]) {
+    dst[i] = S[(int64_t)yy * W + x];
+    return;
+  }
+  const double* M = m + (size_t)n * 6;
+  const double xd = (double)x, yd = (double)yy;
+  const long long adelta = cv_round_d(__dmul_rn(__dmul_rn(M[0], xd), 1024.0));
+  const long long bdelta = cv_round_d(__dmul_rn(__dmul_rn(M[3], xd), 1024.0));
+  const int rd = nearest ? 512 : 16;
+  const long long X0 = cv_round_d(__dmul_rn(__dadd_rn(__dmul_rn(M[1], yd), M[2]), 1024.0)) + rd;
+  const long long Y0 = cv_round_d(__dmul_rn(__dadd_rn(__dmul_rn(M[4], yd), M[5]), 1024.0)) + rd;
+  const long long X = X0 + adelta, Y = Y0 + bdelta;
+  if (nearest) {
+    const long long sx = X >> 10, sy = Y >> 10;
+    dst[i] = (sx >= 0 && sx < W && sy >= 0 && sy < H) ? S[sy * W + sx] : (uint8_t)0;
+    return;
+  }
+  const long long Xs = X >> 5, Ys = Y >> 5;
+  const long long sx = Xs >> 5, sy = Ys >> 5;
+  const int fx = (int)(Xs & 31), fy = (int)(Ys & 31);
+  if (sx >= W || sx + 1 < 0 || sy >= H || sy + 1 < 0) {
+    dst[i] = 0;
+    return;
+  }
+  auto tap = [&](long long yv, long long xv) -> int {
+    return (xv >= 0 && xv < W && yv >= 0 && yv < H) ? (int)S[yv * W + xv] : 0;
+  };
+  const int w0 = (32 - fy) * (32 - fx) * 32, w1 = (32 - fy) * fx * 32;
+  const int w2 = fy * (32 - fx) * 32, w3 = fy * fx * 32;
+  const int v = tap(sy, sx) * w0 + tap(sy, sx + 1) * w1 + tap(sy + 1, sx) * w2 + tap(sy + 1, sx + 1) * w3;
+  dst[i] = sat_u8((v + (1 << 14)) >> 15);
+}
+
+// A.AdvancedBlur (dataset.py:153) = cv2.filter2D(img, -1, kernel), anchor at
+// the centre, BORDER_REFLECT_101: fp32 s = s + k * v over the non-zero
+// coefficients in row-major order, cvRound, saturate (oracle filter2d_u8).
+// kern: [N][7][7] (top-left ksz[n] x ksz[n] used); ksz[n] == 0: copy.
+__global__ void __launch_bounds__(256) filter2d_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                       int N, int H, int W, const float* __restrict__ kern,
+                                                       const int* __restrict__ ksz) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)N * H * W) return;
+  const int n = (int)(i / ((int64_t)H * W));
+  const int64_t r = i - (int64_t)n * H * W;
+  const int y = (int)(r / W), x = (int)(r - (int64_t)(r / W) * W);
+  const uint8_t* S = src + (int64_t)n * H * W;
+  const int k = ksz[n];
+  if (k == 0) {
+    dst[i] = S[r];
+    return;
+  }
+  const float* K = kern + (size_t)n * 49;
+  const int rad = k >> 1;
+  float acc = 0.f;
+  for (int a = 0; a < k; ++a) {
+    const int sy = reflect101(y + a - rad, H);
+    for (int b = 0; b < k; ++b) {
+      const float f = K[a * 7 + b];
+      if (f == 0.f) continue;
+      acc = __fadd_rn(acc, __fmul_rn(f, (float)S[(int64_t)sy * W + reflect101(x + b - rad, W)]));
+    }
+  }
+  dst[i] = sat_u8(cv_round(acc));
+}
+
 static inline unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
 
 hipError_t launch_resize_area(const uint8_t* src, uint8_t* dst, int N, int H, int W, int oh, int ow, hipStream_t st) {
@@ -291,6 +383,22 @@ hipError_t launch_rot90_vflip(const uint8_t* src, uint8_t* dst, int N, int H, in
   if (N <= 0 || H <= 0 || W <= 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(rot90_vflip_kernel, dim3(blocks_for((int64_t)N * H * W)), dim3(256), 0, st, src, dst, N, H, W, k,
                      flip);
+  return hipGetLastError();
+}
+
+hipError_t launch_warp_affine(const uint8_t* src, uint8_t* dst, int N, int H, int W, const double* m, const int* active,
+                              const int* vflip, int nearest, hipStream_t st) {
+  if (N <= 0 || H <= 0 || W <= 0 || (int64_t)H * W >= (1ll << 31)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(warp_affine_kernel, dim3(blocks_for((int64_t)N * H * W)), dim3(256), 0, st, src, dst, N, H, W, m,
+                     active, vflip, nearest);
+  return hipGetLastError();
+}
+
+hipError_t launch_filter2d(const uint8_t* src, uint8_t* dst, int N, int H, int W, const float* kern, const int* ksz,
+                           hipStream_t st) {
+  if (N <= 0 || H < 4 || W < 4) return hipErrorInvalidValue;  // reflect-101 of a 7x7 footprint
+  hipLaunchKernelGGL(filter2d_kernel, dim3(blocks_for((int64_t)N * H * W)), dim3(256), 0, st, src, dst, N, H, W, kern,
+                     ksz);
   return hipGetLastError();
 }
 

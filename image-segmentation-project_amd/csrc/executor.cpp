@@ -1970,6 +1970,20 @@ int unet_rot90_vflip_u8(const uint8_t* src, int N, int H, int W, const int* k, c
   return 0;
 }
 
+int unet_warp_affine_u8(const uint8_t* src, int N, int H, int W, const double* minv, const int* active,
+                        const int* vflip, int nearest, uint8_t* dst, hipStream_t stream) {
+  if (!src || !dst || !minv || !active || !vflip) { set_err("unet_warp_affine_u8: null buffer"); return 1; }
+  CK(launch_warp_affine(src, dst, N, H, W, minv, active, vflip, nearest, stream));
+  return 0;
+}
+
+int unet_filter2d_u8(const uint8_t* src, int N, int H, int W, const float* kernels, const int* ksize, uint8_t* dst,
+                     hipStream_t stream) {
+  if (!src || !dst || !kernels || !ksize) { set_err("unet_filter2d_u8: null buffer"); return 1; }
+  CK(launch_filter2d(src, dst, N, H, W, kernels, ksize, stream));
+  return 0;
+}
+
 int unet_maxpool_fwd(const void* x, int ldx, void* y, uint8_t* idx, int N, int H, int W, int C,
                      hipStream_t stream) {
   MaxPoolArgs m = {};

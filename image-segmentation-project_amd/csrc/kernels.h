@@ -280,6 +280,12 @@ hipError_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, 
 hipError_t launch_resize_area(const uint8_t* src, uint8_t* dst, int N, int H, int W, int oh, int ow, hipStream_t st);
 hipError_t launch_mask_prep(const uint8_t* src, float* dst, int N, int H, int W, int oh, int ow, hipStream_t st);
 hipError_t launch_normalize(const uint8_t* src, float* dst, int N, int H, int W, int normalize, hipStream_t st);
+// A.Affine (+ the following A.VerticalFlip folded in) as cv2.warpAffine's
+// fixed-point path; A.AdvancedBlur as cv2.filter2D (data.hip)
+hipError_t launch_warp_affine(const uint8_t* src, uint8_t* dst, int N, int H, int W, const double* m, const int* active,
+                              const int* vflip, int nearest, hipStream_t st);
+hipError_t launch_filter2d(const uint8_t* src, uint8_t* dst, int N, int H, int W, const float* kern, const int* ksz,
+                           hipStream_t st);
 hipError_t launch_rot90_vflip(const uint8_t* src, uint8_t* dst, int N, int H, int W, const int* k, const int* flip,
                               hipStream_t st);
 

@@ -145,7 +145,7 @@ def _is_frames(x) -> bool:
     import numpy as np
     if isinstance(x, np.ndarray):
         return x.dtype == np.uint8
-    return isinstance(x, (list, tuple)) and len(x) > 0 and getattr(x[0], "dtype", None) == np.uint8
+    return isinstance(x, (list, tuple)) and len(x) > 0 and getattr(x[0], "dtype", None) in (np.uint8, torch.uint8)
 
 
 class TensorLoader:

@@ -204,6 +204,19 @@ int unet_normalize_microscopy(const uint8_t* src, int N, int H, int W, float* ds
 int unet_rot90_vflip_u8(const uint8_t* src, int N, int H, int W, const int* k, const int* vflip, uint8_t* dst,
                         hipStream_t stream);
 
+/* A.Affine (dataset.py:150-151; albumentations 2.0 -> cv2.warpAffine, fixed-point
+ * INTER_LINEAR for images / INTER_NEAREST for masks, BORDER_CONSTANT 0) with the
+ * pipeline's following A.VerticalFlip folded in.  minv: device double [N][6],
+ * the dst -> src map (cv::invertAffineTransform of the forward matrix);
+ * active[n] == 0 copies frame n (still flipped when vflip[n]). */
+int unet_warp_affine_u8(const uint8_t* src, int N, int H, int W, const double* minv, const int* active,
+                        const int* vflip, int nearest, uint8_t* dst, hipStream_t stream);
+/* A.AdvancedBlur (dataset.py:153) = cv2.filter2D(img, -1, kernel), BORDER_REFLECT_101.
+ * kernels: device float32 [N][7][7] (top-left ksize[n]^2 used, odd ksize <= 7);
+ * ksize[n] == 0 copies frame n. */
+int unet_filter2d_u8(const uint8_t* src, int N, int H, int W, const float* kernels, const int* ksize, uint8_t* dst,
+                     hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

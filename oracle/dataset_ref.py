@@ -216,3 +216,123 @@ def rot90_vflip(img: np.ndarray, k: int, vflip: bool) -> np.ndarray:
     if vflip:
         out = out[::-1]
     return np.ascontiguousarray(out)
+
+
+# ---------------------------------------------------------------------------
+# CellAugmenter's interpolating transforms (dataset.py:148-154), restated from
+# the published algorithms of albumentations 2.0 (A.Affine, A.AdvancedBlur;
+# requirements.txt:9 pins only albumentations>=1.1.0 — 2.0.x is what pip
+# resolved at the reference's snapshot) and OpenCV 4.x (cv2.warpAffine's
+# fixed-point INTER_LINEAR / INTER_NEAREST path, imgproc/src/imgwarp.cpp
+# WarpAffineInvoker + remapBilinear / remapNearest; cv2.filter2D's direct
+# Filter2D<uchar, Cast<float, uchar>> loop).  Neither library is installed
+# here: PARITY UNPINNED.  The GPU kernels (csrc/data.hip) are checked
+# bit-exactly against these functions given the same sampled parameters.
+# ---------------------------------------------------------------------------
+
+def affine_matrix(scale_x: float, scale_y: float, tx_frac: float, ty_frac: float, rotate_deg: float,
+                  shear_x_deg: float, shear_y_deg: float, h: int, w: int) -> np.ndarray:
+    """albumentations 2.0 ``create_affine_transformation_matrix``: the FORWARD
+    3x3 matrix (src -> dst) C . T . Sh . R . S . C^-1 about the image centre
+    ((w-1)/2, (h-1)/2); translate is a fraction of the width / height."""
+    cx, cy = (w - 1) / 2.0, (h - 1) / 2.0
+    t_topleft = np.array([[1, 0, -cx], [0, 1, -cy], [0, 0, 1]], np.float64)
+    s = np.array([[scale_x, 0, 0], [0, scale_y, 0], [0, 0, 1]], np.float64)
+    a = np.deg2rad(rotate_deg)
+    r = np.array([[np.cos(a), -np.sin(a), 0], [np.sin(a), np.cos(a), 0], [0, 0, 1]], np.float64)
+    sh = np.array([[1, np.tan(np.deg2rad(shear_x_deg)), 0], [np.tan(np.deg2rad(shear_y_deg)), 1, 0], [0, 0, 1]],
+                  np.float64)
+    t = np.array([[1, 0, tx_frac * w], [0, 1, ty_frac * h], [0, 0, 1]], np.float64)
+    t_center = np.array([[1, 0, cx], [0, 1, cy], [0, 0, 1]], np.float64)
+    return t_center @ t @ sh @ r @ s @ t_topleft
+
+
+def invert_affine(m) -> np.ndarray:
+    """cv::invertAffineTransform on the top 2x3 rows (double), as warpAffine
+    does without WARP_INVERSE_MAP: returns [M0..M5] of the dst -> src map."""
+    m = np.asarray(m, np.float64).reshape(-1)[:6] if np.asarray(m).shape != (3, 3) else \
+        np.asarray(m, np.float64)[:2].reshape(-1)
+    d = m[0] * m[4] - m[1] * m[3]
+    d = 1.0 / d if d != 0.0 else 0.0
+    a11, a22 = m[4] * d, m[0] * d
+    a12, a21 = -m[1] * d, -m[3] * d
+    b1 = -a11 * m[2] - a12 * m[5]
+    b2 = -a21 * m[2] - a22 * m[5]
+    return np.array([a11, a12, b1, a21, a22, b2], np.float64)
+
+
+def warp_affine_u8(img: np.ndarray, minv, nearest: bool = False) -> np.ndarray:
+    """cv2.warpAffine(img, M, (w, h), flags, BORDER_CONSTANT, 0) for uint8 given
+    minv = invert_affine(M): AB_BITS = 10 fixed-point source coordinates
+    (cvRound of the double products), INTER_BITS = 5 sub-pixel index;
+    bilinear weights (32 - f) * 32 products (initInterTab2D, exact), result
+    (sum + 2^14) >> 15; taps outside the image read the border value 0, a
+    pixel whose 2x2 footprint misses the image entirely is 0.  Nearest:
+    (X + 512) >> 10 with the out-of-image test on the source pixel."""
+    h, w = img.shape
+    m = np.asarray(minv, np.float64)
+    xs = np.arange(w, dtype=np.float64)
+    ys = np.arange(h, dtype=np.float64)
+    adelta = np.rint(m[0] * xs * 1024.0).astype(np.int64)
+    bdelta = np.rint(m[3] * xs * 1024.0).astype(np.int64)
+    rd = 512 if nearest else 16
+    x0 = np.rint((m[1] * ys + m[2]) * 1024.0).astype(np.int64) + rd
+    y0 = np.rint((m[4] * ys + m[5]) * 1024.0).astype(np.int64) + rd
+    X = x0[:, None] + adelta[None, :]
+    Y = y0[:, None] + bdelta[None, :]
+    src = img.astype(np.int64)
+    if nearest:
+        sx, sy = X >> 10, Y >> 10
+        inside = (sx >= 0) & (sx < w) & (sy >= 0) & (sy < h)
+        out = np.where(inside, src[np.clip(sy, 0, h - 1), np.clip(sx, 0, w - 1)], 0)
+        return out.astype(np.uint8)
+    X, Y = X >> 5, Y >> 5
+    sx, sy = X >> 5, Y >> 5
+    fx, fy = X & 31, Y & 31
+    w0, w1 = (32 - fy) * (32 - fx) * 32, (32 - fy) * fx * 32
+    w2, w3 = fy * (32 - fx) * 32, fy * fx * 32
+
+    def tap(yy, xx):
+        ok = (xx >= 0) & (xx < w) & (yy >= 0) & (yy < h)
+        return np.where(ok, src[np.clip(yy, 0, h - 1), np.clip(xx, 0, w - 1)], 0)
+
+    v = tap(sy, sx) * w0 + tap(sy, sx + 1) * w1 + tap(sy + 1, sx) * w2 + tap(sy + 1, sx + 1) * w3
+    out = (v + (1 << 14)) >> 15
+    miss = (sx >= w) | (sx + 1 < 0) | (sy >= h) | (sy + 1 < 0)
+    return np.where(miss, 0, np.clip(out, 0, 255)).astype(np.uint8)
+
+
+def advanced_blur_kernel(ksize: int, sigma_x: float, sigma_y: float, angle_deg: float, beta: float,
+                         noise: np.ndarray) -> np.ndarray:
+    """albumentations AdvancedBlur kernel: generalized Gaussian
+    exp(-0.5 * (g^T Sigma^-1 g)^beta) on the centred ksize x ksize grid, Sigma
+    = U diag(sx^2, sy^2) U^T rotated by the angle, times the multiplicative
+    noise matrix, normalised to sum 1; float32 (what cv2.filter2D uses)."""
+    ax = np.arange(-ksize // 2 + 1.0, ksize // 2 + 1.0)
+    grid = np.stack(np.meshgrid(ax, ax), axis=-1)
+    d = np.array([[sigma_x ** 2, 0], [0, sigma_y ** 2]])
+    a = np.deg2rad(angle_deg)
+    u = np.array([[np.cos(a), -np.sin(a)], [np.sin(a), np.cos(a)]])
+    inv = np.linalg.inv(u @ d @ u.T)
+    k = np.exp(-0.5 * np.power(np.sum(np.dot(grid, inv) * grid, 2), beta))
+    k = k * noise
+    return (k.astype(np.float32) / np.sum(k)).astype(np.float32)
+
+
+def filter2d_u8(img: np.ndarray, kernel: np.ndarray) -> np.ndarray:
+    """cv2.filter2D(img, -1, kernel) for uint8 and an odd float32 kernel,
+    anchor at the centre, BORDER_REFLECT_101: per pixel an fp32 sum over the
+    NON-ZERO coefficients in row-major order, s = s + k * v (separate fp32
+    multiply and add: the scalar Filter2D loop), then cvRound and saturate."""
+    h, w = img.shape
+    kh, kw = kernel.shape
+    ry, rx = kh // 2, kw // 2
+    ext = np.pad(img, ((ry, ry), (rx, rx)), mode="reflect").astype(np.float32)
+    s = np.zeros((h, w), np.float32)
+    for i in range(kh):
+        for j in range(kw):
+            f = np.float32(kernel[i, j])
+            if f == 0:
+                continue
+            s = (s + (f * ext[i:i + h, j:j + w]).astype(np.float32)).astype(np.float32)
+    return np.clip(np.rint(s), 0, 255).astype(np.uint8)

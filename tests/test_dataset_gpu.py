@@ -1,6 +1,7 @@
 """The on-GPU data pipeline (csrc/data.hip) against the
 numpy oracle (oracle/dataset_ref.py) — the reference's dataset.py:30-66 and
-CellAugmenter's rot90 / vflip (dataset.py:147,150).
+CellAugmenter's whole pipeline (dataset.py:148-154: RandomRotate90, Affine,
+VerticalFlip, AdvancedBlur).
 
 Bar: bit-exact.  Resized / CLAHE'd frames are uint8, masks {0, 1}, and the
 normalised float32 image is computed from identical uint8 values by the same
@@ -17,6 +18,10 @@ import torch
 from oracle import dataset_ref as D
 
 pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    return importlib.import_module("image-segmentation-project_amd._lib").load()
 
 
 def _frames(seed, n, h, w, kind="cells"):
@@ -92,20 +97,95 @@ def test_preprocess_end_to_end_matches_dataset_getitem(pkg, cuda):
     assert torch.equal(torch.cat([t[0] for t in batches]), x)
 
 
-def test_augmenter_rot90_vflip_exact(pkg, cuda):
-    f = _frames(5, 3, 64, 64, kind="noise")
+def _oracle_copy(f, m, prm, i):
+    """One augmented copy through the numpy restatement of the reference
+    pipeline (dataset.py:148-154) with the augmenter's own parameters."""
+    x = D.rot90_vflip(f, int(prm["k"][i]), False)
+    y = D.rot90_vflip((m > 0).astype(np.uint8) * 255, int(prm["k"][i]), False)
+    if prm["affine"][i]:
+        x = D.warp_affine_u8(x, prm["minv"][i])
+        y = D.warp_affine_u8(y, prm["minv"][i], nearest=True)
+    if prm["vflip"][i]:
+        x, y = np.ascontiguousarray(x[::-1]), np.ascontiguousarray(y[::-1])
+    if prm["blur"][i]:
+        kz = int(prm["ksize"][i])
+        x = D.filter2d_u8(x, prm["kernels"][i][:kz, :kz])
+    return x, y
+
+
+@pytest.mark.parametrize("hw", [(64, 64), (48, 80)], ids=["square", "non-square"])
+def test_augmenter_pipeline_exact(pkg, cuda, hw):
+    """CellAugmenter = the reference's whole pipeline (RandomRotate90 p=0.5,
+    Affine p=0.3, VerticalFlip p=0.5, AdvancedBlur p=0.3): every augmented
+    copy equals the numpy restatement (oracle/dataset_ref.py; albumentations /
+    cv2 absent: parity unpinned) given the same parameters, bit for bit; a
+    non-square frame rotated by 90/270 degrees comes back transposed."""
+    f = _frames(5, 4, *hw, kind="noise")
     m = (f > 128).astype(np.uint8)
-    aug = pkg.CellAugmenter(augmentations_per_image=4, seed=7)
-    with pytest.warns(RuntimeWarning):
-        xs, ms = aug.augment_training_data(f, m)
-    assert xs.shape == (3 + 12, 64, 64) and ms.shape == xs.shape
-    assert torch.equal(xs[:3].cpu(), torch.from_numpy(f))
-    k, fl = aug.last_params["k"], aug.last_params["vflip"]
-    for j in range(12):
-        src = j // 4
-        assert np.array_equal(xs[3 + j].cpu().numpy(), D.rot90_vflip(f[src], int(k[j]), bool(fl[j])))
-        assert np.array_equal(ms[3 + j].cpu().numpy(), D.rot90_vflip((m[src] > 0).astype(np.uint8) * 255,
-                                                                    int(k[j]), bool(fl[j])))
+    aug = pkg.CellAugmenter(augmentations_per_image=8, seed=7)
+    xs, ms = aug.augment_training_data(f, m)
+    prm = aug.last_params
+    assert len(xs) == 4 + 32 and len(ms) == len(xs)
+    for j in range(4):
+        assert np.array_equal(xs[j].cpu().numpy(), f[j])
+    for k in ("affine", "blur", "vflip"):
+        assert 0 < prm[k].sum() < 32, k  # each transform both taken and skipped at this seed
+    for i in range(32):
+        want_x, want_m = _oracle_copy(f[i // 8], m[i // 8], prm, i)
+        got_x, got_m = xs[4 + i].cpu().numpy(), ms[4 + i].cpu().numpy()
+        assert got_x.shape == want_x.shape, (i, got_x.shape, want_x.shape)
+        assert np.array_equal(got_x, want_x), (i, int((got_x != want_x).sum()))
+        assert np.array_equal(got_m, want_m), (i, int((got_m != want_m).sum()))
+    if hw[0] != hw[1]:
+        assert isinstance(xs, list) and any(t.shape == hw[::-1] for t in xs)
+        x, y = pkg.preprocess(xs, ms, img_size=(32, 32))  # frames of two sizes, each resized
+        assert x.shape == (36, 1, 32, 32) and y.shape == x.shape
+
+
+def test_warp_affine_and_filter2d_exact(pkg, cuda):
+    """The two kernels alone on hard cases: large rotations / scales pushing
+    the footprint off the image (constant-0 border, partially covered
+    pixels), nearest for masks, inactive frames copied (flipped or not), and
+    blur kernels of every size with zero taps skipped."""
+    L = _lib()
+    rng = np.random.default_rng(3)
+    n, h, w = 6, 37, 53
+    f = rng.integers(0, 256, (n, h, w), dtype=np.uint8)
+    mats = [D.affine_matrix(1.3, 0.7, 0.2, -0.3, 170.0, 20.0, -10.0, h, w),
+            D.affine_matrix(0.95, 1.05, 0.05, 0.05, 15.0, 5.0, 5.0, h, w),
+            D.affine_matrix(2.5, 2.5, 0.0, 0.0, 33.0, 0.0, 0.0, h, w),
+            np.eye(3), D.affine_matrix(0.5, 0.5, -0.4, 0.4, -90.0, 0.0, 0.0, h, w), np.eye(3)]
+    minv = np.stack([D.invert_affine(mm) for mm in mats])
+    act = np.array([1, 1, 1, 1, 1, 0], np.int32)
+    fl = np.array([0, 1, 0, 1, 0, 1], np.int32)
+    S = torch.cuda.current_stream().cuda_stream
+    x = torch.from_numpy(f).cuda()
+    for nearest in (0, 1):
+        out = torch.empty_like(x)
+        assert L.unet_warp_affine_u8(x.data_ptr(), n, h, w, torch.from_numpy(minv).cuda().data_ptr(),
+                                     torch.from_numpy(act).cuda().data_ptr(), torch.from_numpy(fl).cuda().data_ptr(),
+                                     nearest, out.data_ptr(), S) == 0
+        got = out.cpu().numpy()
+        for i in range(n):
+            want = D.warp_affine_u8(f[i], minv[i], bool(nearest)) if act[i] else f[i]
+            want = want[::-1] if fl[i] else want
+            assert np.array_equal(got[i], want), (nearest, i, int((got[i] != want).sum()))
+    kern = np.zeros((n, 7, 7), np.float32)
+    ksz = np.array([3, 5, 7, 0, 7, 3], np.int32)
+    for i in range(n):
+        if ksz[i]:
+            kk = D.advanced_blur_kernel(int(ksz[i]), 0.2 + 0.15 * i, 1.0 - 0.1 * i, 20.0 * i - 60.0,
+                                        0.5 + 1.3 * i, rng.uniform(0.9, 1.1, (ksz[i], ksz[i])))
+            if i == 4:
+                kk[0, :] = 0.0  # zero taps are skipped, as cv2's Filter2D drops them
+            kern[i, :ksz[i], :ksz[i]] = kk
+    out = torch.empty_like(x)
+    assert L.unet_filter2d_u8(x.data_ptr(), n, h, w, torch.from_numpy(kern).cuda().data_ptr(),
+                              torch.from_numpy(ksz).cuda().data_ptr(), out.data_ptr(), S) == 0
+    got = out.cpu().numpy()
+    for i in range(n):
+        want = D.filter2d_u8(f[i], kern[i][:ksz[i], :ksz[i]]) if ksz[i] else f[i]
+        assert np.array_equal(got[i], want), (i, int((got[i] != want).sum()))
 
 
 def test_train_model_on_frames(pkg, cuda):
@@ -118,7 +198,6 @@ def test_train_model_on_frames(pkg, cuda):
     crit = pkg.get_loss_function({"loss_fn": "bce"})
     opt = pkg.Adam(m.parameters(), lr=1e-3, weight_decay=1e-5)
     cfg = {"batch_size": 4, "img_size": 64, "verbose": False}
-    with pytest.warns(RuntimeWarning):
-        res = pkg.train_model(m, imgs[:4], masks[:4], imgs[4:], masks[4:], crit, opt, None, 2,
-                              torch.device("cuda"), cfg, augmentations_per_image=1)
+    res = pkg.train_model(m, imgs[:4], masks[:4], imgs[4:], masks[4:], crit, opt, None, 2,
+                          torch.device("cuda"), cfg, augmentations_per_image=1)
     assert len(res["train_metrics"]) == 2 and np.isfinite(res["final_train_metrics"]["loss"])
