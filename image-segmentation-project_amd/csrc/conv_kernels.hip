@@ -1287,79 +1287,11 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
   }
 }
 
-// dW index of element e of slab unit u (SlabLayout), -1 if that accumulator
-// lane holds no dW element (tile tails, the idle half of a CO32 block)
-__device__ __forceinline__ long long slab_dw_index(const SlabLayout& L, long long u, int e) {
-  const int lane = (int)(u & 63);
-  long long r = u >> 6;
-  const int frag = (int)(r % L.nf);
-  r /= L.nf;
-  const int wave = (int)(r % L.nw);
-  const int blk = (int)(r / L.nw);
-  const int g = lane >> 4, li = lane & 15;
-  if (L.kind == SLAB_HALO) {
-    // CO32 slabs hold only the wm = 0 waves (wave slot = wn)
-    const int t = frag >> 1, i = frag & 1, wm = L.co32 ? 0 : (wave & 1), wn = L.co32 ? wave : (wave >> 1);
-    const int cob = blk % L.co_blocks, cib = blk / L.co_blocks;
-    if (frag >= 18) {  // folded downsample: dW2 [Cout][C]
-      const int co = cob * 64 + wm * 32 + i * 16 + 4 * g + e;
-      if (co >= L.Cout) return -1;
-      return L.dw2_off + (long long)co * L.C + cib * L.ci + wn * 16 + li;
-    }
-    const int co = cob * (L.co32 ? 32 : 64) + (L.co32 ? 0 : wm * 32) + i * 16 + 4 * g + e;
-    const int c = cib * L.ci + wn * 16 + li;
-    if (co >= L.Cout) return -1;
-    return (long long)co * L.Krow + t * L.C + c;
-  }
-  if (L.kind == SLAB_GEMM) {
-    const int i = frag / L.fn, j = frag % L.fn;
-    const int wm = wave % L.wm, wn = wave / L.wm;
-    const int cob = blk % L.co_blocks, rest = blk / L.co_blocks;
-    const int cblk = rest % L.c_blocks, tap = rest / L.c_blocks;
-    const int co = cob * L.bmo + wm * (L.bmo / L.wm) + i * 16 + 4 * g + e;
-    const int c = cblk * L.bnc + wn * (L.bnc / L.wn) + j * 16 + li;
-    if (c >= L.cmax || co >= L.Cout) return -1;
-    return (long long)co * L.Krow + (long long)tap * L.C + c;
-  }
-  // SLAB_STEM: one block per (split, 64-channel group blk), 4 waves of 32 co x 32 k
-  const int i = frag >> 1, j = frag & 1, wm = wave & 1, wn = wave >> 1;
-  return (long long)(blk * 64 + wm * 32 + i * 16 + 4 * g + e) * 64 + wn * 32 + j * 16 + li;
-}
-
-// dW = sum over the splits of the slab, bit-reproducible: a block covers
-// 256/T consecutive units x T split lanes (lane-major over units, so every wave
-// instruction reads whole runs of 16-B units); split lane r sums splits r, r+T,
-// r+2T, ... in that order (eight loads in flight), then the T partials are
-// added in r order through LDS.  The partition and both orders are fixed, so
-// the result does not depend on timing.  Every dW element is written once.
+// dW = sum over the splits of the slab (slab_reduce_block, common.h)
 __global__ void __launch_bounds__(256) wgrad_slab_reduce_kernel(const f32x4* __restrict__ slab,
                                                                 float* __restrict__ dw, SlabLayout L, int T) {
   __shared__ f32x4 part[256];
-  const int tid = threadIdx.x;
-  const int per = 256 / T;
-  const int ul = tid % per, r = tid / per;
-  const long long u = (long long)blockIdx.x * per + ul;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  if (u < L.units) {
-    int k = r;
-    for (; k + 7 * T < L.splits; k += 8 * T) {
-      f32x4 v[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = slab[(long long)(k + q * T) * L.units + u];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) acc += v[q];
-    }
-    for (; k < L.splits; k += T) acc += slab[(long long)k * L.units + u];
-  }
-  part[tid] = acc;
-  __syncthreads();
-  if (r != 0 || u >= L.units) return;
-  for (int j = 1; j < T; ++j) acc += part[j * per + ul];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const long long idx = slab_dw_index(L, u, e);
-    if (idx >= 0) dw[idx] = acc[e];
-  }
+  slab_reduce_block(slab, dw, L, T, blockIdx.x, part);
 }
 
 // ---------------------------------------------------------------------------
@@ -2100,19 +2032,66 @@ static hipError_t launch_wgrad_halo(const ConvWgradArgs& a0, hipStream_t st) {
 
 bool wgrad_pending() { return g_pending.slab != nullptr; }
 
-hipError_t launch_wgrad_finish(hipStream_t st) {
-  if (!g_pending.slab) return hipSuccess;
-  const PendingReduce r = g_pending;
-  g_pending = PendingReduce{};
-  // split lanes per unit: each thread's loads (<= 8) all in flight at once, up to 16
-  int T = 1;
+// split lanes per unit (each thread's loads, <= 8, all in flight at once; up to
+// 16 lanes) and the block count of the reduction of r
+static void reduce_geometry(const PendingReduce& r, int& T, long long& blocks) {
+  T = 1;
   while (T < 16 && (long long)T * 8 < r.L.splits) T <<= 1;
   const long long per = 256 / T;
-  const long long bx = (r.L.units + per - 1) / per;
+  blocks = (r.L.units + per - 1) / per;
+}
+
+static hipError_t launch_reduce(const PendingReduce& r, hipStream_t st) {
+  int T;
+  long long bx;
+  reduce_geometry(r, T, bx);
   set_kernel_tag("wgrad_slab_reduce_kernel");
   hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)bx), dim3(256), 0, st,
                      reinterpret_cast<const f32x4*>(r.slab), r.dw, r.L, T);
   return hipGetLastError();
+}
+
+hipError_t launch_wgrad_finish(hipStream_t st) {
+  if (!g_pending.slab) return hipSuccess;
+  const PendingReduce r = g_pending;
+  g_pending = PendingReduce{};
+  return launch_reduce(r, st);
+}
+
+static thread_local PendingReduce g_deferred{};
+
+bool wgrad_defer() {
+  if (!g_pending.slab || g_deferred.slab) return false;
+  g_deferred = g_pending;
+  g_pending = PendingReduce{};
+  return true;
+}
+bool wgrad_deferred() { return g_deferred.slab != nullptr; }
+
+bool wgrad_take_deferred(ReduceTail* t) {
+  if (!g_deferred.slab) return false;
+  long long bx;
+  reduce_geometry(g_deferred, t->T, bx);
+  t->slab = g_deferred.slab;
+  t->dw = g_deferred.dw;
+  t->L = g_deferred.L;
+  t->blocks = (int)bx;
+  g_deferred = PendingReduce{};
+  return true;
+}
+
+hipError_t launch_slab_reduce(const ReduceTail& r, hipStream_t st) {
+  set_kernel_tag("wgrad_slab_reduce_kernel");
+  hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)r.blocks), dim3(256), 0, st,
+                     reinterpret_cast<const f32x4*>(r.slab), r.dw, r.L, r.T);
+  return hipGetLastError();
+}
+
+hipError_t launch_wgrad_flush(hipStream_t st) {
+  if (!g_deferred.slab) return hipSuccess;
+  const PendingReduce r = g_deferred;
+  g_deferred = PendingReduce{};
+  return launch_reduce(r, st);
 }
 
 hipError_t launch_convt_wgrad(const ConvWgradArgs& a0, hipStream_t st) {

@@ -6,6 +6,7 @@
 // wave instruction moves 1 KiB; per-channel reductions are kept in registers
 // per thread (each thread owns one 8-channel chunk for its whole pixel loop),
 // folded through LDS once per block and published with fp64 atomics.
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
@@ -295,16 +296,33 @@ hipError_t launch_bn_bwd_reduce(const BnBwdArgs& a, hipStream_t st) {
 // registers.  RELU: dZ = dA * (act > 0) (unfused path; the fused producers
 // store dZ itself).  Blocks grid-stride over passes of kBnPPT pixels per
 // thread with the next pass's loads issued before the current pass's math.
-template <bool TWO, bool RELU>
-__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, double inv_n) {
+// RED: a deferred split-K reduction (ReduceTail) rides as trailing blocks of a
+// 1-D grid: flat block ids [0, gx * gy) are the apply's (bx, by), the rest
+// reduce (256-thread blocks; the coefficient LDS doubles as the reduction's)
+template <bool TWO, bool RELU, bool RED>
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, double inv_n, ReduceTail rt, int gxa,
+                                                           int gya) {
+  extern __shared__ __attribute__((aligned(16))) float coef[];  // [6][CG]
+  int bx, by, gx;
+  if constexpr (RED) {
+    const int flat = blockIdx.x;
+    if (flat >= gxa * gya) {
+      slab_reduce_block(reinterpret_cast<const f32x4*>(rt.slab), rt.dw, rt.L, rt.T, flat - gxa * gya,
+                        reinterpret_cast<f32x4*>(coef));
+      return;
+    }
+    bx = flat % gxa; by = flat / gxa; gx = gxa;
+  } else {
+    bx = blockIdx.x; by = blockIdx.y; gx = gridDim.x;
+  }
   const int CG = bn_group(a.C);
   const int CC = CG >> 3;
   const int rows = blockDim.x / CC;
   const int chunk = threadIdx.x % CC, row = threadIdx.x / CC;
-  const int cg0 = blockIdx.y * CG;
+  const int cg0 = by * CG;
   const int c8 = cg0 + (chunk << 3);
   constexpr int PPT = kBnPPT;
-  const int64_t stride = (int64_t)gridDim.x * rows;
+  const int64_t stride = (int64_t)gx * rows;
   uint4 uda[PPT], uact[PPT], uy[PPT], uy2[PPT];
   auto load = [&](int64_t base) {
 #pragma unroll
@@ -318,9 +336,8 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, double i
       if constexpr (TWO) uy2[u] = in ? *reinterpret_cast<const uint4*>(a.y2 + pix * a.ldy2 + c8) : z;
     }
   };
-  int64_t base = (int64_t)blockIdx.x * rows + row;
+  int64_t base = (int64_t)bx * rows + row;
   if (row < rows) load(base);  // first pass in flight during the prologue
-  extern __shared__ __attribute__((aligned(16))) float coef[];  // [6][CG]
   for (int c = threadIdx.x; c < CG; c += blockDim.x) {
     const int ch = cg0 + c;
     float k1, m1, m2, k1b = 0.f, m2b = 0.f;
@@ -341,7 +358,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, double i
       m1 = (float)(s1 * inv_n);
       m2 = (float)(s2 * inv_n);
       if (TWO) { k1b = a.gamma2[ch] * a.invstd2[ch]; m2b = (float)(t2 * inv_n); }
-      if (blockIdx.x == 0) {
+      if (bx == 0) {
         a.dgamma[ch] = (float)s2;
         a.dbeta[ch] = (float)s1;
         if (TWO) {
@@ -419,10 +436,27 @@ hipError_t launch_bn_bwd_apply(const BnBwdArgs& a, hipStream_t st) {
   const size_t lds = 6 * bn_group(a.C) * sizeof(float);
   const double inv_n = 1.0 / (double)a.npix;
   const bool two = a.y2 != nullptr;
-  if (two && a.relu) hipLaunchKernelGGL((bn_bwd_apply_kernel<true, true>), g, b, lds, st, a, inv_n);
-  else if (two) hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false>), g, b, lds, st, a, inv_n);
-  else if (a.relu) hipLaunchKernelGGL((bn_bwd_apply_kernel<false, true>), g, b, lds, st, a, inv_n);
-  else hipLaunchKernelGGL((bn_bwd_apply_kernel<false, false>), g, b, lds, st, a, inv_n);
+  const ReduceTail r = {};
+  if (two && a.relu) hipLaunchKernelGGL((bn_bwd_apply_kernel<true, true, false>), g, b, lds, st, a, inv_n, r, 0, 0);
+  else if (two) hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false, false>), g, b, lds, st, a, inv_n, r, 0, 0);
+  else if (a.relu) hipLaunchKernelGGL((bn_bwd_apply_kernel<false, true, false>), g, b, lds, st, a, inv_n, r, 0, 0);
+  else hipLaunchKernelGGL((bn_bwd_apply_kernel<false, false, false>), g, b, lds, st, a, inv_n, r, 0, 0);
+  return hipGetLastError();
+}
+
+hipError_t launch_bn_bwd_apply_reduce(const BnBwdArgs& a, const ReduceTail& r, hipStream_t st) {
+  if (!bn_group_ok(a.C)) return hipErrorInvalidValue;
+  if (!a.relu && a.dres) return hipErrorInvalidValue;
+  const dim3 g = bn_grid(a.npix, a.C), b = chunk_block(bn_group(a.C));
+  if (b.x != 256 || r.blocks <= 0) return hipErrorNotSupported;  // the reduction's block shape
+  const size_t lds = std::max<size_t>(6 * bn_group(a.C) * sizeof(float), 256 * 16);
+  const double inv_n = 1.0 / (double)a.npix;
+  const bool two = a.y2 != nullptr;
+  const dim3 g1(g.x * g.y + r.blocks);
+  if (two && a.relu) hipLaunchKernelGGL((bn_bwd_apply_kernel<true, true, true>), g1, b, lds, st, a, inv_n, r, g.x, g.y);
+  else if (two) hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false, true>), g1, b, lds, st, a, inv_n, r, g.x, g.y);
+  else if (a.relu) hipLaunchKernelGGL((bn_bwd_apply_kernel<false, true, true>), g1, b, lds, st, a, inv_n, r, g.x, g.y);
+  else hipLaunchKernelGGL((bn_bwd_apply_kernel<false, false, true>), g1, b, lds, st, a, inv_n, r, g.x, g.y);
   return hipGetLastError();
 }
 
@@ -1157,29 +1191,62 @@ hipError_t launch_unpack(const UnpackTable& t, hipStream_t st) {
 // ---------------------------------------------------------------------------
 // pixel-wise loss and mask metrics (losses.py:13-37,161-171; utils.py:120-151)
 // ---------------------------------------------------------------------------
+// One pass over the pixels: 8 per-thread fp32 sums, folded per block in fp64
+// and added with fp64 atomics.  One block per CU (256 blocks): a 1024-block
+// grid put 1024 fp64 atomics on each of the 8 addresses, which serialised at
+// L2 (62 us per Base step for 4 M pixels; 256 per address now).  float4 loads
+// (4 in flight per thread) when both operands are 16-B aligned.
+__device__ __forceinline__ void loss_accum(float v, float y, int from_prob, float (&s)[8]) {
+  float pred;
+  if (!from_prob) {
+    // torch: (1 - y) * x - log_sigmoid(x),  log_sigmoid(x) = min(x,0) - log1p(exp(-|x|))
+    const float ls = fminf(v, 0.f) - log1pf(expf(-fabsf(v)));
+    s[0] += (1.f - y) * v - ls;
+    const float sg = 1.f / (1.f + expf(-v));
+    s[1] += sg * y;
+    s[2] += sg;
+    s[3] += y;
+    pred = v >= kMaskThreshold ? 1.f : 0.f;  // == (sigmoid_cpu(v) > 0.5)
+  } else {
+    pred = v > 0.5f ? 1.f : 0.f;
+  }
+  s[4] += pred * y;
+  s[5] += pred * (1.f - y);
+  s[6] += (1.f - pred) * y;
+  s[7] += (1.f - pred) * (1.f - y);
+}
+
 __global__ void __launch_bounds__(256) loss_sums_kernel(const float* x, const float* t, int64_t n,
                                                        double* sums, int from_prob) {
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const float v = x[i], y = t[i];
-    float pred;
-    if (!from_prob) {
-      // torch: (1 - y) * x - log_sigmoid(x),  log_sigmoid(x) = min(x,0) - log1p(exp(-|x|))
-      const float ls = fminf(v, 0.f) - log1pf(expf(-fabsf(v)));
-      s[0] += (1.f - y) * v - ls;
-      const float sg = 1.f / (1.f + expf(-v));
-      s[1] += sg * y;
-      s[2] += sg;
-      s[3] += y;
-      pred = v >= kMaskThreshold ? 1.f : 0.f;  // == (sigmoid_cpu(v) > 0.5)
-    } else {
-      pred = v > 0.5f ? 1.f : 0.f;
+  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t done = 0;
+  if (((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(t)) & 15) == 0) {
+    const int64_t n4 = n >> 2;
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    const float4* t4 = reinterpret_cast<const float4*>(t);
+    constexpr int U = 4;
+    for (int64_t i = tid; i < n4; i += U * nthr) {
+      float4 xv[U], tv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t j = i + u * nthr;
+        xv[u] = j < n4 ? x4[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+        tv[u] = j < n4 ? t4[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (i + u * nthr >= n4) break;
+        loss_accum(xv[u].x, tv[u].x, from_prob, s);
+        loss_accum(xv[u].y, tv[u].y, from_prob, s);
+        loss_accum(xv[u].z, tv[u].z, from_prob, s);
+        loss_accum(xv[u].w, tv[u].w, from_prob, s);
+      }
     }
-    s[4] += pred * y;
-    s[5] += pred * (1.f - y);
-    s[6] += (1.f - pred) * y;
-    s[7] += (1.f - pred) * (1.f - y);
+    done = n4 << 2;
   }
+  for (int64_t i = done + tid; i < n; i += nthr) loss_accum(x[i], t[i], from_prob, s);
   __shared__ double red[4][8];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
@@ -1196,7 +1263,7 @@ __global__ void __launch_bounds__(256) loss_sums_kernel(const float* x, const fl
 
 hipError_t launch_loss_sums(const float* logits, const float* target, int64_t n, double* sums, int from_prob,
                             hipStream_t st) {
-  hipLaunchKernelGGL(loss_sums_kernel, dim3(grid_for(n, 256 * 8, 1024)), dim3(256), 0, st, logits, target, n,
+  hipLaunchKernelGGL(loss_sums_kernel, dim3(grid_for(n, 256 * 16, 256)), dim3(256), 0, st, logits, target, n,
                      sums, from_prob);
   return hipGetLastError();
 }

@@ -200,6 +200,9 @@ struct unet_plan {
   // BasicBlock downsample (1x1 / s2) weight gradient folded into the conv1
   // (3x3 / s2) halo weight gradient (UNET_NO_DS_FOLD=1: separate launch, A/B)
   bool ds_wgrad_fold = std::getenv("UNET_NO_DS_FOLD") == nullptr;
+  // single-stream backward: a weight gradient's split-K reduction rides in the
+  // next BN-backward apply launch (UNET_NO_MERGE_REDUCE=1: separate launches)
+  bool merge_reduce = std::getenv("UNET_NO_MERGE_REDUCE") == nullptr;
   double flops_fwd = 0, flops_train = 0;
   // fp8 forward (cfg.fp8): per-tensor delayed-amax states (fp8.hip) for the
   // conv weights and activations; the first forward calibrates
@@ -968,6 +971,15 @@ int wgrad_and_reduce(const Ctx& x, ConvWgradArgs& a, int mode, const std::string
     else CK(launch_conv_wgrad(a, mode, x.wst));
   }
   if (!wgrad_pending()) return 0;
+  if (p->merge_reduce && x.rst == x.wst && x.wst == x.st) {
+    // one reduction at most waits for an apply launch; an older one runs now
+    // (it reads the other slab, so the order against this wgrad is free)
+    if (wgrad_deferred()) {
+      ProfScope pr(p, x.rst, "wgrad_reduce (deferred)", 0);
+      CK(launch_wgrad_flush(x.rst));
+    }
+    if (wgrad_defer()) return 0;
+  }
   if (x.rst != x.wst) RUN(stream_edge(p, x.wst, x.rst));
   {
     ProfScope pr(p, x.rst, "wgrad_reduce " + name, 0);
@@ -1084,11 +1096,31 @@ int bn_backward(const Ctx& x, int bi, BnBwdArgs a, bool fused) {
   } else {
     CK(launch_bn_bwd_reduce(a, x.st));
   }
+  ReduceTail r;
+  if (wgrad_deferred() && x.wst == x.st && wgrad_take_deferred(&r)) {
+    const hipError_t e = launch_bn_bwd_apply_reduce(a, r, x.st);
+    if (e == hipSuccess) return 0;
+    if (e != hipErrorNotSupported) CK(e);
+    // this apply's shape cannot carry it: the reduction on its own, then the apply
+    CK(launch_bn_bwd_apply(a, x.st));
+    CK(launch_slab_reduce(r, x.st));
+    return 0;
+  }
   CK(launch_bn_bwd_apply(a, x.st));
   return 0;
 }
 
+// a deferred reduction that no apply launch took (bucket boundaries, end of
+// the backward)
+int flush_reduce(const Ctx& x) {
+  if (!wgrad_deferred()) return 0;
+  ProfScope pr(x.p, x.wst, "wgrad_reduce (deferred)", 0);
+  CK(launch_wgrad_flush(x.wst));
+  return 0;
+}
+
 int unpack_bucket(const Ctx& x, int bk, float* grads) {
+  RUN(flush_reduce(x));
   if (x.rst != x.wst) RUN(stream_edge(x.p, x.rst, x.wst));  // every reduction so far is in dW
   ProfScope ps(x.p, x.wst, "unpack", 0);
   UnpackTable t;

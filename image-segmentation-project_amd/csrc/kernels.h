@@ -186,6 +186,20 @@ hipError_t launch_convt_wgrad(const ConvWgradArgs& a, hipStream_t st);
 // that launch needed no reduction: one split, or the atomic path)
 hipError_t launch_wgrad_finish(hipStream_t st);
 bool wgrad_pending();
+// A split-K reduction riding as extra blocks [apply_blocks, apply_blocks +
+// blocks) of the next BN-backward apply launch (same stream): the apply and the
+// reduction are independent streaming passes, one launch boundary instead of
+// two.  wgrad_defer() moves the pending reduction into the deferred slot (false
+// if that slot is taken); wgrad_take_deferred() hands it to an apply launch;
+// launch_wgrad_flush() runs a deferred one on its own.
+struct ReduceTail {
+  const void* slab; float* dw; SlabLayout L; int T; int blocks;
+};
+bool wgrad_defer();
+bool wgrad_deferred();
+bool wgrad_take_deferred(ReduceTail* t);
+hipError_t launch_wgrad_flush(hipStream_t st);
+hipError_t launch_slab_reduce(const ReduceTail& r, hipStream_t st);  // r on its own
 const char* last_kernel_tag();  // template instance of the last conv launch (profiler)
 
 // ---- elementwise / reduction kernels (elementwise.hip) ----
@@ -202,6 +216,9 @@ hipError_t launch_bn_apply(const BnApplyArgs& a, hipStream_t st);
 
 hipError_t launch_bn_bwd_reduce(const BnBwdArgs& a, hipStream_t st);
 hipError_t launch_bn_bwd_apply(const BnBwdArgs& a, hipStream_t st);
+// the same with a deferred split-K reduction as trailing blocks (256-thread
+// apply blocks only, i.e. C % 64 == 0); hipErrorNotSupported otherwise
+hipError_t launch_bn_bwd_apply_reduce(const BnBwdArgs& a, const ReduceTail& r, hipStream_t st);
 
 struct MaxPoolArgs {
   const bf16_t* x; int ldx; bf16_t* y; int ldy; uint8_t* idx;
