@@ -354,6 +354,8 @@ SLAB_CASES = [  # N, Ci, H, Co, R, stride, pad, stem  -- every wgrad kernel fami
     (4, 32, 64, 32, 3, 1, 1, 0),     # halo CO32 (decoder1 shape)
     (2, 96, 64, 32, 3, 1, 1, 0),     # halo 32-channel blocks, CO32
     (2, 512, 16, 512, 3, 1, 1, 0),   # halo, one split (block owns its tile)
+    (4, 128, 16, 128, 3, 1, 1, 0),   # halo 16-wide tiles (16x16 maps), several splits
+    (2, 64, 64, 96, 3, 1, 1, 0),     # halo, output-channel tail (96 = 64 + 32)
     (2, 64, 32, 128, 3, 2, 1, 0),    # stride-2 halo wgrad (2TH+1 x 2TW+1 input halo), many splits
     (2, 128, 64, 256, 3, 2, 1, 0),   # stride-2 halo, enc3.0 shape family
     (4, 256, 32, 512, 3, 2, 1, 0),   # stride-2 halo, enc4.0 shape family (16x16 output)
