@@ -945,10 +945,30 @@ static hipError_t launch_halo_shape(const ConvFwdArgs& a, hipStream_t st) {
   if (wscfg == 2 && C == 64 && Co % 32 == 0 && a.P % 8 == 0) return launch_ws<2, 2, 8, 4, FLIP>(a, st);
   if (wscfg == 3 && C == 64 && Co % 32 == 0 && a.P % 8 == 0) return launch_ws<2, 2, 8, 8, FLIP>(a, st);
   if (C == 64 && Co % 64 == 0 && a.P % 16 == 0) return launch_ws<2, 4, 16, 8, FLIP>(a, st);
-  if (C == 32 && Co == 32 && a.P % 16 == 0) return launch_ws<1, 2, 16, 4, FLIP>(a, st);
-  if (C == 32 && Co == 96 && a.P % 16 == 0) return launch_ws<1, 6, 16, 8, FLIP>(a, st);
+  // decoder1 shapes (256^2, 96 / 32 channels), UNET_D1CFG sweep on the Base
+  // config: 8-row tiles on 8 waves (one row each, two waves per SIMD hide each
+  // other's LDS latency) beat the 4-wave and 16-row tiles except for the 32->32
+  // forward (decoder1.0 dgrad 140 -> 111 us: the FN = 6 block spilled 36
+  // VGPRs; decoder1.0 fwd 121 -> 104, decoder1.3 dgrad 60 -> 55)
+  static const int d1 = std::getenv("UNET_D1CFG") ? std::atoi(std::getenv("UNET_D1CFG")) : 0;  // tuning
+  if (C == 32 && Co == 32 && a.P % 16 == 0) {
+    if (d1 == 1) return launch_ws<1, 2, 16, 8, FLIP>(a, st);
+    if (d1 == 2) return launch_ws<1, 2, 8, 4, FLIP>(a, st);
+    if (FLIP || d1 == 3) return launch_ws<1, 2, 8, 8, FLIP>(a, st);
+    return launch_ws<1, 2, 16, 4, FLIP>(a, st);
+  }
+  if (C == 32 && Co == 96 && a.P % 16 == 0) {
+    if (d1 == 1) return launch_ws<1, 2, 16, 8, FLIP>(a, st);
+    if (d1 == 2) return launch_ws<1, 6, 16, 4, FLIP>(a, st);
+    if (d1 == 4) return launch_ws<1, 6, 16, 8, FLIP>(a, st);
+    return launch_ws<1, 2, 8, 8, FLIP>(a, st);
+  }
   if (C == 32 && Co % 64 == 0 && a.P % 16 == 0) return launch_ws<1, 4, 16, 8, FLIP>(a, st);
-  if (C == 96 && Co == 32 && a.P % 8 == 0) return launch_ws<3, 2, 8, 4, FLIP>(a, st);
+  if (C == 96 && Co == 32 && a.P % 8 == 0) {
+    if (d1 == 2 && a.P % 4 == 0) return launch_ws<3, 2, 4, 4, FLIP>(a, st);
+    if (d1 == 4) return launch_ws<3, 2, 8, 4, FLIP>(a, st);
+    return launch_ws<3, 2, 8, 8, FLIP>(a, st);
+  }
   // halo-streamed: 256-pixel tiles while they still give >= ~1 block per CU
   if (C % 32 == 0 && C >= 128 && Co % 64 == 0) {
     const long long t16 = (long long)a.N * (a.P / 16) * (a.Q / 16) * (Co / 64);
