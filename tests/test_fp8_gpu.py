@@ -151,7 +151,7 @@ def test_fp8_model_forward_ops_and_end_to_end(pkg, cuda, width):
     """Every fp8 conv, teacher-forced on the executor's own bf16 input: relative
     L2 <= 0.08 against the fp32 conv (e4m3 carries 3 mantissa bits; measured
     ~3e-2); the bf16 layers keep 2e-2.  End to end vs the fp32 oracle: BCE loss
-    within 3 %, |IoU diff| <= 2e-2 (values printed)."""
+    within 3 %, |IoU diff| <= 1e-3 (north_star bar; values printed)."""
     torch.manual_seed(0)
     N, Hs = 2, 128
     ref = oracle.ReferenceUNet(width=width)
@@ -198,7 +198,7 @@ def test_fp8_model_forward_ops_and_end_to_end(pkg, cuda, width):
     print(f"width {width} fp8: loss {loss.item():.5f} vs {rloss:.5f}, IoU {iou:.5f} vs {iou_ref:.5f}, "
           f"logits rel {_rel(out.detach(), rl.detach()):.3e}")
     assert abs(loss.item() - rloss) <= 0.03 * rloss
-    assert abs(iou - iou_ref) <= 2e-2
+    assert abs(iou - iou_ref) <= 1e-3
     for k, p_ in m.named_parameters():
         assert torch.isfinite(p_.grad).all(), k
 
