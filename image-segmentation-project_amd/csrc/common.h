@@ -217,6 +217,30 @@ __device__ __forceinline__ void bn_finalize(const unet::BnLaunch& p) {
   }
 }
 
+// Per-channel BN-backward apply coefficients from the replica sums:
+// dY = A dZ + B y + C, A = k1 = gamma invstd, B = -k1 invstd m2,
+// C = k1 (invstd m2 mu - m1), m1 = mean dZ, m2 = mean dZ xhat.  Shared by
+// bn_bwd_apply_kernel and the BN-fused weight gradient (its dY side product
+// must be bit-identical to the apply pass): no contraction, fixed order.
+__device__ __forceinline__ void bn_bwd_apply_coef(const unet::BnBwdArgs& a, int ch, double inv_n, float& A,
+                                                  float& B, float& C, double& s1, double& s2) {
+#pragma clang fp contract(off)
+  s1 = 0.0;
+  s2 = 0.0;
+  for (int r = 0; r < unet::kStatRep; ++r) {
+    const size_t rep = (size_t)r * 2 * a.C;
+    s1 += a.sums[rep + ch];
+    s2 += a.sums[rep + a.C + ch];
+  }
+  // explicit round-to-nearest operations: no context-dependent contraction
+  const float k1 = __fmul_rn(a.gamma[ch], a.invstd[ch]);
+  const float m1 = (float)__dmul_rn(s1, inv_n), m2 = (float)__dmul_rn(s2, inv_n);
+  const float is = a.invstd[ch], mu = a.mean[ch];
+  A = k1;
+  B = __fmul_rn(__fmul_rn(-k1, is), m2);
+  C = __fmul_rn(k1, __fsub_rn(__fmul_rn(__fmul_rn(is, m2), mu), m1));
+}
+
 // Last block of a BN-backward reduction (bn_bwd_reduce_kernel or a fused
 // conv-dgrad epilogue): per-channel coefficients of the apply pass and the
 // parameter gradients dgamma = sum dZ*xhat, dbeta = sum dZ.

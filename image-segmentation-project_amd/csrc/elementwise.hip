@@ -347,17 +347,14 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, double i
       m2 = a.coef[2 * a.C + ch];
       if (TWO) { k1b = a.coef[3 * a.C + ch]; m2b = a.coef[4 * a.C + ch]; }
     } else {
-      double s1 = 0.0, s2 = 0.0, t2 = 0.0;
-      for (int r = 0; r < kStatRep; ++r) {
-        const size_t rep = (size_t)r * 2 * a.C;
-        s1 += a.sums[rep + ch];
-        s2 += a.sums[rep + a.C + ch];
-        if (TWO) t2 += a.sums2[rep + a.C + ch];
+      double s1, s2, t2 = 0.0;
+      float cA, cB, cC;
+      bn_bwd_apply_coef(a, ch, inv_n, cA, cB, cC, s1, s2);
+      if (TWO) {
+        for (int r = 0; r < kStatRep; ++r) t2 += a.sums2[(size_t)r * 2 * a.C + a.C + ch];
+        k1b = a.gamma2[ch] * a.invstd2[ch];
+        m2b = (float)(t2 * inv_n);
       }
-      k1 = a.gamma[ch] * a.invstd[ch];
-      m1 = (float)(s1 * inv_n);
-      m2 = (float)(s2 * inv_n);
-      if (TWO) { k1b = a.gamma2[ch] * a.invstd2[ch]; m2b = (float)(t2 * inv_n); }
       if (bx == 0) {
         a.dgamma[ch] = (float)s2;
         a.dbeta[ch] = (float)s1;
@@ -366,6 +363,17 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, double i
           a.dbeta2[ch] = (float)s1;  // same dZ feeds both BNs
         }
       }
+      coef[c] = cA;
+      coef[CG + c] = cB;
+      coef[2 * CG + c] = cC;
+      m1 = (float)(s1 * inv_n);
+      if (TWO) {
+        const float isb = a.invstd2[ch], mub = a.mean2[ch];
+        coef[3 * CG + c] = k1b;
+        coef[4 * CG + c] = -k1b * isb * m2b;
+        coef[5 * CG + c] = k1b * (isb * m2b * mub - m1);
+      }
+      continue;
     }
     const float is = a.invstd[ch], mu = a.mean[ch];
     coef[c] = k1;
