@@ -199,6 +199,8 @@ def main():
     ap.add_argument("--graph", dest="graph", action="store_true", default=None,
                     help="replay the step as one HIP graph (default for --gpus 1)")
     ap.add_argument("--no-graph", dest="graph", action="store_false")
+    ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="N>1: gradient exchange dtype (bf16: opt-in compression, ddp.py)")
     ap.add_argument("--torch-adam", action="store_true",
                     help="torch.optim.Adam (foreach) instead of the fused HIP Adam (optim.py)")
     args = ap.parse_args()
@@ -223,7 +225,7 @@ def main():
     model = pkg.UNetWithBackbone(n_classes=1, backbone=args.backbone, pretrained=False,
                                   use_attention=args.attention, width=args.width, fp8=args.fp8).to(dev)
     if world > 1:
-        ddp.enable_data_parallel(model)
+        ddp.enable_data_parallel(model, grad_dtype=args.grad_dtype)
     use_graph = args.graph if args.graph is not None else world == 1
     if args.torch_adam:
         opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-5, capturable=use_graph)
@@ -323,7 +325,8 @@ def main():
                    + f" U-Net {args.backbone} " + ("attention" if args.attention else "no-attention")
                    + " train step (fwd+bce+bwd+Adam)",
                    "global_batch": args.batch * world, "image": f"{args.size}x{args.size}",
-                   "parallelism": f"dp{world}", "fp8": bool(args.fp8)},
+                   "parallelism": f"dp{world}", "fp8": bool(args.fp8),
+                   "grad_exchange": args.grad_dtype if world > 1 else None},
         "roofline": {"bound": "mfma", "achieved": round(achieved_tflops, 2), "peak": dom_peak,
                      "unit": "TFLOP/s", "frac": round(achieved_tflops / dom_peak, 4),
                      "traffic": traffic,

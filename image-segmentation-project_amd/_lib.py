@@ -60,6 +60,8 @@ SIGNATURES = {
     "unet_mask_metrics": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
     "unet_adam_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float,
                                c_float, c_float, c_int, c_void_p]),
+    "unet_grad_to_bf16": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "unet_grad_from_bf16": (c_int, [c_void_p, c_void_p, c_int64, c_float, c_void_p]),
     "unet_conv_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]
                       + [c_int] * 12 + [c_void_p]),
     "unet_conv_wgrad": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p] + [c_int] * 12 + [c_void_p]),

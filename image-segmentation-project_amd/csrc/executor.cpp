@@ -1895,6 +1895,24 @@ int unet_adam_step(float* params, const float* grads, float* exp_avg, float* exp
   return 0;
 }
 
+int unet_grad_to_bf16(const float* src, void* dst, int64_t n, hipStream_t stream) {
+  if (n < 0 || (n > 0 && (!src || !dst))) {
+    set_err("unet_grad_to_bf16: null buffer or negative size");
+    return 1;
+  }
+  CK(launch_grad_to_bf16(src, (bf16_t*)dst, n, stream));
+  return 0;
+}
+
+int unet_grad_from_bf16(const void* src, float* dst, int64_t n, float scale, hipStream_t stream) {
+  if (n < 0 || (n > 0 && (!src || !dst))) {
+    set_err("unet_grad_from_bf16: null buffer or negative size");
+    return 1;
+  }
+  CK(launch_grad_from_bf16((const bf16_t*)src, dst, n, scale, stream));
+  return 0;
+}
+
 int unet_conv_fwd(const void* x, int ldx, const void* w, void* y, int ldy, const float* bias, const void* addend,
                   int ldadd, double* stats, int N, int H, int W, int C, int P, int Q, int Cout, int R, int S,
                   int stride, int pad, int mode, hipStream_t stream) {

@@ -298,6 +298,8 @@ hipError_t launch_loss_grad(const float* logits, const float* target, int64_t n,
 // fused Adam over flat fp32 buffers (optim.hip); coef = {step, step_size, sqrt(bc2)} on device
 hipError_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float* coef, float lr,
                        float beta1, float beta2, float eps, float wd, int advance_step, hipStream_t st);
+hipError_t launch_grad_to_bf16(const float* src, bf16_t* dst, int64_t n, hipStream_t st);
+hipError_t launch_grad_from_bf16(const bf16_t* src, float* dst, int64_t n, float scale, hipStream_t st);
 
 // on-GPU preprocessing of uint8 frames (data.hip; dataset.py:30-66,147-151)
 hipError_t launch_resize_area(const uint8_t* src, uint8_t* dst, int N, int H, int W, int oh, int ow, hipStream_t st);

@@ -87,4 +87,66 @@ hipError_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, 
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// bf16 gradient exchange (opt-in, ddp.enable_data_parallel(grad_dtype="bf16")):
+// the bucket is rounded to bf16 (RNE) before the all-reduce, which halves the
+// xGMI bytes, and widened back to fp32 (times `scale`, 1/world for a SUM
+// collective) after it.  The reference all-reduces nothing (single process);
+// torch DDP's bf16 compress hook is the semantics this mirrors.
+// ---------------------------------------------------------------------------
+template <bool VEC>
+__global__ void __launch_bounds__(256) grad_to_bf16_kernel(const float* __restrict__ src, bf16_t* __restrict__ dst,
+                                                           int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n8 = VEC ? n >> 3 : 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    const float4 a = reinterpret_cast<const float4*>(src)[2 * i];
+    const float4 b = reinterpret_cast<const float4*>(src)[2 * i + 1];
+    reinterpret_cast<uint4*>(dst)[i] =
+        make_uint4(pack_bf2(a.x, a.y), pack_bf2(a.z, a.w), pack_bf2(b.x, b.y), pack_bf2(b.z, b.w));
+  }
+  for (int64_t i = (n8 << 3) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = f2bf(src[i]);
+}
+
+template <bool VEC>
+__global__ void __launch_bounds__(256) grad_from_bf16_kernel(const bf16_t* __restrict__ src, float* __restrict__ dst,
+                                                             int64_t n, float scale) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n8 = VEC ? n >> 3 : 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    float f[8];
+    unpack8(reinterpret_cast<const uint4*>(src)[i], f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] *= scale;
+    reinterpret_cast<float4*>(dst)[2 * i] = make_float4(f[0], f[1], f[2], f[3]);
+    reinterpret_cast<float4*>(dst)[2 * i + 1] = make_float4(f[4], f[5], f[6], f[7]);
+  }
+  for (int64_t i = (n8 << 3) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    dst[i] = bf2f(src[i]) * scale;
+}
+
+static unsigned stream_blocks(int64_t n) {
+  int64_t b = (n / 8 + 255) / 256;
+  return (unsigned)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
+}
+
+hipError_t launch_grad_to_bf16(const float* src, bf16_t* dst, int64_t n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (((uintptr_t)src | (uintptr_t)dst) % 16 == 0)
+    hipLaunchKernelGGL(grad_to_bf16_kernel<true>, dim3(stream_blocks(n)), dim3(256), 0, st, src, dst, n);
+  else
+    hipLaunchKernelGGL(grad_to_bf16_kernel<false>, dim3(stream_blocks(8 * n)), dim3(256), 0, st, src, dst, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_grad_from_bf16(const bf16_t* src, float* dst, int64_t n, float scale, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (((uintptr_t)src | (uintptr_t)dst) % 16 == 0)
+    hipLaunchKernelGGL(grad_from_bf16_kernel<true>, dim3(stream_blocks(n)), dim3(256), 0, st, src, dst, n, scale);
+  else
+    hipLaunchKernelGGL(grad_from_bf16_kernel<false>, dim3(stream_blocks(8 * n)), dim3(256), 0, st, src, dst, n,
+                       scale);
+  return hipGetLastError();
+}
+
 }  // namespace unet

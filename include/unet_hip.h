@@ -120,6 +120,15 @@ int unet_adam_step(float* params, const float* grads, float* exp_avg, float* exp
                    int64_t n, float lr, float beta1, float beta2, float eps, float weight_decay,
                    int advance_step, hipStream_t stream);
 
+/* ---- bf16 gradient exchange (opt-in DDP compression) ----
+ * Replace nothing in the reference (it trains in one process); they sit at
+ * the DDP insertion point train.py:48-49, around each bucket's all-reduce:
+ * dst[i] = bf16_rne(src[i]) before it, dst[i] = float(src[i]) * scale after
+ * it (scale = 1/world for a SUM collective).  n elements; any alignment (16-B
+ * aligned buffers take the 8-wide path). */
+int unet_grad_to_bf16(const float* src, void* dst, int64_t n, hipStream_t stream);
+int unet_grad_from_bf16(const void* src, float* dst, int64_t n, float scale, hipStream_t stream);
+
 /* ---- single ops (tests / custom graphs) ---- */
 /* mode 0: conv  y = conv(x, w) [stride, pad]           (w packed [Cout][R][S][C])
  * mode 1: transposed gather (conv dgrad / ConvTranspose2d forward)
