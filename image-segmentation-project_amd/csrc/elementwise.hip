@@ -18,9 +18,12 @@ constexpr float kMaskThreshold = 8.94069742685133e-08f;  // 0x33C00001, SURVEY.m
 
 // grid cap of the BN apply kernels (each block recomputes the per-channel
 // coefficients in its prologue; fewer, longer blocks amortise that and keep
-// the next pass's loads in flight: 512 = 2 blocks per CU, measured best of
-// 256..4096 for both directions on the Base config)
-static int g_apply_cap = std::getenv("UNET_APPLY_CAP") ? std::atoi(std::getenv("UNET_APPLY_CAP")) : 512;
+// the next pass's loads in flight).  256 = 1 block per CU: since split-K
+// reductions ride as trailing blocks of the backward apply, the smaller apply
+// grid leaves the other CU slots to them (A/B on one box: bn_bwd 0.85 -> 0.81
+// ms, 2445 -> 2466 img/s; 128 and 192 were slower, 512 was best before the
+// reductions were merged)
+static int g_apply_cap = std::getenv("UNET_APPLY_CAP") ? std::atoi(std::getenv("UNET_APPLY_CAP")) : 256;
 
 static inline int grid_for(int64_t work, int per_block, int cap = 2048) {
   int64_t g = (work + per_block - 1) / per_block;
