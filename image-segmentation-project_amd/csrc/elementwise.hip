@@ -747,11 +747,15 @@ hipError_t launch_bn_relu_maxpool_fwd(const MaxPoolArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// blocks of the maxpool backward (tuning; its fused BN-backward sums end in
+// fp64 replica atomics, blocks / kStatRep per address)
+static int g_mp_blocks = std::getenv("UNET_MP_BLOCKS") ? std::atoi(std::getenv("UNET_MP_BLOCKS")) : 2048;
+
 hipError_t launch_maxpool_bwd(const MaxPoolArgs& a, hipStream_t st) {
   if (a.C % 8 || 256 % (a.C / 8)) return hipErrorInvalidValue;
   if (a.bb.sums && a.bb.y2) return hipErrorInvalidValue;
   const int nrows = a.N * a.H;
-  const int rpb = rows_per_block(nrows, 2048);
+  const int rpb = rows_per_block(nrows, g_mp_blocks);
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3((nrows + rpb - 1) / rpb), dim3(256), 0, st, a, rpb);
   return hipGetLastError();
 }
@@ -985,10 +989,14 @@ __global__ void __launch_bounds__(256) channel_sum_kernel(const bf16_t* x, int l
   }
 }
 
+// grid cap of the channel sums (tuning): each fp64 replica address takes
+// blocks / kStatRep atomics
+static int g_chsum_cap = std::getenv("UNET_CHSUM_CAP") ? std::atoi(std::getenv("UNET_CHSUM_CAP")) : 2048;
+
 hipError_t launch_channel_sum(const bf16_t* x, int ldx, int64_t npix, int C, double* acc, hipStream_t st) {
   if (C % 8 || C / 8 > 256) return hipErrorInvalidValue;
   const int CC = C / 8, rows = 256 / CC;
-  hipLaunchKernelGGL(channel_sum_kernel, dim3(grid_for(npix, rows * 8, 2048)), dim3(rows * CC),
+  hipLaunchKernelGGL(channel_sum_kernel, dim3(grid_for(npix, rows * 8, g_chsum_cap)), dim3(rows * CC),
                      (size_t)rows * C * sizeof(float), st, x, ldx, npix, C, acc);
   return hipGetLastError();
 }
