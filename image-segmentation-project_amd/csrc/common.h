@@ -33,6 +33,14 @@ using unet::kTimSlots;
 #define TSTAMP_RT(T, k) ((void)0)
 #endif
 
+// Phase ablation (debug builds only, `make abl`: -DUNET_TIMING -DUNET_ABL=n):
+// 1 = the halo conv / weight-gradient kernels skip their MFMA work, 2 = they
+// stage only the pipeline's first stages (later stages compute on stale LDS).
+// Outputs are garbage; only the phase stamps mean anything.
+#ifndef UNET_ABL
+#define UNET_ABL 0
+#endif
+
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 
 __device__ __forceinline__ float bf2f(bf16_t v) {

@@ -469,7 +469,7 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
 
   for (int k = 0; t < ntiles; ++k, t += nslot) {
     const int b = k & 1;
-    if (t + nslot < ntiles) {  // lands while this tile computes
+    if (t + nslot < ntiles && UNET_ABL != 2) {  // lands while this tile computes
       int n, oh0, ow0;
       tile_origin(t + nslot, n, oh0, ow0);
       issue_halo(hl + (b ^ 1) * HBUF, n, oh0, ow0);
@@ -514,7 +514,7 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
 #pragma unroll
       for (int i = 0; i < FN; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int p = 0; p < NP; ++p)
+    for (int p = 0; p < (UNET_ABL == 1 ? 0 : NP); ++p)
       mfma_panel<FN, RW, NP * COT * 64, FLIP>(acc, wl + p * COT * 64, H + p * PANEL, aoff, boff);
     if (k < 9) TSTAMP(a.tim, 2 + 2 * k);
     if (!PREF) epi.fetch(a, pix, co0, lane);
@@ -623,10 +623,10 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_hs_kernel(ConvFwdArgs a, int 
     wait_vmcnt<0>();               // stage kc landed (this wave's part) ...
     __builtin_amdgcn_s_barrier();  // ... everyone's; and stage kc-1 is no longer read
     if (kc < 16) TSTAMP(a.tim, 2 + kc);
-    if (kc + 1 < KC) issue(kc + 1, (kc + 1) & 1);
+    if (kc + 1 < KC && UNET_ABL != 2) issue(kc + 1, (kc + 1) & 1);
     else if (PREF) epi.fetch(a, pix, co0, lane);  // epilogue operands ride beside the last chunk
     const char* S = smem + (kc & 1) * STAGE;
-    mfma_panel<FN, RW, COT * 64, FLIP>(acc, S + HBYTES, S, aoff, boff);
+    if (UNET_ABL != 1) mfma_panel<FN, RW, COT * 64, FLIP>(acc, S + HBYTES, S, aoff, boff);
   }
   TSTAMP(a.tim, 20);
   if (!PREF) epi.fetch(a, pix, co0, lane);

@@ -1297,11 +1297,11 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
     if constexpr (FUSE) {
       if (kt + 1 < KT) issue_y(kt + 1, ynext);
     }
-    if (kt + NS - 1 < KT) issue(kt + NS - 1, (kt + NS - 1) % NS);
+    if (kt + NS - 1 < KT && UNET_ABL != 2) issue(kt + NS - 1, (kt + NS - 1) % NS);
     const char* As = smem + (kt % NS) * STAGE;
     const char* Bs = As + A_BYTES;
 #pragma unroll
-    for (int k2 = 0; k2 < (CO32 ? 2 : 4); ++k2) {
+    for (int k2 = 0; k2 < (UNET_ABL == 1 ? 0 : CO32 ? 2 : 4); ++k2) {
       const int kk = CO32 ? wm * 2 + k2 : k2;    // CO32: the wm pair splits the pixels
       const int p_lo = kk * 32 + 8 * g + trq;  // this lane's pixel (first tr read)
       bf16x8 af[2];
@@ -2213,6 +2213,13 @@ hipError_t launch_slab_reduce(const ReduceTail& r, hipStream_t st) {
   hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)r.blocks), dim3(256), 0, st,
                      reinterpret_cast<const f32x4*>(r.slab), r.dw, r.L, r.T);
   return hipGetLastError();
+}
+
+// drop any split-K reduction left queued by an earlier backward that ended
+// on an error (its slab / dW pointers belong to that plan's workspace)
+void wgrad_reset() {
+  g_pending = PendingReduce{};
+  g_deferred = PendingReduce{};
 }
 
 hipError_t launch_wgrad_flush(hipStream_t st) {

@@ -1451,6 +1451,7 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
                         float* grads, hipStream_t st) {
   Ctx x{p, ws, prm, nullptr, st, 1};
   const int N = p->cfg.N;
+  wgrad_reset();  // nothing queued by an earlier backward that failed midway
   if (p->want_events) RUN(ensure_events(p));
   if (p->two_stream && !p->wstream) {
     int least = 0, greatest = 0;

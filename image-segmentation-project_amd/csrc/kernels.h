@@ -205,6 +205,7 @@ bool wgrad_deferred();
 bool wgrad_deferred_reads(const void* slab);
 bool wgrad_take_deferred(ReduceTail* t);
 hipError_t launch_wgrad_flush(hipStream_t st);
+void wgrad_reset();  // clears the pending and deferred slots (start of every backward)
 hipError_t launch_slab_reduce(const ReduceTail& r, hipStream_t st);  // r on its own
 const char* last_kernel_tag();  // template instance of the last conv launch (profiler)
 
