@@ -316,8 +316,8 @@ __device__ __forceinline__ void load_epi_constants(const ConvFwdArgs& a, float* 
 // LDS at `scratch`), fp64 atomics into replica blockIdx.x % kStatRep, and the
 // optional last-block finalisation.
 template <int FN, int NW, bool TWO>
-__device__ __forceinline__ void commit_stats(const ConvFwdArgs& a, float (&q0)[FN][4], float (&q1)[FN][4],
-                                             float (&q2)[FN][4], int co0, char* scratch) {
+__device__ __forceinline__ void stats_atomics(const ConvFwdArgs& a, float (&q0)[FN][4], float (&q1)[FN][4],
+                                              float (&q2)[FN][4], int co0, char* scratch) {
   constexpr int COT = FN * 16;
   const BnBwdArgs& bb = a.bb;
   const bool fbwd = bb.sums != nullptr;
@@ -361,6 +361,15 @@ __device__ __forceinline__ void commit_stats(const ConvFwdArgs& a, float (&q0)[F
       if (TWO) atomicAdd(bb.sums2 + rep + a.Cout + co, (double)s2);
     }
   }
+}
+
+// the launch's last block (ticket) finalises the BN (forward or backward) whose
+// sums the blocks added (stats_atomics)
+template <int COT, int NW>
+__device__ __forceinline__ void stats_ticket(const ConvFwdArgs& a, char* scratch) {
+  const BnBwdArgs& bb = a.bb;
+  const bool fbwd = bb.sums != nullptr;
+  const int tid = threadIdx.x;
   unsigned* ticket = fbwd ? bb.ticket : a.bn.ticket;
   if (ticket) {
     int* flag = reinterpret_cast<int*>(scratch + NW * COT * 3 * sizeof(float));
@@ -369,6 +378,13 @@ __device__ __forceinline__ void commit_stats(const ConvFwdArgs& a, float (&q0)[F
       else bn_finalize(a.bn);
     }
   }
+}
+
+template <int FN, int NW, bool TWO>
+__device__ __forceinline__ void commit_stats(const ConvFwdArgs& a, float (&q0)[FN][4], float (&q1)[FN][4],
+                                             float (&q2)[FN][4], int co0, char* scratch) {
+  stats_atomics<FN, NW, TWO>(a, q0, q1, q2, co0, scratch);
+  stats_ticket<FN * 16, NW>(a, scratch);
 }
 
 // ---------------------------------------------------------------------------
@@ -533,11 +549,17 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
 }
 
 // ---------------------------------------------------------------------------
-// halo-streamed (C >= 128, multiple of 32): one TH x 16 x COT output tile per
-// block, K loop over 32-channel chunks, stage = halo panel + 9 weight taps
+// halo-streamed (C >= 128, multiple of 32): TH x 16 x COT output tiles, K
+// loop over 32-channel chunks, stage = halo panel + 9 weight taps.  A block
+// owns output-channel block cob and the tiles slot, slot + nslot, ... (grid =
+// ncb x nslot): when the grid is larger than the resident slots the blocks are
+// persistent, the first stage of the next tile is staged under the last
+// chunk's MFMAs and the BN sums of all its tiles are committed once (enc2 /
+// decoder3: 1024 tiles x co-blocks on 512 slots, formerly two rounds of
+// blocks, each paying its own prologue; profiles/r04/s1 conv_timing.txt)
 // ---------------------------------------------------------------------------
-template <int FN, int TH, int NW, bool FLIP, bool TWO>
-__global__ void __launch_bounds__(NW * 64) conv3x3_hs_kernel(ConvFwdArgs a, int ncb) {
+template <int FN, int TH, int NW, bool FLIP, bool TWO, bool MT>
+__global__ void __launch_bounds__(NW * 64) conv3x3_hs_kernel(ConvFwdArgs a, int ncb, int ntiles) {
   constexpr int COT = FN * 16;
   constexpr int RW = TH / NW;
   constexpr int HPR = ((TH + 2) * kHW + 15) / 16 * 16;
@@ -554,34 +576,41 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_hs_kernel(ConvFwdArgs a, int 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int cob = bid % ncb, tile = bid / ncb;
+  const int cob = bid % ncb, nslot = gridDim.x / ncb;
   const int co0 = cob * COT;
   const int tq = a.Q >> 4, tp = a.P / TH;
-  const int n = tile / (tp * tq);
-  const int rem = tile - n * (tp * tq);
-  const int oh0 = (rem / tq) * TH, ow0 = (rem % tq) << 4;
   const int KC = a.C >> 5;
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
   const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (unsigned)((size_t)a.Cout * 9 * a.C * 2));
+  int tile = bid / ncb;
 
-  // Per-lane DMA offsets of channel chunk 0, computed once: chunk kc only
-  // adds kc * 64 B, passed as the instruction's scalar offset (the address
+  // Per-lane DMA offsets of channel chunk 0 (per tile for the halo): chunk kc
+  // only adds kc * 64 B, passed as the instruction's scalar offset (the address
   // arithmetic would otherwise sit between the barrier and the MFMAs of every
   // stage, on both waves of a SIMD at once).
   constexpr int H_NINS = HPR / 16, H_PER = (H_NINS + NW - 1) / NW;
   constexpr int W_NINS = 9 * COT / 16, W_PER = (W_NINS + NW - 1) / NW;
   unsigned hoff[H_PER], woff[W_PER];
+  auto tile_origin = [&](int t, int& n, int& oh0, int& ow0) {
+    n = t / (tp * tq);
+    const int rem = t - n * (tp * tq);
+    oh0 = (rem / tq) * TH;
+    ow0 = (rem % tq) << 4;
+  };
+  auto set_hoff = [&](int t) {
+    int n, oh0, ow0;
+    tile_origin(t, n, oh0, ow0);
 #pragma unroll
-  for (int k = 0; k < H_PER; ++k) {
-    const int rowg = (wave + k * NW) * 16 + (lane >> 2);
-    const int hp = rowg;  // one panel per stage
-    const int lchunk = (lane & 3) ^ ((hp >> 1) & 2);
-    const int hr = hp / kHW, hc = hp - hr * kHW;
-    const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
-    hoff[k] = kOOB;
-    if (hp < (TH + 2) * kHW && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
-      hoff[k] = (unsigned)((((n * a.H + ih) * a.W + iw) * a.ldx + lchunk * 8) * 2);
-  }
+    for (int k = 0; k < H_PER; ++k) {
+      const int hp = (wave + k * NW) * 16 + (lane >> 2);  // one panel per stage
+      const int lchunk = (lane & 3) ^ ((hp >> 1) & 2);
+      const int hr = hp / kHW, hc = hp - hr * kHW;
+      const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
+      hoff[k] = kOOB;
+      if (hp < (TH + 2) * kHW && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+        hoff[k] = (unsigned)((((n * a.H + ih) * a.W + iw) * a.ldx + lchunk * 8) * 2);
+    }
+  };
 #pragma unroll
   for (int k = 0; k < W_PER; ++k) {
     const int rowg = (wave + k * NW) * 16 + (lane >> 2);
@@ -599,6 +628,7 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_hs_kernel(ConvFwdArgs a, int 
     for (int k = 0; k < W_PER; ++k)
       if (wave + k * NW < W_NINS) glds16s(wr, S + HBYTES + (wave + k * NW) * 1024, woff[k], so);
   };
+  set_hoff(tile);
   issue(0, 0);
   load_epi_constants<COT>(a, cst, co0, tid, NW * 64);
 
@@ -608,37 +638,59 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_hs_kernel(ConvFwdArgs a, int 
   for (int h = 0; h < RW + 2; ++h)
 #pragma unroll
     for (int d = 0; d < 3; ++d) boff[h][d] = ws_off((wave * RW + h) * kHW + d + (lane & 15), lane >> 4);
-  size_t pix[RW];
-#pragma unroll
-  for (int j = 0; j < RW; ++j) pix[j] = ((size_t)n * a.P + oh0 + wave * RW + j) * a.Q + ow0 + (lane & 15);
-
-  f32x4 acc[RW][FN];
-#pragma unroll
-  for (int j = 0; j < RW; ++j)
-#pragma unroll
-    for (int i = 0; i < FN; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  TileEpi<FN, RW, FLIP, PREF, TWO> epi;
   TSTAMP(a.tim, 1);
-  for (int kc = 0; kc < KC; ++kc) {
-    wait_vmcnt<0>();               // stage kc landed (this wave's part) ...
-    __builtin_amdgcn_s_barrier();  // ... everyone's; and stage kc-1 is no longer read
-    if (kc < 16) TSTAMP(a.tim, 2 + kc);
-    if (kc + 1 < KC && UNET_ABL != 2) issue(kc + 1, (kc + 1) & 1);
-    else if (PREF) epi.fetch(a, pix, co0, lane);  // epilogue operands ride beside the last chunk
-    const char* S = smem + (kc & 1) * STAGE;
-    if (UNET_ABL != 1) mfma_panel<FN, RW, COT * 64, FLIP>(acc, S + HBYTES, S, aoff, boff);
+  const bool stats = a.stats || a.bb.sums;
+  int stg = 0;  // stages so far: LDS buffer parity across tiles
+  for (;;) {
+    int n, oh0, ow0;
+    tile_origin(tile, n, oh0, ow0);
+    size_t pix[RW];
+#pragma unroll
+    for (int j = 0; j < RW; ++j) pix[j] = ((size_t)n * a.P + oh0 + wave * RW + j) * a.Q + ow0 + (lane & 15);
+    const int next = tile + nslot;
+    f32x4 acc[RW][FN];
+#pragma unroll
+    for (int j = 0; j < RW; ++j)
+#pragma unroll
+      for (int i = 0; i < FN; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    TileEpi<FN, RW, FLIP, PREF, TWO> epi;
+    for (int kc = 0; kc < KC; ++kc, ++stg) {
+      // stage kc landed (this wave's part) ...; at the first chunk of a later
+      // tile the previous tile's epilogue stores (at least RW * FN / 2 per wave,
+      // issued after this chunk's DMA) may stay in flight
+      if (MT && kc == 0 && stg > 0) wait_vmcnt<RW * FN / 2>();
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();  // ... everyone's; and stage kc-1 is no longer read
+      if (stg < 16) TSTAMP(a.tim, 2 + stg);
+      if (kc + 1 < KC) {
+        if (UNET_ABL != 2) issue(kc + 1, (stg + 1) & 1);
+      } else {
+        if (MT && next < ntiles) {  // the next tile's first chunk stages under this one's MFMAs
+          set_hoff(next);
+          issue(0, (stg + 1) & 1);
+        }
+        if (PREF) epi.fetch(a, pix, co0, lane);  // epilogue operands ride beside the last chunk
+      }
+      const char* S = smem + (stg & 1) * STAGE;
+      if (UNET_ABL != 1) mfma_panel<FN, RW, COT * 64, FLIP>(acc, S + HBYTES, S, aoff, boff);
+    }
+    TSTAMP(a.tim, 20);
+    if (!PREF) epi.fetch(a, pix, co0, lane);
+    epi.landed();
+    float q0[FN][4], q1[FN][4], q2[FN][4];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) q0[i][e] = q1[i][e] = q2[i][e] = 0.f;
+    epi.store(a, acc, pix, co0, lane, cst, q0, q1, q2);
+    TSTAMP(a.tim, 21);
+    // per tile: the buffer of the last chunk is free once every wave is past
+    // the barrier inside (the next tile's first chunk lands in the other one)
+    if (stats) stats_atomics<FN, NW, TWO>(a, q0, q1, q2, co0, smem + ((stg - 1) & 1) * STAGE);
+    tile = next;
+    if (!MT || tile >= ntiles) break;
   }
-  TSTAMP(a.tim, 20);
-  if (!PREF) epi.fetch(a, pix, co0, lane);
-  epi.landed();
-  float q0[FN][4], q1[FN][4], q2[FN][4];
-#pragma unroll
-  for (int i = 0; i < FN; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) q0[i][e] = q1[i][e] = q2[i][e] = 0.f;
-  epi.store(a, acc, pix, co0, lane, cst, q0, q1, q2);
-  TSTAMP(a.tim, 21);
-  if (a.stats || a.bb.sums) commit_stats<FN, NW, TWO>(a, q0, q1, q2, co0, smem);
+  if (stats) stats_ticket<COT, NW>(a, smem);
   TSTAMP(a.tim, 22);
   TSTAMP_RT(a.tim, 31);
 }
@@ -913,12 +965,27 @@ static hipError_t launch_hs(const ConvFwdArgs& a, hipStream_t st) {
   if (a.Cout % COT || a.P % TH) return hipErrorNotSupported;
   const int ncb = a.Cout / COT;
   const int ntiles = a.N * (a.P / TH) * (a.Q / 16);
+  // two 80 KB blocks per CU: past 512 blocks the grid stays at 512 and each
+  // block walks several tiles (UNET_HS_SLOTS overrides, 0 = one tile per block)
+  static const int slots_env = std::getenv("UNET_HS_SLOTS") ? std::atoi(std::getenv("UNET_HS_SLOTS")) : 512;
+  // (forward only: the multi-tile data gradient holds its fused BN-backward
+  // epilogue operands across tiles, 324 VGPRs, one block per CU)
+  long long grid = (long long)ntiles * ncb;
+  if (!FLIP && slots_env > 0 && grid > slots_env && slots_env % ncb == 0) grid = slots_env;
+  const bool mt = grid < (long long)ntiles * ncb;
   char tag[96];
-  std::snprintf(tag, sizeof(tag), "conv3x3_hs_kernel<%d, %d, %d, %s, %s>", FN, TH, NW, FLIP ? "true" : "false",
-                TWO ? "true" : "false");
+  std::snprintf(tag, sizeof(tag), "conv3x3_hs_kernel<%d, %d, %d, %s, %s, %s>", FN, TH, NW, FLIP ? "true" : "false",
+                TWO ? "true" : "false", mt ? "true" : "false");
   conv_kernel_tag(tag);
-  hipLaunchKernelGGL((conv3x3_hs_kernel<FN, TH, NW, FLIP, TWO>), dim3(ntiles * ncb), dim3(NW * 64), lds, st, a,
-                     ncb);
+  if constexpr (!FLIP) {
+    if (mt) {
+      hipLaunchKernelGGL((conv3x3_hs_kernel<FN, TH, NW, FLIP, TWO, true>), dim3((unsigned)grid), dim3(NW * 64), lds,
+                         st, a, ncb, ntiles);
+      return hipGetLastError();
+    }
+  }
+  hipLaunchKernelGGL((conv3x3_hs_kernel<FN, TH, NW, FLIP, TWO, false>), dim3((unsigned)grid), dim3(NW * 64), lds, st,
+                     a, ncb, ntiles);
   return hipGetLastError();
 }
 

@@ -1413,6 +1413,191 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// 3x3 / stride-1 weight gradient with dedicated LOADER waves (the C, Cout % 64
+// layers at Q % 32 == 0: enc1-3 and decoder2-4).  Same block geometry, split-K
+// slab and MFMA work as wgrad3x3_halo_kernel<32, 3, 64> (64 co x 64 ci x 9 taps
+// per block, 32 x 4 output-pixel tiles, 3 stages), restructured after the phase
+// ablation of that kernel (profiles/r04/s1): one stage took 4340 cycles with
+// every wave issuing its share of the LDS-DMA, 1800 for the DMA alone and 3250
+// for the MFMA work alone.  Here
+//  * 4 loader waves (one per SIMD) issue all of the LDS-DMA and wait for it;
+//    the 8 compute waves only read LDS and issue MFMAs (one barrier per stage);
+//  * the halo image rows sit at a pitch of 48 LDS rows (a multiple of 16, so the
+//    row swizzle of tr_off<64> does not change from one halo row to the next):
+//    every fragment read is a per-lane base register plus an immediate offset,
+//    no per-read address arithmetic;
+//  * fragments are read in halo-row order: the stage's 8 dY fragments first,
+//    then each of the 18 halo fragments once, feeding every tap it serves.
+// ---------------------------------------------------------------------------
+constexpr int kWlNW = 8;                  // compute waves: wave tile 32 co x 16 ci x 9 taps
+constexpr int kWlNL = 4;                  // loader waves
+constexpr int kWlNS = 3;                  // stages
+constexpr int kWlHP = 48;                 // LDS rows per halo image row (34 used)
+constexpr int kWlA = 128 * 128;           // dY tile: 128 px x 64 co, bf16
+constexpr int kWlB = 6 * kWlHP * 128;     // halo: 6 image rows x 48 x 64 ci, bf16
+constexpr int kWlStage = kWlA + kWlB;     // 53,248 B; 3 stages = 159,744 B of LDS
+constexpr int kWlHIns = 32;               // halo DMA instructions per stage (30 used + 2 zero-fill)
+constexpr int kWlLps = 16 / kWlNL + kWlHIns / kWlNL;  // LDS-DMA per loader wave per stage
+
+__global__ void __launch_bounds__((kWlNW + kWlNL) * 64)
+wgrad3x3_ld_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
+  constexpr int TW = 32, TH = 4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  typedef TrTile<64, 64, 128> TA;
+  TSTAMP_RT(a.tim, 30);
+  TSTAMP(a.tim, 0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int combos = a.co_blocks * a.c_blocks;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int combo = bid % combos, split = bid / combos;
+  const int cob = combo % a.co_blocks, cib = combo / a.co_blocks;
+  const int co0 = cob * 64, c0 = cib * 64;
+  const int t0 = split * tiles_per_split;
+  const int t1 = min(tiles_total, t0 + tiles_per_split);
+  const int KT = t1 - t0;
+  const int nsplit = gridDim.x / combos;
+  if (KT <= 0 && !(a.slab && nsplit > 1)) return;
+  const int tq = a.Q / TW, tp = a.P / TH;
+
+  if (wave >= kWlNW) {
+    // ---- loader wave lw: dY instructions 4 lw .. 4 lw + 3 of 16, halo
+    // instructions 8 lw .. 8 lw + 7 of 32 (image row idx / 5, 8-column block
+    // idx % 5; 30 and 31 zero-fill the never-read padding rows 40-47 of image
+    // rows 0 and 1, so every loader issues the same count) ----
+    constexpr int AI = 16 / kWlNL, HI = kWlHIns / kWlNL;
+    const int lw = wave - kWlNW;
+    const i32x4 dyr = make_rsrc_sgpr(a.dy, (unsigned)((size_t)a.N * a.P * a.Q * a.lddy * 2));
+    const i32x4 xr = make_rsrc_sgpr(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
+    const int lrow = lane >> 3, lslot = lane & 7;  // 8 rows of 128 B per instruction
+    unsigned arel[AI];
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+      const int row = (lw * AI + j) * 8 + lrow;  // pixel of the tile
+      const int f = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+      const int lchunk = (((lslot >> 1) ^ f) << 1) | (lslot & 1);
+      arel[j] = (unsigned)((((row / TW) * a.Q + row % TW) * a.lddy) + co0 + lchunk * 8) * 2u;
+    }
+    int hrr[HI], hcc[HI], hdst[HI];
+    unsigned hch[HI];
+#pragma unroll
+    for (int j = 0; j < HI; ++j) {
+      const int idx = lw * HI + j;
+      const bool pad = idx >= 30;
+      const int ir = pad ? idx - 30 : idx / 5;
+      const int col = (pad ? 40 : (idx % 5) * 8) + lrow;  // column in the halo image row
+      const int f = ((col >> 1) & 1) | (((col >> 3) & 1) << 1);  // = the swizzle of LDS row ir * 48 + col
+      const int lchunk = (((lslot >> 1) ^ f) << 1) | (lslot & 1);
+      hrr[j] = (!pad && col < TW + 2) ? ir - 1 : -(1 << 20);  // rows past the halo fail the bounds test
+      hcc[j] = col - 1;
+      hch[j] = (unsigned)(c0 + lchunk * 8);
+      hdst[j] = (ir * kWlHP + (pad ? 40 : (idx % 5) * 8)) * 128;
+    }
+    auto issue = [&](int kt, int buf) {
+      const int t = t0 + kt;
+      const int n = t / (tp * tq);
+      const int rem = t - n * (tp * tq);
+      const int oh0 = (rem / tq) * TH, ow0 = (rem % tq) * TW;
+      char* As = smem + buf * kWlStage;
+      char* Bs = As + kWlA;
+      const unsigned abase = (unsigned)(((n * a.P + oh0) * a.Q + ow0) * a.lddy) * 2u;
+#pragma unroll
+      for (int j = 0; j < AI; ++j) glds16_asm(dyr, As + (lw * AI + j) * 1024, arel[j], abase);
+#pragma unroll
+      for (int j = 0; j < HI; ++j) {
+        const int ih = oh0 + hrr[j], iw = ow0 + hcc[j];
+        const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        const unsigned off = (unsigned)((((n * a.H + ih) * a.W + iw) * a.ldx) + (int)hch[j]) * 2u;
+        glds16_asm(xr, Bs + hdst[j], ok ? off : kOOB, 0u);
+      }
+    };
+#pragma unroll
+    for (int s = 0; s < kWlNS - 1; ++s)
+      if (s < KT) issue(s, s);
+    for (int kt = 0; kt < KT; ++kt) {
+      // stage kt has landed when at most the younger stages are in flight
+      if (KT - 1 - kt >= kWlNS - 2) wait_vmcnt<(kWlNS - 2) * kWlLps>();
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();  // ... and every compute wave is done with stage kt - 1
+      if (kt + kWlNS - 1 < KT && UNET_ABL != 2) issue(kt + kWlNS - 1, (kt + kWlNS - 1) % kWlNS);
+    }
+    return;  // an exited wave no longer takes part in the compute waves' barriers
+  }
+
+  // ---- compute waves ----
+  const int wm = wave & 1, wn = wave >> 1;  // wave tile 32 co x 16 ci
+  const int g = lane >> 4, li = lane & 15, trq = li >> 2, trp = li & 3;
+  // per-lane fragment bases (LDS bytes): dY pixel 8g + trq (+4) of k-step 0 (a
+  // k-step adds 32 pixel rows = 4096 B), halo column 8g + trq + s (+4) of image
+  // row 0 (an image row adds 48 LDS rows = 6144 B)
+  int aoff[2][2], boff[3][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) aoff[i][h] = TA::off(8 * g + trq + 4 * h, wm * 32 + i * 16 + 4 * trp);
+#pragma unroll
+    for (int s = 0; s < 3; ++s) boff[s][h] = tr_off<64>(8 * g + trq + s + 4 * h, wn * 16 + 4 * trp);
+  }
+  f32x4 acc[9][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  TSTAMP(a.tim, 1);
+  for (int kt = 0; kt < KT; ++kt) {
+    __builtin_amdgcn_s_barrier();  // the loaders have waited for stage kt
+    if (kt < 16) TSTAMP(a.tim, 2 + kt);
+    const char* As = smem + (kt % kWlNS) * kWlStage;
+    const char* Bs = As + kWlA;
+    if (UNET_ABL == 1) continue;
+    bf16x8 af[4][2];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[kk][i] = tr_read8(As + aoff[i][0] + kk * 4096, As + aoff[i][1] + kk * 4096);
+#pragma unroll
+    for (int h = 0; h < 6; ++h) {  // halo image row h serves k-step kk at tap row r = h - kk
+      bf16x8 bfr[3];
+#pragma unroll
+      for (int s = 0; s < 3; ++s) bfr[s] = tr_read8(Bs + boff[s][0] + h * 6144, Bs + boff[s][1] + h * 6144);
+#pragma unroll
+      for (int kk = (h > 2 ? h - 2 : 0); kk <= (h < 3 ? h : 3); ++kk)
+#pragma unroll
+        for (int s = 0; s < 3; ++s)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+            acc[(h - kk) * 3 + s][i] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[s], acc[(h - kk) * 3 + s][i], 0, 0, 0);
+    }
+  }
+  TSTAMP(a.tim, 20);
+  if (a.slab && nsplit > 1) {  // this split's partial in the SLAB_HALO layout (18 fragments per wave)
+    const size_t units = (size_t)combos * kWlNW * 18 * 64;
+    f32x4* dst = reinterpret_cast<f32x4*>(a.slab) + (size_t)split * units + ((size_t)combo * kWlNW + wave) * (18 * 64) + lane;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) dst[(t * 2 + i) * 64] = acc[t][i];
+    TSTAMP(a.tim, 21);
+    TSTAMP_RT(a.tim, 31);
+    return;
+  }
+  const int Krow = 9 * a.C;
+  const int c = c0 + wn * 16 + li;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = co0 + wm * 32 + i * 16 + 4 * g + e;
+        if (co < a.Cout) {
+          float* d = a.dw + (size_t)co * Krow + t * a.C + c;
+          if (a.slab) *d = acc[t][i][e];
+          else atomicAdd(d, acc[t][i][e]);
+        }
+      }
+}
+
 // dW = sum over the splits of the slab (slab_reduce_block, common.h)
 __global__ void __launch_bounds__(256) wgrad_slab_reduce_kernel(const f32x4* __restrict__ slab,
                                                                 float* __restrict__ dw, SlabLayout L, int T) {
@@ -2157,6 +2342,34 @@ static hipError_t launch_wgrad_halo(const ConvWgradArgs& a0, hipStream_t st) {
   return hipGetLastError();
 }
 
+// wgrad3x3_ld_kernel: C % 64 == 0, Cout % 64 == 0, Q % 32 == 0, P % 4 == 0
+static hipError_t launch_wgrad_ld(const ConvWgradArgs& a0, hipStream_t st) {
+  ConvWgradArgs a = a0;
+  a.co_blocks = a.Cout / 64;
+  a.c_blocks = a.C / 64;
+  int blocks_xy, tiles, per, splits;
+  halo_geometry<32, 64, false>(a, blocks_xy, tiles, per, splits);
+  const long long units = (long long)blocks_xy * kWlNW * 18 * 64;
+  const long long cap = slab_split_cap(a, units * 16);
+  if (splits > cap) {
+    splits = (int)cap;
+    per = (tiles + splits - 1) / splits;
+    splits = (tiles + per - 1) / per;
+  }
+  constexpr size_t lds = (size_t)kWlNS * kWlStage;
+  static_assert(lds <= 163840, "LDS");
+  set_kernel_tag("wgrad3x3_ld_kernel");
+  hipLaunchKernelGGL(wgrad3x3_ld_kernel, dim3(blocks_xy * splits), dim3((kWlNW + kWlNL) * 64), lds, st, a, tiles, per);
+  if (a.slab && splits > 1) {
+    SlabLayout L = {};
+    L.kind = SLAB_HALO; L.splits = splits; L.blocks = blocks_xy; L.nw = kWlNW; L.nf = 18; L.units = units;
+    L.Cout = a.Cout; L.C = a.C; L.Krow = 9 * a.C; L.cmax = a.C;
+    L.co_blocks = a.co_blocks; L.c_blocks = a.c_blocks; L.ci = 64; L.co32 = 0;
+    g_pending = PendingReduce{a.slab, a.dw, L};
+  }
+  return hipGetLastError();
+}
+
 bool wgrad_pending() { return g_pending.slab != nullptr; }
 
 // split lanes per unit (each thread's loads, <= 8, all in flight at once; up to
@@ -2282,6 +2495,14 @@ hipError_t launch_conv_wgrad(const ConvWgradArgs& a0, int stem, hipStream_t st) 
       if (wcfg == 3) return launch_wgrad_halo<32, 32, false, 3>(a, st);
     }
     if (a.C % 64 == 0) {
+      // loader-wave kernel where blocks share their tiles (C or Cout >= 128:
+      // enc2-3, decoder2-4 first convs), the all-waves-issue kernel for the
+      // 64 x 64-channel layers (enc1, decoder2.3), where the loader form
+      // measured slower (profiles/r04/s1).  UNET_WG_LD=0: never, 1: always (A/B)
+      static const int ld = std::getenv("UNET_WG_LD") ? std::atoi(std::getenv("UNET_WG_LD")) : 2;
+      if (ld && (ld != 2 || a.C >= 128 || a.Cout >= 128) && a.Cout % 64 == 0 && a.Q % 32 == 0 && a.P % 4 == 0 &&
+          wcfg == 0)
+        return launch_wgrad_ld(a, st);
       if (a.Q % 32 == 0 && a.P % 4 == 0) return launch_wgrad_halo<32, 64>(a, st);
       if (a.Q % 16 == 0 && a.P % 8 == 0) return launch_wgrad_halo<16, 64>(a, st);
     }
