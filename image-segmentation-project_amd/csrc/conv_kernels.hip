@@ -1598,6 +1598,236 @@ wgrad3x3_ld_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
       }
 }
 
+// ---------------------------------------------------------------------------
+// Batched 3x3 / stride-1 weight gradients (WgBatchArgs, kernels.h): the
+// loader / compute structure of wgrad3x3_ld_kernel over a stream-K range of
+// (unit, tile) items spanning several layers.  Every block of the one launch
+// has the same number of stages; a unit (layer, 64 co x 64 ci block) that
+// ends inside the block's range is written out (dW directly when the whole unit
+// ran in this block, else a slab partial) and its accumulators restart for the
+// next unit.  Replaces one launch + one 37.7 MB split-K slab round trip per
+// layer (every halo wgrad launch wrote 256 blocks x 147 KB whatever the layer).
+// ---------------------------------------------------------------------------
+struct WbPos {  // (layer, unit of the layer, tile) of an item, advanced item by item
+  int l, combo, tile;
+  __device__ __forceinline__ void locate(const WgBatchArgs& a, long long it) {
+    l = 0;
+    while (l + 1 < a.nl && it >= a.L[l + 1].item0) ++l;
+    const long long r = it - a.L[l].item0;
+    combo = (int)(r / a.L[l].tiles);
+    tile = (int)(r - (long long)combo * a.L[l].tiles);
+  }
+  __device__ __forceinline__ void next(const WgBatchArgs& a) {
+    if (++tile == a.L[l].tiles) {
+      tile = 0;
+      if (++combo == a.L[l].co_blocks * a.L[l].c_blocks) {
+        combo = 0;
+        ++l;
+      }
+    }
+  }
+};
+__device__ __forceinline__ long long wb_begin(const WgBatchArgs& a, int b) { return (long long)b * a.items / a.grid; }
+
+__global__ void __launch_bounds__((kWlNW + kWlNL) * 64) wgrad3x3_batch_kernel(WgBatchArgs a) {
+  constexpr int TW = 32, TH = 4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  typedef TrTile<64, 64, 128> TA;
+  TSTAMP_RT(a.tim, 30);
+  TSTAMP(a.tim, 0);
+  const int b = blockIdx.x;
+  const long long i0 = wb_begin(a, b), i1 = wb_begin(a, b + 1);
+  const int KT = (int)(i1 - i0);
+  if (KT <= 0) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  if (wave >= kWlNW) {
+    // ---- loader wave lw (the instruction split of wgrad3x3_ld_kernel) ----
+    constexpr int AI = 16 / kWlNL, HI = kWlHIns / kWlNL;
+    const int lw = wave - kWlNW;
+    const int lrow = lane >> 3, lslot = lane & 7;
+    int arow[AI], alch[AI];
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+      const int row = (lw * AI + j) * 8 + lrow;  // pixel of the tile
+      const int f = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+      arow[j] = row;
+      alch[j] = (((lslot >> 1) ^ f) << 1) | (lslot & 1);
+    }
+    int hrr[HI], hcc[HI], hdst[HI], hlch[HI];
+#pragma unroll
+    for (int j = 0; j < HI; ++j) {
+      const int idx = lw * HI + j;
+      const bool pad = idx >= 30;
+      const int ir = pad ? idx - 30 : idx / 5;
+      const int col = (pad ? 40 : (idx % 5) * 8) + lrow;
+      const int f = ((col >> 1) & 1) | (((col >> 3) & 1) << 1);
+      hlch[j] = (((lslot >> 1) ^ f) << 1) | (lslot & 1);
+      hrr[j] = (!pad && col < TW + 2) ? ir - 1 : -(1 << 20);
+      hcc[j] = col - 1;
+      hdst[j] = (ir * kWlHP + (pad ? 40 : (idx % 5) * 8)) * 128;
+    }
+    WbPos pos;
+    pos.locate(a, i0);
+    auto issue = [&](int buf) {  // the stage of item `pos`, then advance
+      const int l = __builtin_amdgcn_readfirstlane(pos.l);
+      const WgBatchLayer& L = a.L[l];
+      const int combo = __builtin_amdgcn_readfirstlane(pos.combo), t = __builtin_amdgcn_readfirstlane(pos.tile);
+      const int co0 = (combo % L.co_blocks) * 64, c0 = (combo / L.co_blocks) * 64;
+      const int n = t / (L.tp * L.tq);
+      const int rem = t - n * (L.tp * L.tq);
+      const int oh0 = (rem / L.tq) * TH, ow0 = (rem % L.tq) * TW;
+      const i32x4 dyr = make_rsrc_sgpr(L.dy, (unsigned)((size_t)a.N * L.H * L.W * L.lddy * 2));
+      const i32x4 xr = make_rsrc_sgpr(L.x, (unsigned)((size_t)a.N * L.H * L.W * L.ldx * 2));
+      char* As = smem + buf * kWlStage;
+      char* Bs = As + kWlA;
+      const unsigned abase = (unsigned)(((n * L.H + oh0) * L.W + ow0) * L.lddy) * 2u;
+#pragma unroll
+      for (int j = 0; j < AI; ++j) {
+        const unsigned rel = (unsigned)((((arow[j] / TW) * L.W + arow[j] % TW) * L.lddy) + co0 + alch[j] * 8) * 2u;
+        glds16_asm(dyr, As + (lw * AI + j) * 1024, rel, abase);
+      }
+#pragma unroll
+      for (int j = 0; j < HI; ++j) {
+        const int ih = oh0 + hrr[j], iw = ow0 + hcc[j];
+        const bool ok = (unsigned)ih < (unsigned)L.H && (unsigned)iw < (unsigned)L.W;
+        const unsigned off = (unsigned)((((n * L.H + ih) * L.W + iw) * L.ldx) + c0 + hlch[j] * 8) * 2u;
+        glds16_asm(xr, Bs + hdst[j], ok ? off : kOOB, 0u);
+      }
+      pos.next(a);
+    };
+#pragma unroll
+    for (int s = 0; s < kWlNS - 1; ++s)
+      if (s < KT) issue(s);
+    for (int kt = 0; kt < KT; ++kt) {
+      if (KT - 1 - kt >= kWlNS - 2) wait_vmcnt<(kWlNS - 2) * kWlLps>();
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      if (kt + kWlNS - 1 < KT) issue((kt + kWlNS - 1) % kWlNS);
+    }
+    return;
+  }
+
+  // ---- compute waves ----
+  const int wm = wave & 1, wn = wave >> 1;
+  const int g = lane >> 4, li = lane & 15, trq = li >> 2, trp = li & 3;
+  int aoff[2][2], boff[3][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) aoff[i][h] = TA::off(8 * g + trq + 4 * h, wm * 32 + i * 16 + 4 * trp);
+#pragma unroll
+    for (int s = 0; s < 3; ++s) boff[s][h] = tr_off<64>(8 * g + trq + s + 4 * h, wn * 16 + 4 * trp);
+  }
+  WbPos pos;
+  pos.locate(a, i0);
+  const int ufirst = a.L[pos.l].unit0 + pos.combo;  // the block's first unit: its slab slot 0
+  f32x4 acc[9][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  TSTAMP(a.tim, 1);
+  for (int kt = 0; kt < KT; ++kt) {
+    __builtin_amdgcn_s_barrier();  // the loaders have waited for stage kt
+    if (kt < 16) TSTAMP(a.tim, 2 + kt);
+    const char* As = smem + (kt % kWlNS) * kWlStage;
+    const char* Bs = As + kWlA;
+    if (UNET_ABL != 1) {
+      bf16x8 af[4][2];
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[kk][i] = tr_read8(As + aoff[i][0] + kk * 4096, As + aoff[i][1] + kk * 4096);
+#pragma unroll
+      for (int h = 0; h < 6; ++h) {
+        bf16x8 bfr[3];
+#pragma unroll
+        for (int s = 0; s < 3; ++s) bfr[s] = tr_read8(Bs + boff[s][0] + h * 6144, Bs + boff[s][1] + h * 6144);
+#pragma unroll
+        for (int kk = (h > 2 ? h - 2 : 0); kk <= (h < 3 ? h : 3); ++kk)
+#pragma unroll
+          for (int s = 0; s < 3; ++s)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+              acc[(h - kk) * 3 + s][i] =
+                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[s], acc[(h - kk) * 3 + s][i], 0, 0, 0);
+      }
+    }
+    const int l = __builtin_amdgcn_readfirstlane(pos.l);
+    const WgBatchLayer& L = a.L[l];
+    if (pos.tile == L.tiles - 1 || kt == KT - 1) {  // the unit's last item in this block
+      const int combo = __builtin_amdgcn_readfirstlane(pos.combo);
+      const long long S = L.item0 + (long long)combo * L.tiles;
+      if (S >= i0 && S + L.tiles <= i1) {  // the whole unit ran here: dW directly
+        const int co0 = (combo % L.co_blocks) * 64, c0 = (combo / L.co_blocks) * 64;
+        const int Krow = 9 * L.C;
+        const int c = c0 + wn * 16 + li;
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              L.dw[(size_t)(co0 + wm * 32 + i * 16 + 4 * g + e) * Krow + t * L.C + c] = acc[t][i][e];
+      } else {  // a partial: slot b * maxseg + the unit's rank in this block
+        const int slot = b * a.maxseg + (L.unit0 + combo - ufirst);
+        f32x4* dst = reinterpret_cast<f32x4*>(a.slab) + (size_t)slot * (kWlNW * 18 * 64) + wave * (18 * 64) + lane;
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+          for (int i = 0; i < 2; ++i) dst[(t * 2 + i) * 64] = acc[t][i];
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    pos.next(a);
+  }
+  TSTAMP(a.tim, 20);
+  TSTAMP_RT(a.tim, 31);
+}
+
+// the block whose item range holds item it
+__device__ __forceinline__ int wb_block_of(const WgBatchArgs& a, long long it) {
+  int b = (int)((it * a.grid) / a.items);
+  while (b + 1 < a.grid && wb_begin(a, b + 1) <= it) ++b;
+  while (b > 0 && wb_begin(a, b) > it) --b;
+  return b;
+}
+
+// dW of every unit spread over several blocks = the sum of its partials in
+// block order; grid (units, 36): 256 threads x one f32x4 element of the unit's
+// 9216-element (8 waves x 18 fragments x 64 lanes) SLAB_HALO partial each
+__global__ void __launch_bounds__(256) wgrad_batch_reduce_kernel(WgBatchArgs a) {
+  const int u = blockIdx.x;
+  int l = 0;
+  while (l + 1 < a.nl && u >= a.L[l + 1].unit0) ++l;
+  const WgBatchLayer& L = a.L[l];
+  const int combo = u - L.unit0;
+  const long long S = L.item0 + (long long)combo * L.tiles;
+  const int b0 = wb_block_of(a, S), b1 = wb_block_of(a, S + L.tiles - 1);
+  if (b0 == b1) return;  // written directly by its block
+  const int q = blockIdx.y * 256 + threadIdx.x;
+  const f32x4* slab = reinterpret_cast<const f32x4*>(a.slab);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int b = b0; b <= b1; ++b) {
+    const long long ib = wb_begin(a, b);
+    if (wb_begin(a, b + 1) == ib) continue;  // an empty range (batches of fewer items than blocks)
+    WbPos p;
+    p.locate(a, ib);
+    const int slot = b * a.maxseg + (u - (a.L[p.l].unit0 + p.combo));
+    acc += slab[(size_t)slot * (kWlNW * 18 * 64) + q];
+  }
+  const int lane = q & 63, r = q >> 6;
+  const int frag = r % 18, wave = r / 18;
+  const int t = frag >> 1, i = frag & 1, wm = wave & 1, wn = wave >> 1;
+  const int g = lane >> 4, li = lane & 15;
+  const int co0 = (combo % L.co_blocks) * 64, c0 = (combo / L.co_blocks) * 64;
+  const int Krow = 9 * L.C;
+  const int c = c0 + wn * 16 + li;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) L.dw[(size_t)(co0 + wm * 32 + i * 16 + 4 * g + e) * Krow + t * L.C + c] = acc[e];
+}
+
 // dW = sum over the splits of the slab (slab_reduce_block, common.h)
 __global__ void __launch_bounds__(256) wgrad_slab_reduce_kernel(const f32x4* __restrict__ slab,
                                                                 float* __restrict__ dw, SlabLayout L, int T) {
@@ -2367,6 +2597,51 @@ static hipError_t launch_wgrad_ld(const ConvWgradArgs& a0, hipStream_t st) {
     L.co_blocks = a.co_blocks; L.c_blocks = a.c_blocks; L.ci = 64; L.co32 = 0;
     g_pending = PendingReduce{a.slab, a.dw, L};
   }
+  return hipGetLastError();
+}
+
+bool wgrad_batch_ok(const ConvWgradArgs& a) {
+  return a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.C % 64 == 0 && a.Cout % 64 == 0 && a.P == a.H &&
+         a.Q == a.W && a.Q % 32 == 0 && a.P % 4 == 0 && !a.dy2 && !a.bn_fuse && a.lddy % 8 == 0 &&
+         a.ldx % 8 == 0 && (size_t)a.N * a.H * a.W * a.ldx * 2 < 0x80000000ull &&
+         (size_t)a.N * a.P * a.Q * a.lddy * 2 < 0x80000000ull;
+}
+
+int wgrad_batch_grid() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
+// largest number of units any block of the batch touches (its slab slots)
+int wgrad_batch_maxseg(const WgBatchArgs& a) {
+  auto unit_of = [&](long long it) {
+    int l = 0;
+    while (l + 1 < a.nl && it >= a.L[l + 1].item0) ++l;
+    return a.L[l].unit0 + (int)((it - a.L[l].item0) / a.L[l].tiles);
+  };
+  int m = 1;
+  for (int b = 0; b < a.grid; ++b) {
+    const long long i0 = (long long)b * a.items / a.grid, i1 = (long long)(b + 1) * a.items / a.grid;
+    if (i1 > i0) m = std::max(m, unit_of(i1 - 1) - unit_of(i0) + 1);
+  }
+  return m;
+}
+
+hipError_t launch_wgrad_batch(const WgBatchArgs& a, hipStream_t st) {
+  constexpr size_t lds = (size_t)kWlNS * kWlStage;
+  set_kernel_tag("wgrad3x3_batch_kernel");
+  hipLaunchKernelGGL(wgrad3x3_batch_kernel, dim3(a.grid), dim3((kWlNW + kWlNL) * 64), lds, st, a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  set_kernel_tag("wgrad_batch_reduce_kernel");
+  hipLaunchKernelGGL(wgrad_batch_reduce_kernel, dim3(a.units, (unsigned)(kWbPartBytes / 16 / 256)), dim3(256), 0, st,
+                     a);
   return hipGetLastError();
 }
 

@@ -207,6 +207,13 @@ struct unet_plan {
   // weight gradient (wgrad_bn_fuse_ok).  Off unless UNET_WG_BN=1: measured
   // slower than the separate apply pass
   bool wg_bn_fuse = std::getenv("UNET_WG_BN") != nullptr;
+  // 3x3 / s1 weight gradients of a gradient bucket collected and run as ONE
+  // batched stream-K launch at the bucket boundary (wgrad3x3_batch_kernel):
+  // no per-layer split-K slab round trip.  UNET_WG_BATCH=0: one launch per layer (A/B)
+  bool wg_batch = !(std::getenv("UNET_WG_BATCH") && std::atoi(std::getenv("UNET_WG_BATCH")) == 0);
+  std::vector<ConvWgradArgs> wgb;  // collected weight gradients of the current bucket
+  std::vector<std::string> wgb_names;
+  double wgb_flops = 0;
   double flops_fwd = 0, flops_train = 0;
   // fp8 forward (cfg.fp8): per-tensor delayed-amax states (fp8.hip) for the
   // conv weights and activations; the first forward calibrates
@@ -1040,7 +1047,77 @@ int conv_wgrad(const Ctx& x, int ci, const Act& dy, const Act& in, int ds = -1, 
     fl += conv_flops(x.p, dv, *dyds);
     name += " +ds";
   }
+  if (x.p->wg_batch && wgrad_batch_ok(a)) {  // runs in the bucket's batch (flush_wgrad_batch)
+    x.p->wgb.push_back(a);
+    x.p->wgb_names.push_back(name);
+    x.p->wgb_flops += fl;
+    return 0;
+  }
   return wgrad_and_reduce(x, a, 0, name, fl);
+}
+
+int flush_reduce(const Ctx& x);
+
+// the collected weight gradients (conv_wgrad) as batched launches of at most
+// kWbMaxLayers layers whose partials fit the halo slab (the per-layer
+// reductions that read it have run: flush_reduce first)
+int flush_wgrad_batch(const Ctx& x) {
+  unet_plan* p = x.p;
+  if (p->wgb.empty()) return 0;
+  RUN(flush_reduce(x));
+  const int grid = wgrad_batch_grid();
+  const size_t cap = 2 * p->wslab_bytes / kWbPartBytes;  // slab slots
+  size_t first = 0;
+  while (first < p->wgb.size()) {
+    // as many layers as the table and the slab hold
+    size_t n = std::min(p->wgb.size() - first, (size_t)kWbMaxLayers);
+    WgBatchArgs b;
+    for (;;) {
+      b = WgBatchArgs{};
+      b.grid = grid;
+      b.N = p->cfg.N;
+      long long items = 0;
+      int units = 0;
+      for (size_t j = 0; j < n; ++j) {
+        const ConvWgradArgs& a = p->wgb[first + j];
+        WgBatchLayer& L = b.L[j];
+        L.dy = a.dy; L.x = a.x; L.dw = a.dw;
+        L.H = a.H; L.W = a.W; L.C = a.C; L.Cout = a.Cout; L.lddy = a.lddy; L.ldx = a.ldx;
+        L.tq = a.Q / 32; L.tp = a.P / 4;
+        L.co_blocks = a.Cout / 64; L.c_blocks = a.C / 64;
+        L.tiles = a.N * L.tp * L.tq;
+        L.unit0 = units; L.item0 = items;
+        units += L.co_blocks * L.c_blocks;
+        items += (long long)L.co_blocks * L.c_blocks * L.tiles;
+      }
+      b.nl = (int)n; b.units = units; b.items = items;
+      b.maxseg = wgrad_batch_maxseg(b);
+      if ((size_t)grid * b.maxseg <= cap || n == 1) break;
+      n = (n + 1) / 2;
+    }
+    if ((size_t)grid * b.maxseg > cap) {
+      set_err("weight-gradient batch: slab too small");
+      return -1;
+    }
+    b.slab = x.W<float>(p->wslab);
+    std::string nm = "wgrad batch";
+    for (size_t j = 0; j < n; ++j) nm += (j ? "," : " ") + p->wgb_names[first + j];
+    b.tim = tim_slot(p, "wgrad batch x" + std::to_string(n));
+    double fl = 0;
+    for (size_t j = 0; j < n; ++j) {
+      const ConvWgradArgs& a = p->wgb[first + j];
+      fl += 2.0 * a.N * a.P * a.Q * a.Cout * a.C * 9;
+    }
+    {
+      ProfScope ps(p, x.wst, nm, fl);
+      CK(launch_wgrad_batch(b, x.wst));
+    }
+    first += n;
+  }
+  p->wgb.clear();
+  p->wgb_names.clear();
+  p->wgb_flops = 0;
+  return 0;
 }
 
 // The BN-backward apply f (dY = f.dy from dZ = f.da and y) can ride in the
@@ -1154,6 +1231,7 @@ int flush_reduce(const Ctx& x) {
 }
 
 int unpack_bucket(const Ctx& x, int bk, float* grads) {
+  RUN(flush_wgrad_batch(x));
   RUN(flush_reduce(x));
   if (x.rst != x.wst) RUN(stream_edge(x.p, x.rst, x.wst));  // every reduction so far is in dW
   ProfScope ps(x.p, x.wst, "unpack", 0);
@@ -1452,6 +1530,9 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
   Ctx x{p, ws, prm, nullptr, st, 1};
   const int N = p->cfg.N;
   wgrad_reset();  // nothing queued by an earlier backward that failed midway
+  p->wgb.clear();
+  p->wgb_names.clear();
+  p->wgb_flops = 0;
   if (p->want_events) RUN(ensure_events(p));
   if (p->two_stream && !p->wstream) {
     int least = 0, greatest = 0;

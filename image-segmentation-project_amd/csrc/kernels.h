@@ -207,6 +207,35 @@ bool wgrad_take_deferred(ReduceTail* t);
 hipError_t launch_wgrad_flush(hipStream_t st);
 void wgrad_reset();  // clears the pending and deferred slots (start of every backward)
 hipError_t launch_slab_reduce(const ReduceTail& r, hipStream_t st);  // r on its own
+
+// Batched 3x3 / stride-1 weight gradients (wgrad3x3_batch_kernel): the weight
+// gradients of several layers (wgrad_batch_ok) in ONE stream-K launch.  Layer l
+// has co_blocks x c_blocks units of 64 x 64 channels, each a K loop over `tiles`
+// 32 x 4 output-pixel tiles; the units' items (unit, tile) are numbered layer by
+// layer, unit by unit, and block b of the grid runs items [b I / G, (b+1) I / G).
+// A unit inside one block is written to dW directly; a unit spread over blocks
+// b0..b1 leaves one partial per block in the slab (slot b * maxseg + the unit's
+// rank among block b's units), summed in block order by the reduce (fixed order:
+// bit-reproducible).
+constexpr int kWbMaxLayers = 16;
+struct WgBatchLayer {
+  const bf16_t* dy; const bf16_t* x; float* dw;
+  int H, W, C, Cout, lddy, ldx, tq, tp, co_blocks, c_blocks, tiles, unit0;
+  long long item0;
+};
+struct WgBatchArgs {
+  WgBatchLayer L[kWbMaxLayers];
+  int nl, grid, maxseg, units, N;
+  long long items;
+  float* slab;               // grid * maxseg partials of 147,456 B
+  unsigned long long* tim;   // phase stamps (debug build only)
+};
+bool wgrad_batch_ok(const ConvWgradArgs& a);
+constexpr size_t kWbPartBytes = 8 * 18 * 64 * 16;  // one block's 64 x 64 x 9 fp32 partial (SLAB_HALO layout)
+// the grid of a batch (one block per CU) and the largest slab slot count it needs
+int wgrad_batch_grid();
+int wgrad_batch_maxseg(const WgBatchArgs& a);
+hipError_t launch_wgrad_batch(const WgBatchArgs& a, hipStream_t st);
 const char* last_kernel_tag();  // template instance of the last conv launch (profiler)
 
 // ---- elementwise / reduction kernels (elementwise.hip) ----

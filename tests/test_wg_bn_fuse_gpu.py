@@ -35,6 +35,9 @@ def test_wgrad_bn_fuse_bit_identical(pkg, cuda, monkeypatch, att):
           for k, v in pkg.UNetWithBackbone(pretrained=False, use_attention=att).state_dict().items()}
     xs, ms = pkg.synthetic_cells(2, 256, 256, seed=23)
     x, y = torch.from_numpy(xs).cuda(), torch.from_numpy(ms).cuda()
+    # both runs on the per-layer weight-gradient kernels (the fused apply is
+    # one of them; the default batched launch sums split partials differently)
+    monkeypatch.setenv("UNET_WG_BATCH", "0")
     monkeypatch.setenv("UNET_WG_BN", "1")  # read when the native plan is created
     fused = _run(pkg, sd, x, y, att)
     monkeypatch.delenv("UNET_WG_BN")
