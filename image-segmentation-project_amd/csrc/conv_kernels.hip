@@ -1629,8 +1629,58 @@ struct WbPos {  // (layer, unit of the layer, tile) of an item, advanced item by
 };
 __device__ __forceinline__ long long wb_begin(const WgBatchArgs& a, int b) { return (long long)b * a.items / a.grid; }
 
+// the loaders' position, with the current layer's fields and the tile origin
+// kept incrementally (no per-stage divisions or kernel-argument loads)
+struct WbLoad {
+  int l, tile, cob, cib, n, oh0, ow0;
+  const bf16_t* dy;
+  const bf16_t* x;
+  int H, W, lddy, ldx, co_blocks, c_blocks, tiles;
+  __device__ __forceinline__ void layer(const WgBatchArgs& a) {
+    const WgBatchLayer& L = a.L[l];
+    dy = L.dy; x = L.x;
+    H = L.H; W = L.W; lddy = L.lddy; ldx = L.ldx;
+    co_blocks = L.co_blocks; c_blocks = L.c_blocks; tiles = L.tiles;
+  }
+  __device__ __forceinline__ void locate(const WgBatchArgs& a, long long it) {
+    WbPos p;
+    p.locate(a, it);
+    l = p.l;
+    layer(a);
+    tile = p.tile;
+    cob = p.combo % co_blocks;
+    cib = p.combo / co_blocks;
+    const int tq = W / 32, tp = H / 4;
+    n = tile / (tp * tq);
+    const int rem = tile - n * (tp * tq);
+    oh0 = (rem / tq) * 4;
+    ow0 = (rem % tq) * 32;
+  }
+  __device__ __forceinline__ void next(const WgBatchArgs& a) {
+    ow0 += 32;
+    if (ow0 == W) {
+      ow0 = 0;
+      oh0 += 4;
+      if (oh0 == H) {
+        oh0 = 0;
+        ++n;
+      }
+    }
+    if (++tile == tiles) {
+      tile = n = oh0 = ow0 = 0;
+      if (++cob == co_blocks) {
+        cob = 0;
+        if (++cib == c_blocks) {
+          cib = 0;
+          if (++l < a.nl) layer(a);
+        }
+      }
+    }
+  }
+};
+
 __global__ void __launch_bounds__((kWlNW + kWlNL) * 64) wgrad3x3_batch_kernel(WgBatchArgs a) {
-  constexpr int TW = 32, TH = 4;
+  constexpr int TW = 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   typedef TrTile<64, 64, 128> TA;
   TSTAMP_RT(a.tim, 30);
@@ -1668,31 +1718,27 @@ __global__ void __launch_bounds__((kWlNW + kWlNL) * 64) wgrad3x3_batch_kernel(Wg
       hcc[j] = col - 1;
       hdst[j] = (ir * kWlHP + (pad ? 40 : (idx % 5) * 8)) * 128;
     }
-    WbPos pos;
+    WbLoad pos;
     pos.locate(a, i0);
     auto issue = [&](int buf) {  // the stage of item `pos`, then advance
-      const int l = __builtin_amdgcn_readfirstlane(pos.l);
-      const WgBatchLayer& L = a.L[l];
-      const int combo = __builtin_amdgcn_readfirstlane(pos.combo), t = __builtin_amdgcn_readfirstlane(pos.tile);
-      const int co0 = (combo % L.co_blocks) * 64, c0 = (combo / L.co_blocks) * 64;
-      const int n = t / (L.tp * L.tq);
-      const int rem = t - n * (L.tp * L.tq);
-      const int oh0 = (rem / L.tq) * TH, ow0 = (rem % L.tq) * TW;
-      const i32x4 dyr = make_rsrc_sgpr(L.dy, (unsigned)((size_t)a.N * L.H * L.W * L.lddy * 2));
-      const i32x4 xr = make_rsrc_sgpr(L.x, (unsigned)((size_t)a.N * L.H * L.W * L.ldx * 2));
+      const int H = pos.H, W = pos.W, lddy = pos.lddy, ldx = pos.ldx;
+      const int n = pos.n, oh0 = pos.oh0, ow0 = pos.ow0;
+      const int co0 = pos.cob * 64, c0 = pos.cib * 64;
+      const i32x4 dyr = make_rsrc_sgpr(pos.dy, (unsigned)((size_t)a.N * H * W * lddy * 2));
+      const i32x4 xr = make_rsrc_sgpr(pos.x, (unsigned)((size_t)a.N * H * W * ldx * 2));
       char* As = smem + buf * kWlStage;
       char* Bs = As + kWlA;
-      const unsigned abase = (unsigned)(((n * L.H + oh0) * L.W + ow0) * L.lddy) * 2u;
+      const unsigned abase = (unsigned)(((n * H + oh0) * W + ow0) * lddy) * 2u;
 #pragma unroll
       for (int j = 0; j < AI; ++j) {
-        const unsigned rel = (unsigned)((((arow[j] / TW) * L.W + arow[j] % TW) * L.lddy) + co0 + alch[j] * 8) * 2u;
+        const unsigned rel = (unsigned)((((arow[j] / TW) * W + arow[j] % TW) * lddy) + co0 + alch[j] * 8) * 2u;
         glds16_asm(dyr, As + (lw * AI + j) * 1024, rel, abase);
       }
 #pragma unroll
       for (int j = 0; j < HI; ++j) {
         const int ih = oh0 + hrr[j], iw = ow0 + hcc[j];
-        const bool ok = (unsigned)ih < (unsigned)L.H && (unsigned)iw < (unsigned)L.W;
-        const unsigned off = (unsigned)((((n * L.H + ih) * L.W + iw) * L.ldx) + c0 + hlch[j] * 8) * 2u;
+        const bool ok = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+        const unsigned off = (unsigned)((((n * H + ih) * W + iw) * ldx) + c0 + hlch[j] * 8) * 2u;
         glds16_asm(xr, Bs + hdst[j], ok ? off : kOOB, 0u);
       }
       pos.next(a);
@@ -1704,7 +1750,7 @@ __global__ void __launch_bounds__((kWlNW + kWlNL) * 64) wgrad3x3_batch_kernel(Wg
       if (KT - 1 - kt >= kWlNS - 2) wait_vmcnt<(kWlNS - 2) * kWlLps>();
       else wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
-      if (kt + kWlNS - 1 < KT) issue((kt + kWlNS - 1) % kWlNS);
+      if (kt + kWlNS - 1 < KT && UNET_ABL != 2) issue((kt + kWlNS - 1) % kWlNS);
     }
     return;
   }
@@ -1723,6 +1769,8 @@ __global__ void __launch_bounds__((kWlNW + kWlNL) * 64) wgrad3x3_batch_kernel(Wg
   WbPos pos;
   pos.locate(a, i0);
   const int ufirst = a.L[pos.l].unit0 + pos.combo;  // the block's first unit: its slab slot 0
+  // the current layer's unit length and count, reloaded only when the layer changes
+  int tiles = a.L[pos.l].tiles, ncombo = a.L[pos.l].co_blocks * a.L[pos.l].c_blocks;
   f32x4 acc[9][2];
 #pragma unroll
   for (int t = 0; t < 9; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1753,9 +1801,9 @@ __global__ void __launch_bounds__((kWlNW + kWlNL) * 64) wgrad3x3_batch_kernel(Wg
                   __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[s], acc[(h - kk) * 3 + s][i], 0, 0, 0);
       }
     }
-    const int l = __builtin_amdgcn_readfirstlane(pos.l);
-    const WgBatchLayer& L = a.L[l];
-    if (pos.tile == L.tiles - 1 || kt == KT - 1) {  // the unit's last item in this block
+    if (pos.tile == tiles - 1 || kt == KT - 1) {  // the unit's last item in this block
+      const int l = __builtin_amdgcn_readfirstlane(pos.l);
+      const WgBatchLayer& L = a.L[l];
       const int combo = __builtin_amdgcn_readfirstlane(pos.combo);
       const long long S = L.item0 + (long long)combo * L.tiles;
       if (S >= i0 && S + L.tiles <= i1) {  // the whole unit ran here: dW directly
@@ -1780,7 +1828,16 @@ __global__ void __launch_bounds__((kWlNW + kWlNL) * 64) wgrad3x3_batch_kernel(Wg
 #pragma unroll
       for (int t = 0; t < 9; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    pos.next(a);
+    if (++pos.tile == tiles) {  // WbPos::next with the layer fields cached
+      pos.tile = 0;
+      if (++pos.combo == ncombo) {
+        pos.combo = 0;
+        if (++pos.l < a.nl) {
+          tiles = a.L[pos.l].tiles;
+          ncombo = a.L[pos.l].co_blocks * a.L[pos.l].c_blocks;
+        }
+      }
+    }
   }
   TSTAMP(a.tim, 20);
   TSTAMP_RT(a.tim, 31);

@@ -155,7 +155,7 @@ def test_ddp_two_gpus_equal_chunk_mean(pkg):
         assert max(errs) <= 1e-5 and same, (rank, errs, same)
 
 
-def _shared_gpu_worker(rank, world, port, q):
+def _shared_gpu_worker(rank, world, port, q, width=1, fp8=False):
     """One rank of a world-2 group whose two processes share cuda:0 (gloo on
     CUDA tensors: RCCL refuses two ranks on one device).  Everything the
     multi-GPU path runs runs here: the native backward records its per-bucket
@@ -177,9 +177,9 @@ def _shared_gpu_worker(rank, world, port, q):
         xs, ms = pkg.synthetic_cells(2 * world, 128, 128, seed=8)
         x, y = torch.from_numpy(xs).to(dev), torch.from_numpy(ms).to(dev)
         crit = pkg.get_loss_function({"loss_fn": "bce"})
-        ref = oracle.ReferenceUNet()
+        ref = oracle.ReferenceUNet(width=width)
         sd = oracle.closed_form_state_dict(ref, seed=2)
-        m = pkg.UNetWithBackbone(pretrained=False, use_attention=False).to(dev).train()
+        m = pkg.UNetWithBackbone(pretrained=False, use_attention=False, width=width, fp8=fp8).to(dev).train()
         with torch.no_grad():  # rank 1 starts from other weights: the broadcast must fix them
             for p in m.parameters():
                 p.mul_(0.5 if rank else 1.0)
@@ -246,7 +246,8 @@ def _shared_gpu_worker(rank, world, port, q):
         q.put((rank, [1.0], [False], {}, False, repr(e) + traceback.format_exc()))
 
 
-def test_ddp_two_ranks_share_one_gpu(pkg):
+@pytest.mark.parametrize("width,fp8", [(1, False), (2, True)], ids=["base", "wide_fp8"])
+def test_ddp_two_ranks_share_one_gpu(pkg, width, fp8):
     """two processes, both on cuda:0 (gloo over CUDA
     tensors), each running the native backward on its half of the batch with
     enable_data_parallel and the per-bucket events on.  Every rank's reduced
@@ -254,11 +255,18 @@ def test_ddp_two_ranks_share_one_gpu(pkg):
     L2 <= 1e-6; exact in practice: the backward is bit-reproducible and a sum
     of two fp32 values halved is exact), the head gradients match the fp32
     oracle's chunk mean at the end-to-end head bar of test_model_gpu (0.1),
-    and the parameters are identical on both ranks after the fused Adam step."""
+    and the parameters are identical on both ranks after the fused Adam step.
+    wide_fp8: the same multi-process path for BASELINE
+    configs[4] (width 2, fp8 forward).  Its delayed-amax scales evolve with
+    every forward, so the single-process reference (two chunk forwards in one
+    process) quantizes with other scales than the ranks: there the bar is
+    relative L2 <= 0.1 (fp8 e4m3 carries 3 mantissa bits; measured value
+    printed), the head bar 0.2, and the replicas must still be bit-identical
+    after Adam."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_shared_gpu_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_shared_gpu_worker, args=(r, 2, port, q, width, fp8)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in procs], key=lambda r: r[0])
@@ -268,8 +276,8 @@ def test_ddp_two_ranks_share_one_gpu(pkg):
         print(f"rank {rank}: reduced vs single-process mean {errs} exact {exact}; head vs oracle {head}; "
               f"params equal after Adam {same}")
         assert not msg, msg
-        assert max(errs) <= 1e-6 and same, (rank, errs, same)
-        assert head and max(head.values()) <= 0.1, head
+        assert max(errs) <= (0.1 if fp8 else 1e-6) and same, (rank, errs, same)
+        assert head and max(head.values()) <= (0.2 if fp8 else 0.1), head
 
 
 def test_grad_bf16_pack_kernels(pkg, cuda):

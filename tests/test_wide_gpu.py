@@ -3,8 +3,9 @@ on the HIP path, checked against the oracle (``ReferenceUNet(width=2)``, the
 reference topology of advanced_models.py:72-100,157-160 with doubled channels)
 on the same seeded inputs and closed-form weights.
 
-The HIP path computes in bf16 (the configs[4] fp8 MFMA variant is not built;
-DESIGN.md). Tolerances are the end-to-end ones of test_model_gpu.py:
+The HIP path computes in bf16 here (the configs[4] fp8 forward, ``fp8=True``,
+is checked by test_fp8_gpu.py and, at its 16 x 512^2 workload, by
+test_wide_fp8_full_gpu.py). Tolerances are the end-to-end ones of test_model_gpu.py:
   train logits ||d||/||ref|| <= 0.10; masks agree on >= 95 % of pixels and are
   bit-exact where |logit_ref| > 1; BCE loss relative 1e-3; every gradient
   finite; head gradients within relative L2 0.10.  Every other op and gradient
