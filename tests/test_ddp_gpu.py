@@ -190,6 +190,14 @@ def _shared_gpu_worker(rank, world, port, q, width=1, fp8=False):
         per = x.shape[0] // world
         mine = slice(rank * per, (rank + 1) * per)
         errs, exact = [], []
+        if fp8:
+            # delayed-amax scales: after a few forwards of the same chunk and
+            # weights they stop moving, so the DDP and the local step below
+            # quantize alike (per-rank scales, as in training)
+            with torch.no_grad():
+                for _ in range(3):
+                    m.load_state_dict(sd)
+                    m(x[mine])
         for step in range(3):  # first DDP backward (no bucket events yet), then event-ordered buckets
             m.load_state_dict(sd)
             for p in m.parameters():
@@ -197,15 +205,30 @@ def _shared_gpu_worker(rank, world, port, q, width=1, fp8=False):
             crit(m(x[mine]), y[mine]).backward()
             torch.cuda.synchronize()
             got = [p.grad.detach().clone() for p in m.parameters()]
-            ddp_state, m._ddp = m._ddp, None  # single-process reference: both chunks here
-            acc = None
-            for r in range(world):
+            ddp_state, m._ddp = m._ddp, None
+            if fp8:
+                # each rank's own chunk gradient without DDP, at the settled scales,
+                # summed over the ranks by hand (a plain gloo all_reduce)
                 m.load_state_dict(sd)
                 for p in m.parameters():
                     p.grad = None
-                crit(m(x[r * per:(r + 1) * per]), y[r * per:(r + 1) * per]).backward()
-                g = [p.grad.detach().clone() for p in m.parameters()]
-                acc = g if acc is None else [a + b for a, b in zip(acc, g)]
+                crit(m(x[mine]), y[mine]).backward()
+                acc = [p.grad.detach().clone() for p in m.parameters()]
+                flat = torch.cat([a.reshape(-1) for a in acc])
+                dist.all_reduce(flat)
+                acc, o = [], 0
+                for p in m.parameters():
+                    acc.append(flat[o:o + p.numel()].view_as(p))
+                    o += p.numel()
+            else:
+                acc = None  # single-process reference: both chunks here
+                for r in range(world):
+                    m.load_state_dict(sd)
+                    for p in m.parameters():
+                        p.grad = None
+                    crit(m(x[r * per:(r + 1) * per]), y[r * per:(r + 1) * per]).backward()
+                    g = [p.grad.detach().clone() for p in m.parameters()]
+                    acc = g if acc is None else [a + b for a, b in zip(acc, g)]
             m._ddp = ddp_state
             want = [a / world for a in acc]
             errs.append(max(_rel(a, b) for a, b in zip(got, want) if b.norm() > 0))
@@ -257,12 +280,14 @@ def test_ddp_two_ranks_share_one_gpu(pkg, width, fp8):
     oracle's chunk mean at the end-to-end head bar of test_model_gpu (0.1),
     and the parameters are identical on both ranks after the fused Adam step.
     wide_fp8: the same multi-process path for BASELINE
-    configs[4] (width 2, fp8 forward).  Its delayed-amax scales evolve with
-    every forward, so the single-process reference (two chunk forwards in one
-    process) quantizes with other scales than the ranks: there the bar is
-    relative L2 <= 0.1 (fp8 e4m3 carries 3 mantissa bits; measured value
-    printed), the head bar 0.2, and the replicas must still be bit-identical
-    after Adam."""
+    configs[4] (width 2, fp8 forward).  Its delayed-amax scales are per
+    process and move with every forward, so a single-process two-chunk
+    reference quantizes with other scales than the ranks (measured: relative
+    L2 ~1 through the 2 x 128^2 batch's tiny-sample BNs).  There each rank
+    first settles its scales on its own chunk, and the reference is the sum
+    over ranks (plain all_reduce) of each rank's own non-DDP chunk gradient at
+    those scales: bar relative L2 <= 1e-3, head vs oracle 0.2, replicas
+    bit-identical after Adam."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -276,7 +301,7 @@ def test_ddp_two_ranks_share_one_gpu(pkg, width, fp8):
         print(f"rank {rank}: reduced vs single-process mean {errs} exact {exact}; head vs oracle {head}; "
               f"params equal after Adam {same}")
         assert not msg, msg
-        assert max(errs) <= (0.1 if fp8 else 1e-6) and same, (rank, errs, same)
+        assert max(errs) <= (1e-3 if fp8 else 1e-6) and same, (rank, errs, same)
         assert head and max(head.values()) <= (0.2 if fp8 else 0.1), head
 
 
