@@ -200,84 +200,102 @@ struct TileEpi {
     const bool fbwd = a.bb.sums != nullptr;
     const bool stats = a.stats != nullptr || fbwd;
     const bool vec16 = (a.ldy % 8 == 0) && (!a.ysplit || (a.ldysplit % 8 == 0 && a.csplit % 8 == 0));
+    const bool fold = !FLIP && a.fold_on;
     const int g = lane >> 4;
+    // fragment pairs (2 ip, 2 ip + 1) outermost: the lane's channel constants
+    // of the pair (4 consecutive channels per fragment: bias or shift' | scale
+    // or mean | invstd | mean2 | invstd2) are read from LDS once, together,
+    // and serve every row of the tile
 #pragma unroll
-    for (int j = 0; j < RW; ++j) {
-      uint2 oq[FN];
+    for (int ip = 0; ip < FN / 2; ++ip) {
+      f32x4 kb[2], km[2], ki[2], km2[2], ki2[2];
 #pragma unroll
-      for (int i = 0; i < FN; ++i) {
-        const int cl = i * 16 + (g << 2);
-        const int co = co0 + cl;
-        const bool live = co < a.Cout;
-        float v[4];
-        if (!FLIP && a.fold_on) {  // eval BN folded: (conv + bias) * scale + shift' (cst: shift' | scale)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = acc[j][i][e] * cst[COT + cl + e] + cst[cl + e];
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = acc[j][i][e] + cst[cl + e];
-        }
-        if (!FLIP && a.add) {  // forward residual, then the folded BN's ReLU
-          const uint2 u = uadd[j][i];
-          v[0] += __uint_as_float(u.x << 16); v[1] += __uint_as_float(u.x & 0xffff0000u);
-          v[2] += __uint_as_float(u.y << 16); v[3] += __uint_as_float(u.y & 0xffff0000u);
-        }
-        if (!FLIP && a.fold_relu) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-        }
-        if (FLIP) {
-          const uint2 u = uadd[j][i], m = uact[j][i];
-          v[0] += __uint_as_float(u.x << 16); v[1] += __uint_as_float(u.x & 0xffff0000u);
-          v[2] += __uint_as_float(u.y << 16); v[3] += __uint_as_float(u.y & 0xffff0000u);
-          if (fbwd) {
-            if (!(__uint_as_float(m.x << 16) > 0.f)) v[0] = 0.f;
-            if (!(__uint_as_float(m.x & 0xffff0000u) > 0.f)) v[1] = 0.f;
-            if (!(__uint_as_float(m.y << 16) > 0.f)) v[2] = 0.f;
-            if (!(__uint_as_float(m.y & 0xffff0000u) > 0.f)) v[3] = 0.f;
-          }
-        }
-        uint2 o;
-        o.x = pack_bf2(v[0], v[1]);
-        o.y = pack_bf2(v[2], v[3]);
-        oq[i] = o;
-        if (!live) continue;
-        if (!vec16) {
-          if (a.ysplit && co >= a.csplit) *reinterpret_cast<uint2*>(a.ysplit + pix[j] * a.ldysplit + co - a.csplit) = o;
-          else *reinterpret_cast<uint2*>(a.y + pix[j] * a.ldy + co) = o;
-        }
-        if (FLIP && fbwd) {  // sums of the stored bf16 dZ, as bn_bwd_reduce_kernel would read them
-          const float dz[4] = {__uint_as_float(o.x << 16), __uint_as_float(o.x & 0xffff0000u),
-                               __uint_as_float(o.y << 16), __uint_as_float(o.y & 0xffff0000u)};
-          const uint2 u = uy[j][i];
-          const float yv[4] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
-                               __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            q0[i][e] += dz[e];
-            q1[i][e] += dz[e] * (yv[e] - cst[COT + cl + e]) * cst[2 * COT + cl + e];
-          }
-          if constexpr (TWO) {
-            const uint2 w = uy2[j][i];
-            const float y2[4] = {__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
-                                 __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) q2[i][e] += dz[e] * (y2[e] - cst[3 * COT + cl + e]) * cst[4 * COT + cl + e];
-          }
-        } else if (stats) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) { q0[i][e] += v[e]; q1[i][e] += v[e] * v[e]; }
+      for (int h = 0; h < 2; ++h) {
+        const int cl = (2 * ip + h) * 16 + (g << 2);
+        kb[h] = *reinterpret_cast<const f32x4*>(cst + cl);
+        if (fold || (FLIP && fbwd)) km[h] = *reinterpret_cast<const f32x4*>(cst + COT + cl);
+        if (FLIP && fbwd) ki[h] = *reinterpret_cast<const f32x4*>(cst + 2 * COT + cl);
+        if (TWO && FLIP && fbwd) {
+          km2[h] = *reinterpret_cast<const f32x4*>(cst + 3 * COT + cl);
+          ki2[h] = *reinterpret_cast<const f32x4*>(cst + 4 * COT + cl);
         }
       }
-      if (vec16) {
 #pragma unroll
-        for (int ip = 0; ip < FN / 2; ++ip) {
+      for (int j = 0; j < RW; ++j) {
+        uint2 oq[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int i = 2 * ip + h;
+          const int cl = i * 16 + (g << 2);
+          const int co = co0 + cl;
+          const bool live = co < a.Cout;
+          float v[4];
+          if (fold) {  // eval BN folded: (conv + bias) * scale + shift' (cst: shift' | scale)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = acc[j][i][e] * km[h][e] + kb[h][e];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = acc[j][i][e] + kb[h][e];
+          }
+          if (!FLIP && a.add) {  // forward residual, then the folded BN's ReLU
+            const uint2 u = uadd[j][i];
+            v[0] += __uint_as_float(u.x << 16); v[1] += __uint_as_float(u.x & 0xffff0000u);
+            v[2] += __uint_as_float(u.y << 16); v[3] += __uint_as_float(u.y & 0xffff0000u);
+          }
+          if (!FLIP && a.fold_relu) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+          }
+          if (FLIP) {
+            const uint2 u = uadd[j][i], m = uact[j][i];
+            v[0] += __uint_as_float(u.x << 16); v[1] += __uint_as_float(u.x & 0xffff0000u);
+            v[2] += __uint_as_float(u.y << 16); v[3] += __uint_as_float(u.y & 0xffff0000u);
+            if (fbwd) {
+              if (!(__uint_as_float(m.x << 16) > 0.f)) v[0] = 0.f;
+              if (!(__uint_as_float(m.x & 0xffff0000u) > 0.f)) v[1] = 0.f;
+              if (!(__uint_as_float(m.y << 16) > 0.f)) v[2] = 0.f;
+              if (!(__uint_as_float(m.y & 0xffff0000u) > 0.f)) v[3] = 0.f;
+            }
+          }
+          uint2 o;
+          o.x = pack_bf2(v[0], v[1]);
+          o.y = pack_bf2(v[2], v[3]);
+          oq[h] = o;
+          if (!live) continue;
+          if (!vec16) {
+            if (a.ysplit && co >= a.csplit) *reinterpret_cast<uint2*>(a.ysplit + pix[j] * a.ldysplit + co - a.csplit) = o;
+            else *reinterpret_cast<uint2*>(a.y + pix[j] * a.ldy + co) = o;
+          }
+          if (FLIP && fbwd) {  // sums of the stored bf16 dZ, as bn_bwd_reduce_kernel would read them
+            const float dz[4] = {__uint_as_float(o.x << 16), __uint_as_float(o.x & 0xffff0000u),
+                                 __uint_as_float(o.y << 16), __uint_as_float(o.y & 0xffff0000u)};
+            const uint2 u = uy[j][i];
+            const float yv[4] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                                 __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              q0[i][e] += dz[e];
+              q1[i][e] += dz[e] * (yv[e] - km[h][e]) * ki[h][e];
+            }
+            if constexpr (TWO) {
+              const uint2 w = uy2[j][i];
+              const float y2[4] = {__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+                                   __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)};
+#pragma unroll
+              for (int e = 0; e < 4; ++e) q2[i][e] += dz[e] * (y2[e] - km2[h][e]) * ki2[h][e];
+            }
+          } else if (stats) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { q0[i][e] += v[e]; q1[i][e] += v[e] * v[e]; }
+          }
+        }
+        if (vec16) {
           // rows (0,1,2,3) end up holding channels (0-7, 16-23, 8-15, 24-31) of the pair
-          const auto sx = __builtin_amdgcn_permlane16_swap(oq[2 * ip].x, oq[2 * ip + 1].x, false, false);
-          const auto sy = __builtin_amdgcn_permlane16_swap(oq[2 * ip].y, oq[2 * ip + 1].y, false, false);
+          const auto sx = __builtin_amdgcn_permlane16_swap(oq[0].x, oq[1].x, false, false);
+          const auto sy = __builtin_amdgcn_permlane16_swap(oq[0].y, oq[1].y, false, false);
           const uint4 chunk = make_uint4(sx[0], sy[0], sx[1], sy[1]);
           const int co = co0 + ip * 32 + ((g & 1) << 4) + ((g >> 1) << 3);
-          if (co < a.Cout) {
+          if (co < a.Cout && UNET_ABL != 4) {  // (ABL 4: timing build without the tile stores)
             if (a.ysplit && co >= a.csplit)
               *reinterpret_cast<uint4*>(a.ysplit + pix[j] * a.ldysplit + co - a.csplit) = chunk;
             else *reinterpret_cast<uint4*>(a.y + pix[j] * a.ldy + co) = chunk;
@@ -532,15 +550,19 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
 #pragma unroll
     for (int p = 0; p < (UNET_ABL == 1 ? 0 : NP); ++p)
       mfma_panel<FN, RW, NP * COT * 64, FLIP>(acc, wl + p * COT * 64, H + p * PANEL, aoff, boff);
-    if (k < 9) TSTAMP(a.tim, 2 + 2 * k);
+    // stamps: 2 per tile (after the MFMAs, after the epilogue); UNET_ABL == 3
+    // (fine build): 4 per tile for the first 4 tiles (+ after the wait, after the barrier)
+    if (UNET_ABL >= 3 ? k < 4 : k < 9) TSTAMP(a.tim, UNET_ABL >= 3 ? 2 + 4 * k : 2 + 2 * k);
     if (!PREF) epi.fetch(a, pix, co0, lane);
     epi.landed();
     wait_vmcnt<0>();               // the next tile's halo (issued before this tile's MFMAs) has landed ...
+    if (UNET_ABL >= 3 && k < 4) TSTAMP(a.tim, 3 + 4 * k);
     __builtin_amdgcn_s_barrier();  // ... everyone's part; buffer b is free for reuse
+    if (UNET_ABL >= 3 && k < 4) TSTAMP(a.tim, 4 + 4 * k);
     // the stores go out AFTER the wait: they drain under the next tile's MFMAs
     // instead of being waited for here (vmcnt counts stores too)
     epi.store(a, acc, pix, co0, lane, cst, q0, q1, q2);
-    if (k < 9) TSTAMP(a.tim, 3 + 2 * k);
+    if (UNET_ABL >= 3 ? k < 4 : k < 9) TSTAMP(a.tim, UNET_ABL >= 3 ? 5 + 4 * k : 3 + 2 * k);
   }
   TSTAMP(a.tim, 20);
   if (a.stats || a.bb.sums) commit_stats<FN, NW, false>(a, q0, q1, q2, co0, smem);

@@ -9,6 +9,8 @@
 //                           as resizeAreaFast_ (block sum * 1/area), otherwise
 //                           the computeResizeAreaTab coverage weights, float
 //                           accumulation, cvRound                        (:51)
+//   resize_area_up_kernel   the same call enlarging an axis: OpenCV's
+//                           fixed-point area-mode linear resize          (:51)
 //   mask_kernel             cv2.resize INTER_NEAREST, then mask > 0 -> 1.f (:52,61)
 //   normalize_kernel        np.percentile(2, 98) + clip + astype(uint8) (:33-34),
 //                           CLAHE(2.0, 8x8) (:37-38), min-max to [0, 1] (:41);
@@ -83,6 +85,42 @@ __global__ void __launch_bounds__(256) resize_area_kernel(const uint8_t* __restr
     acc = j == 0 ? t : __fadd_rn(acc, t);
   }
   dst[i] = sat_u8(cv_round(acc));
+}
+
+// cv2.resize INTER_AREA when an axis is ENLARGED (OpenCV resize.cpp: not
+// is-area: resizeGeneric_ with area_mode linear coefficients, fixed point for
+// 8U): per axis sx = floor(d * scale), f = (float)((d+1) - (sx+1) * inv_scale),
+// f = f <= 0 ? 0 : f - floor(f), coefficients saturate_cast<short>({1-f, f} *
+// 2048); horizontal D = S[sx] a0 + S[sx+1] a1 (S[sx] * 2048 once sx + 1 >= W),
+// vertical ((b0 (D0 >> 4)) >> 16) + ((b1 (D1 >> 4)) >> 16) + 2) >> 2 over rows
+// clip(sy, sy+1 to H-1).  Integer arithmetic after the coefficients.
+__device__ __forceinline__ void area_linear_coef(int d, int ssize, int dsize, int& s, int& c0, int& c1) {
+  const double inv = (double)dsize / ssize, scale = 1.0 / inv;
+  s = (int)floor(d * scale);
+  float f = (float)((d + 1) - (s + 1) * inv);
+  f = f <= 0.f ? 0.f : __fsub_rn(f, floorf(f));
+  if (s >= ssize - 1) s = ssize - 1;
+  c0 = (int)rintf(__fmul_rn(__fsub_rn(1.f, f), 2048.f));
+  c1 = (int)rintf(__fmul_rn(f, 2048.f));
+}
+
+__global__ void __launch_bounds__(256) resize_area_up_kernel(const uint8_t* __restrict__ src,
+                                                             uint8_t* __restrict__ dst, int N, int H, int W, int oh,
+                                                             int ow) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)N * oh * ow) return;
+  const int dx = (int)(i % ow), dy = (int)((i / ow) % oh), n = (int)(i / ((int64_t)oh * ow));
+  const uint8_t* img = src + (int64_t)n * H * W;
+  int sx, a0, a1, sy, b0, b1;
+  area_linear_coef(dx, W, ow, sx, a0, a1);
+  area_linear_coef(dy, H, oh, sy, b0, b1);
+  int D[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const uint8_t* row = img + (int64_t)min(sy + k, H - 1) * W;
+    D[k] = sx + 1 >= W ? (int)row[sx] * 2048 : (int)row[sx] * a0 + (int)row[sx + 1] * a1;
+  }
+  dst[i] = (uint8_t)((((b0 * (D[0] >> 4)) >> 16) + ((b1 * (D[1] >> 4)) >> 16) + 2) >> 2);
 }
 
 __global__ void __launch_bounds__(256) mask_kernel(const uint8_t* __restrict__ src, float* __restrict__ dst, int N,
@@ -354,7 +392,12 @@ __global__ void __launch_bounds__(256) filter2d_kernel(const uint8_t* __restrict
 static inline unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
 
 hipError_t launch_resize_area(const uint8_t* src, uint8_t* dst, int N, int H, int W, int oh, int ow, hipStream_t st) {
-  if (N <= 0 || oh <= 0 || ow <= 0 || oh > H || ow > W) return hipErrorInvalidValue;
+  if (N <= 0 || oh <= 0 || ow <= 0 || H <= 0 || W <= 0) return hipErrorInvalidValue;
+  if (oh > H || ow > W) {  // an axis is enlarged: cv::resize leaves the area path
+    hipLaunchKernelGGL(resize_area_up_kernel, dim3(blocks_for((int64_t)N * oh * ow)), dim3(256), 0, st, src, dst, N, H,
+                       W, oh, ow);
+    return hipGetLastError();
+  }
   if ((double)W / ow > kAreaCap - 2 || (double)H / oh > kAreaCap - 2) return hipErrorInvalidValue;
   // cv::resize is_area_fast: both scales 1 / (dsize / ssize) within DBL_EPSILON of an integer
   const double sx = 1.0 / ((double)ow / W), sy = 1.0 / ((double)oh / H);

@@ -211,6 +211,15 @@ struct unet_plan {
   // batched stream-K launch at the bucket boundary (wgrad3x3_batch_kernel):
   // no per-layer split-K slab round trip.  UNET_WG_BATCH=0: one launch per layer (A/B)
   bool wg_batch = !(std::getenv("UNET_WG_BATCH") && std::atoi(std::getenv("UNET_WG_BATCH")) == 0);
+  // the stem by recompute (stem_rc.hip): the raw 7x7 conv output y0 is never
+  // stored; statistics pass + act/pool pass forward, one pass for the maxpool
+  // backward, the stem BN backward and the stem weight gradient.  Shapes with
+  // stem rows over 256 pixels (HiRes) keep the stored-y0 path.  UNET_STEM_RC=0:
+  // stored-y0 path everywhere (A/B); UNET_STEM_KEEP=1: y0 and dZ are stored
+  // too (tests of the intermediates)
+  bool stem_rc = !(std::getenv("UNET_STEM_RC") && std::atoi(std::getenv("UNET_STEM_RC")) == 0);
+  bool stem_keep = std::getenv("UNET_STEM_KEEP") && std::atoi(std::getenv("UNET_STEM_KEEP")) != 0;
+  size_t stem_part = 0, stem_tot = 0;
   std::vector<ConvWgradArgs> wgb;  // collected weight gradients of the current bucket
   std::vector<std::string> wgb_names;
   double wgb_flops = 0;
@@ -526,6 +535,12 @@ static int build_plan(unet_plan* p) {
   p->y0 = act(A, N, H2, W2, c0);
   p->p0 = act(A, N, H4, W4, c0);
   p->pidx = A.take((size_t)N * H4 * W4 * c0);
+  p->stem_rc = p->stem_rc && p->fuse_bwd && p->stem_bn_fuse && stem_rc_ok(c0, H2, W2) && H2 == 2 * H4 &&
+               W2 == 2 * W4 && H == 2 * H2 && W == 2 * W2;
+  if (p->stem_rc) {
+    p->stem_part = A.take(stem_rc_part_bytes(N, H2, W2, c0));
+    p->stem_tot = A.take(stem_rc_tot_bytes(c0));
+  }
   // split-K partials of one weight-gradient launch (register-native layout);
   // launchers cap their split count to what fits
   p->wslab_bytes = (size_t)(64 * w * w) << 20;
@@ -708,9 +723,12 @@ static int build_plan(unet_plan* p) {
 
   // named views for tests: forward activations and their gradients
   auto& nm = p->named;
-  nm.push_back({"y0", p->y0}); nm.push_back({"x1", p->x1}); nm.push_back({"p0", p->p0});
-  nm.push_back({"d.x1", p->d_x1}); nm.push_back({"d.p0", p->d_p0});
-  if (!(p->fuse_bwd && p->stem_bn_fuse)) nm.push_back({"d.y0", p->d_y0});  // else never stored
+  const bool y0_stored = !p->stem_rc || p->stem_keep;  // recompute: y0 / dZ only kept for tests
+  if (y0_stored) nm.push_back({"y0", p->y0});
+  nm.push_back({"x1", p->x1}); nm.push_back({"p0", p->p0});
+  if (y0_stored) nm.push_back({"d.x1", p->d_x1});
+  nm.push_back({"d.p0", p->d_p0});
+  if (!(p->fuse_bwd && p->stem_bn_fuse) && !p->stem_rc) nm.push_back({"d.y0", p->d_y0});  // else never stored
   {
     int bi = 0;
     for (int s = 0; s < 4; ++s)
@@ -834,8 +852,8 @@ BnLaunch bn_launch(const Ctx& x, int bi, int64_t npix) {
   l.stats = x.W<double>(b.stats);
   l.gamma = x.prm[b.gamma];
   l.beta = x.prm[b.beta];
-  l.run_mean = x.buf[3 * b.idx + 0];
-  l.run_var = x.buf[3 * b.idx + 1];
+  l.run_mean = x.buf ? x.buf[3 * b.idx + 0] : nullptr;  // (backward contexts carry no buffers)
+  l.run_var = x.buf ? x.buf[3 * b.idx + 1] : nullptr;
   l.save_mean = x.W<float>(b.save);
   l.save_invstd = x.W<float>(b.save) + b.C;
   l.count = (double)npix;
@@ -1353,6 +1371,22 @@ int ch_att_forward(const Ctx& x, int l) {
   return 0;
 }
 
+// the stem-by-recompute arguments shared by its forward and backward passes
+StemRcArgs stem_rc_args(const Ctx& x, const float* image) {
+  const unet_plan* p = x.p;
+  const Conv& cv = p->convs[p->stem_conv];
+  StemRcArgs s = {};
+  s.img = image; s.H = p->cfg.H; s.W = p->cfg.W;
+  s.w = x.W<bf16_t>(cv.pk_fwd);
+  s.N = p->cfg.N; s.P = p->y0.H; s.Q = p->y0.W; s.Cout = cv.Co; s.Pp = p->p0.H; s.Qp = p->p0.W;
+  s.bn = bn_launch(x, p->stem_bn, (int64_t)s.N * s.P * s.Q);
+  s.stats = x.training ? x.W<double>(p->bns[p->stem_bn].stats) : nullptr;
+  if (p->stem_keep) { s.y = x.A(p->y0); s.ldy = p->y0.ld; }
+  s.act = x.A(p->x1); s.ldact = p->x1.ld;
+  s.pool = x.A(p->p0); s.ldpool = p->p0.ld; s.idx = x.W<uint8_t>(p->pidx);
+  return s;
+}
+
 static int run_forward(unet_plan* p, const float* image, const float* const* prm, float* const* buf, char* ws,
                        float* logits, int training, hipStream_t st) {
   Ctx x{p, ws, prm, buf, st, training};
@@ -1398,7 +1432,18 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
     RUN(flush());
   }
   // stem: conv7x7/s2 -> bn1 -> relu into cat1[:, :c0]; maxpool
-  {
+  if (p->stem_rc) {
+    StemRcArgs s = stem_rc_args(x, image);
+    const double fl = 2.0 * N * p->y0.H * p->y0.W * p->convs[p->stem_conv].Co * 49;
+    if (training) {
+      ProfScope ps(p, st, "fwd input_conv.weight (stats)", fl);
+      s.tim = tim_slot(p, "fwd input_conv.weight (stats)");
+      CK(launch_stem_rc_fwd(s, 0, st));
+    }
+    ProfScope ps(p, st, "fwd input_conv.weight +bn+pool", fl);
+    s.tim = tim_slot(p, "fwd input_conv.weight +bn+pool");
+    CK(launch_stem_rc_fwd(s, 1, st));
+  } else {
     const Conv& cv = p->convs[p->stem_conv];
     ConvFwdArgs a = {};
     a.x = reinterpret_cast<const bf16_t*>(image); a.ldx = 1;
@@ -1743,7 +1788,33 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     }
   }
   // maxpool + stem
-  {
+  if (p->stem_rc && fz) {
+    // one pass: maxpool backward, stem BN backward, stem weight gradient
+    StemRcArgs s = stem_rc_args(x, image);
+    const Act skip = att ? p->atts[3].dskip : slice(p->decs[3].dcat, 0, p->x1.C);
+    const BnBwdArgs sb = bwd_args(x, p->stem_bn, p->d_x1, p->x1, p->y0, p->d_y0, -1, nullptr, nullptr, nullptr,
+                                  grads);
+    s.dpool = x.A(p->d_p0); s.lddpool = p->d_p0.ld;
+    s.add = x.A(skip); s.ldadd = skip.ld;
+    s.mean = sb.mean; s.invstd = sb.invstd;
+    if (p->stem_keep) { s.dz = x.A(p->d_x1); s.lddz = p->d_x1.ld; }
+    s.part = x.W<float>(p->stem_part);
+    s.l2 = reinterpret_cast<double*>(s.part + stem_rc_l2_offset(N, p->y0.H, p->y0.W, p->x1.C) / sizeof(float));
+    s.tot = x.W<double>(p->stem_tot);
+    s.dw = x.W<float>(p->convs[p->stem_conv].wacc);
+    s.dgamma = sb.dgamma; s.dbeta = sb.dbeta;
+    s.npix = (int64_t)N * p->y0.H * p->y0.W;
+    {
+      ProfScope ps(p, st, "wgrad input_conv.weight +maxpool+bn", 3.0 * 2.0 * N * p->y0.H * p->y0.W * p->x1.C * 49);
+      s.tim = tim_slot(p, "wgrad input_conv.weight +maxpool+bn");
+      CK(launch_stem_rc_bwd(s, 0, st));
+    }
+    {
+      ProfScope ps(p, st, "wgrad_reduce input_conv.weight", 0);
+      CK(launch_stem_rc_bwd(s, 1, st));
+    }
+    RUN(fork());
+  } else {
     MaxPoolArgs m = {};
     m.dy = x.A(p->d_p0); m.lddy = p->d_p0.ld; m.idx = x.W<uint8_t>(p->pidx);
     const Act skip = att ? p->atts[3].dskip : slice(p->decs[3].dcat, 0, p->x1.C);

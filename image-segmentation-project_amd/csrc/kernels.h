@@ -273,6 +273,39 @@ hipError_t launch_maxpool_fwd(const MaxPoolArgs& a, hipStream_t st);
 hipError_t launch_bn_relu_maxpool_fwd(const MaxPoolArgs& a, hipStream_t st);
 hipError_t launch_maxpool_bwd(const MaxPoolArgs& a, hipStream_t st);
 
+// The stem by recompute (stem_rc.hip): conv 7x7/s2 (1 -> Cout) + BN + ReLU +
+// MaxPool(3,2,1) without storing the raw conv output.  Forward: a statistics
+// pass (mode 0: BN sums, last block finalises bn; y stored only when y != null,
+// tests) and an apply pass (mode 1: act, pooled, idx).  Backward: dZ of the
+// stem BN from dpool / idx / add (the maxpool backward, stored to dz only when
+// dz != null) and, in the same pass, partial sums of dZ^T im2col, xhat^T
+// im2col, im2col, dZ, dZ xhat per block (part); a fixed-order reduce (tot,
+// tot64) and a finalise write dw [Cout][64], dgamma, dbeta.
+struct StemRcArgs {
+  const float* img; int H, W;        // fp32 [N][H][W]
+  const bf16_t* w;                   // packed [Cout][64] bf16
+  int N, P, Q, Cout, Pp, Qp;         // conv output P x Q, pooled Pp x Qp
+  double* stats; BnLaunch bn;        // BN of the stem (bn.ss: scale | shift)
+  bf16_t* y; int ldy;
+  bf16_t* act; int ldact;
+  bf16_t* pool; int ldpool; uint8_t* idx;   // idx [pixel][Cout]
+  const bf16_t* dpool; int lddpool;
+  const bf16_t* add; int ldadd;
+  const float* mean; const float* invstd;   // saved batch statistics
+  bf16_t* dz; int lddz;
+  float* part; double* l2; double* tot;   // partials, fp64 level-1 sums, fp64 totals
+  float* dw; float* dgamma; float* dbeta;
+  int64_t npix;
+  unsigned long long* tim;           // phase stamps (debug build only)
+};
+bool stem_rc_ok(int Cout, int P, int Q);
+hipError_t launch_stem_rc_fwd(const StemRcArgs& a, int mode, hipStream_t st);
+// stage 0: the fused backward pass; stage 1: the fixed-order reduce + finalise
+hipError_t launch_stem_rc_bwd(const StemRcArgs& a, int stage, hipStream_t st);
+size_t stem_rc_part_bytes(int N, int P, int Q, int Cout);  // a.part followed by a.l2
+size_t stem_rc_tot_bytes(int Cout);                        // a.tot
+size_t stem_rc_l2_offset(int N, int P, int Q, int Cout);   // bytes from a.part to a.l2
+
 // fused ConvTranspose2d(k2,s2, Cin->16) + Conv1x1(16->1): logits[2i+a,2j+b] =
 // c0 + sum_c X[i,j,c] V[c][a][b],  V[c][ab] = sum_o Wf[o] W0[c][o][ab].
 struct HeadArgs {

@@ -1,0 +1,796 @@
+// The stem (input_conv 7x7/s2/p3 1 -> C0, bn1, ReLU, MaxPool2d(3,2,1);
+// advanced_models.py:76-83 via the resnet34 stem) by RECOMPUTE: the raw conv
+// output y (N x H/2 x W/2 x C0 bf16, 134 MB at 16 x 512^2) is never stored.
+// Its input is a 1-channel fp32 image (16 MB) and the conv is 49 MACs per
+// output value, so recomputing it wherever y is needed costs a few MFMAs per
+// pixel against ~0.3 GB of HBM traffic saved per step.
+//
+//   stats pass   conv -> BN batch sums (fp64 replica atomics, last block
+//                finalises scale/shift/save/running stats as stem_fwd did)
+//   apply pass   conv -> bf16 y -> relu(y * scale + shift) = act (the
+//                decoder1 skip, stored once) -> MaxPool(3,2,1) of act in LDS
+//                -> pooled + argmax index.  A block walks pooled rows, keeping
+//                the last three act rows in an LDS ring; its first pooled row
+//                recomputes the act row above it (owned by the previous block).
+//   backward     conv -> y, xhat; dZ = [act > 0] (maxpool scatter of dpool +
+//                the skip gradient) -- maxpool_bwd's expression, bit-identical
+//                dZ -- and, in the same pass, the stem weight gradient through
+//                the BN-backward identity
+//                  dY = k1 dZ - k1 m1 - k1 m2 xhat       (k1 = gamma invstd,
+//                  m1 = mean dZ, m2 = mean dZ xhat), so
+//                  dW[co][k] = k1 (sum dZ im - m1 sum im - m2 sum xhat im)
+//                three GEMMs over the pixels whose coefficients are only known
+//                at the end: each block leaves its partial sums (dZ^T im,
+//                xhat^T im, sum im, sum dZ, sum dZ xhat), a fixed-order reduce
+//                sums them and a finalise forms dW, dgamma, dbeta.
+// Nothing here depends on timing: every sum has a fixed order (bit-
+// reproducible backward).
+//
+// im2col K layout (as the packed stem weights [Cout][64]): k = kr * 8 + ks,
+// kr, ks < 7 the 7x7 taps, the rest zero.  MFMA 16x16x32 bf16, A = weights
+// (rows = channels), B = im2col (cols = pixels): lane holds 4 consecutive
+// channels of one pixel.
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace unet {
+
+void conv_kernel_tag(const char* tag);  // conv_kernels.hip (profiler column)
+
+namespace {
+
+// [pixel][64 bf16] tile with 16-B chunks XOR-swizzled by (pixel & 7)
+__device__ __forceinline__ int ring_off(int px, int co) {
+  return px * 128 + ((((co >> 3) ^ px) & 7) << 4) + ((co & 7) << 1);
+}
+
+// [pixel][64] tile read through ds_read_b64_tr_b16 (conv_kernels.hip tr_off<64>)
+__device__ __forceinline__ int tt_off(int row, int col) {
+  const int unit = col >> 4;
+  const int f = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+  return row * 128 + ((unit ^ f) << 5) + ((col & 15) << 1);
+}
+
+__device__ __forceinline__ bf16x8 tr8(const char* lo, const char* hi) {
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, lo));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, hi));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 r = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+// Input patch: rows ih0 .. ih0 + nrows - 1 of image n, columns iw0 .. iw0 +
+// COLS - 1 (zero outside the image), COLS = 2 * NPX + 6 for NPX output pixels;
+// fetched into registers (PT per thread, NT threads), stored as bf16 rows of
+// pitch PITCH (4-B aligned: the im2col reads 4 dwords from column 2 px).
+template <int NPX, int NT, int PT>
+struct Patch {
+  static constexpr int COLS = 2 * NPX + 6;
+  static constexpr int PITCH = 2 * NPX + 8;
+  float v[PT];
+  __device__ __forceinline__ void fetch(const float* img, int H, int W, int n, int ih0, int nrows, int iw0) {
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+      const int i = threadIdx.x + j * NT;
+      const int r = i / COLS, c = i - r * COLS;
+      const int ih = ih0 + r, iw = iw0 + c;
+      v[j] = (r < nrows && ih >= 0 && ih < H && iw >= 0 && iw < W) ? img[((size_t)n * H + ih) * W + iw] : 0.f;
+    }
+  }
+  __device__ __forceinline__ void store(bf16_t* patch, int nrows) const {
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+      const int i = threadIdx.x + j * NT;
+      const int r = i / COLS, c = i - r * COLS;
+      if (r < nrows) patch[r * PITCH + c] = f2bf(v[j]);
+    }
+  }
+};
+
+// im2col chunk kr (8 taps ks = 0..7 of patch row prow0 + kr, 8th masked) of
+// output pixel px: 4 dwords from column 2 px
+template <int PITCH>
+__device__ __forceinline__ uint4 im2col_chunk(const bf16_t* patch, int prow0, int px, int kr) {
+  if (kr >= 7) return make_uint4(0, 0, 0, 0);
+  const unsigned* w = reinterpret_cast<const unsigned*>(patch + (prow0 + kr) * PITCH + 2 * px);
+  return make_uint4(w[0], w[1], w[2], w[3] & 0xffffu);
+}
+
+// packed weights of channel group cg as MFMA A fragments: wf[kk][i] = W[cg +
+// i*16 + (lane&15)][(kk*4 + (lane>>4)) * 8 ..]
+__device__ __forceinline__ void load_wfrag(const bf16_t* w, int cg, bf16x8 (&wf)[2][4]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      wf[kk][i] = *reinterpret_cast<const bf16x8*>(w + (size_t)(cg + i * 16 + (lane & 15)) * 64 +
+                                                   (kk * 4 + (lane >> 4)) * 8);
+}
+
+// one wave's 32 output pixels (x0 .. x0+31 of the Xs tile) x 64 channels:
+// the MFMA sequence of stem_fwd_kernel (same K split), so y is bit-identical
+__device__ __forceinline__ void conv32(const char* Xs, int x0, const bf16x8 (&wf)[2][4], f32x4 (&acc)[4][2]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int ch = kk * 4 + (lane >> 4);
+    bf16x8 xf[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) xf[j] = *reinterpret_cast<const bf16x8*>(Xs + tt_off(x0 + j * 16 + (lane & 15), ch * 8));
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kk][i], xf[j], acc[i][j], 0, 0, 0);
+  }
+}
+
+// workgroup barrier ordering LDS only (conv_halo.hip lds_barrier): the
+// global loads prefetched into registers and the HBM stores stay in flight
+// (__syncthreads' fence would wait for every one of them)
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// act = bf16(relu(y * sc + sh)) of a bf16-rounded y (bn_relu_maxpool_fwd's expression)
+__device__ __forceinline__ float stem_act(float y, float sc, float sh) {
+  const float z = y * sc + sh;
+  return bf2f(f2bf(z > 0.f ? z : 0.f));
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// forward: MODE 0 = BN statistics (and, for tests, the raw y), MODE 1 = act +
+// pool.  512 threads (8 waves x 32 pixels = one 256-pixel output row per conv
+// round).  A block owns pooled rows [j0, j1) of the flattened N x Pp grid (one
+// pooled row = stem rows 2jp, 2jp+1), channel group blockIdx.y.
+// ---------------------------------------------------------------------------
+constexpr int kRcNT = 512;
+constexpr int kRcNPX = 256;
+typedef Patch<kRcNPX, kRcNT, 12> FwdPatch;  // up to 11 input rows x 518 columns
+constexpr int kRcRing = 3 * kRcNPX * 128;
+constexpr int kRcXs = kRcNPX * 128;
+constexpr int kRcPatchB = 11 * FwdPatch::PITCH * 2;
+
+template <int MODE>
+__global__ void __launch_bounds__(kRcNT) stem_rc_fwd_kernel(StemRcArgs a, int per) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  TSTAMP_RT(a.tim, 30);
+  TSTAMP(a.tim, 0);
+  char* ring = smem;                                            // MODE 1: act rows r % 3
+  char* Xs = smem + (MODE == 1 ? kRcRing : 0);                  // im2col of one output row
+  bf16_t* patch = reinterpret_cast<bf16_t*>(Xs + kRcXs);
+  float* coef = reinterpret_cast<float*>(Xs + kRcXs + kRcPatchB);  // [2][64] scale | shift
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int cg = blockIdx.y * 64;
+  const int total = a.N * a.Pp;
+  const int j0 = xcd_remap(blockIdx.x, gridDim.x) * per;
+  const int j1 = min(total, j0 + per);
+  bf16x8 wf[2][4];
+  load_wfrag(a.w, cg, wf);
+  if (MODE == 1 && tid < 64) {
+    const int c = cg + tid;
+    if (a.bn.training && a.bn.ss) {
+      coef[tid] = a.bn.ss[c];
+      coef[64 + tid] = a.bn.ss[a.Cout + c];
+    } else {  // from the batch sums (or running statistics): every block alike
+      float m, inv, var;
+      bn_scale_shift(a.bn, c, coef[tid], coef[64 + tid], m, inv, var);
+      if (blockIdx.x == 0 && a.bn.training) {  // block 0 of the group: saved / running statistics
+        a.bn.save_mean[c] = m;
+        a.bn.save_invstd[c] = inv;
+        const double cnt = a.bn.count;
+        const float unb = (float)((double)var * (cnt / (cnt > 1.0 ? cnt - 1.0 : 1.0)));
+        a.bn.run_mean[c] = (1.f - a.bn.momentum) * a.bn.run_mean[c] + a.bn.momentum * m;
+        a.bn.run_var[c] = (1.f - a.bn.momentum) * a.bn.run_var[c] + a.bn.momentum * unb;
+      }
+    }
+  }
+  float q0[4][4], q1[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) q0[i][e] = q1[i][e] = 0.f;
+
+  // pooled row j: stem rows 2jp - extra .. 2jp + 1, input rows from 4jp - 3 - 2 extra
+  auto extra_of = [&](int j) { return (MODE == 1 && j == j0 && (j % a.Pp) > 0) ? 1 : 0; };
+  FwdPatch pf;
+  auto fetch = [&](int j) {
+    const int n = j / a.Pp, jp = j - n * a.Pp, ex = extra_of(j);
+    pf.fetch(a.img, a.H, a.W, n, 4 * jp - 3 - 2 * ex, 9 + 2 * ex, -3);
+  };
+  if (j0 < j1) fetch(j0);
+  TSTAMP(a.tim, 1);
+  for (int j = j0; j < j1; ++j) {
+    const int n = j / a.Pp, jp = j - n * a.Pp, ex = extra_of(j);
+    lds_sync();  // previous pooled row: patch, Xs and ring slots consumed
+    pf.store(patch, 9 + 2 * ex);
+    if (j + 1 < j1) fetch(j + 1);
+    for (int t = -ex; t < 2; ++t) {
+      const int h = 2 * jp + t;  // stem row
+      lds_sync();           // patch stored / previous round's Xs consumed
+      {  // im2col of row h: thread -> (pixel, half of the 8 chunks)
+        const int px = tid & (kRcNPX - 1), half = tid >> 8;
+        const int prow0 = 2 * (t + ex);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int kr = half * 4 + c;
+          const uint4 v = px < a.Q ? im2col_chunk<FwdPatch::PITCH>(patch, prow0, px, kr) : make_uint4(0, 0, 0, 0);
+          *reinterpret_cast<uint4*>(Xs + tt_off(px, kr * 8)) = v;
+        }
+      }
+      lds_sync();
+      f32x4 acc[4][2];
+      conv32(Xs, wave * 32, wf, acc);
+      const size_t rowpix = ((size_t)n * a.P + h) * a.Q;
+#pragma unroll
+      for (int j2 = 0; j2 < 2; ++j2) {
+        const int px = wave * 32 + j2 * 16 + li;
+        if (px >= a.Q) continue;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int co = i * 16 + 4 * g;
+          if constexpr (MODE == 0) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { q0[i][e] += acc[i][j2][e]; q1[i][e] += acc[i][j2][e] * acc[i][j2][e]; }
+            if (a.y) {
+              uint2 o;
+              o.x = pack_bf2(acc[i][j2][0], acc[i][j2][1]);
+              o.y = pack_bf2(acc[i][j2][2], acc[i][j2][3]);
+              *reinterpret_cast<uint2*>(a.y + (rowpix + px) * a.ldy + cg + co) = o;
+            }
+          } else {
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = stem_act(bf2f(f2bf(acc[i][j2][e])), coef[co + e], coef[64 + co + e]);
+            uint2 o;
+            o.x = pack_bf2(v[0], v[1]);
+            o.y = pack_bf2(v[2], v[3]);
+            *reinterpret_cast<uint2*>(ring + (h % 3) * (kRcNPX * 128) + ring_off(px, co)) = o;
+          }
+        }
+      }
+    }
+    if (j - j0 < 8) TSTAMP(a.tim, 2 + 2 * (j - j0));
+    if constexpr (MODE == 1) {
+      lds_sync();  // act rows 2jp-1 .. 2jp+1 in the ring
+      // act rows 2jp, 2jp+1 to HBM (whole 128-B pixel lines)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int h = 2 * jp + t;
+        const size_t rowpix = ((size_t)n * a.P + h) * a.Q;
+#pragma unroll
+        for (int it = 0; it < kRcNPX * 8 / kRcNT; ++it) {
+          const int i = tid + it * kRcNT, px = i >> 3, ch = i & 7;
+          if (px < a.Q)
+            *reinterpret_cast<uint4*>(a.act + (rowpix + px) * a.ldact + cg + ch * 8) =
+                *reinterpret_cast<const uint4*>(ring + (h % 3) * (kRcNPX * 128) + ring_off(px, ch * 8));
+        }
+      }
+      // MaxPool2d(3, 2, 1) of pooled row jp: first maximum in (kh, kw) scan
+      // order wins (strict >), NaN propagates (maxpool_fwd_kernel's rule)
+#pragma unroll
+      for (int it = 0; it < (kRcNPX / 2) * 8 / kRcNT; ++it) {
+        const int i = tid + it * kRcNT, q = i >> 3, ch = i & 7;
+        if (q >= a.Qp) continue;
+        float best[8];
+        int bi[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; bi[k] = -1; }
+#pragma unroll
+        for (int t9 = 0; t9 < 9; ++t9) {
+          const int kh = t9 / 3, kw = t9 % 3;
+          const int h = 2 * jp - 1 + kh, w = 2 * q - 1 + kw;
+          if (h < 0 || w < 0 || w >= a.Q) continue;
+          float v[8];
+          unpack8(*reinterpret_cast<const uint4*>(ring + (h % 3) * (kRcNPX * 128) + ring_off(w, ch * 8)), v);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const bool take = bi[k] < 0 || v[k] > best[k] || (v[k] != v[k] && best[k] == best[k]);
+            best[k] = take ? v[k] : best[k];
+            bi[k] = take ? t9 : bi[k];
+          }
+        }
+        const size_t opix = ((size_t)n * a.Pp + jp) * a.Qp + q;
+        *reinterpret_cast<uint4*>(a.pool + opix * a.ldpool + cg + ch * 8) = pack8(best);
+        uint2 ix;
+        ix.x = (unsigned)bi[0] | ((unsigned)bi[1] << 8) | ((unsigned)bi[2] << 16) | ((unsigned)bi[3] << 24);
+        ix.y = (unsigned)bi[4] | ((unsigned)bi[5] << 8) | ((unsigned)bi[6] << 16) | ((unsigned)bi[7] << 24);
+        *reinterpret_cast<uint2*>(a.idx + opix * a.Cout + cg + ch * 8) = ix;
+      }
+    }
+    if (j - j0 < 8) TSTAMP(a.tim, 3 + 2 * (j - j0));
+  }
+  TSTAMP(a.tim, 20);
+  if constexpr (MODE == 0) {
+    // fold over the 16 pixel lanes, then the 8 waves, then one replica atomic per channel
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          q0[i][e] += __shfl_xor(q0[i][e], o, 64);
+          q1[i][e] += __shfl_xor(q1[i][e], o, 64);
+        }
+    lds_sync();
+    float* red = reinterpret_cast<float*>(smem);  // [8 waves][64][2]
+    if (li == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = i * 16 + 4 * g + e;
+          red[(wave * 64 + c) * 2] = q0[i][e];
+          red[(wave * 64 + c) * 2 + 1] = q1[i][e];
+        }
+    }
+    lds_sync();
+    if (tid < 64) {
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int w = 0; w < kRcNT / 64; ++w) { s0 += red[(w * 64 + tid) * 2]; s1 += red[(w * 64 + tid) * 2 + 1]; }
+      double* rep = a.stats + (size_t)(blockIdx.x % kStatRep) * 2 * a.Cout + cg;
+      atomicAdd(rep + tid, (double)s0);
+      atomicAdd(rep + a.Cout + tid, (double)s1);
+    }
+    if (a.bn.ticket) {
+      int* flag = reinterpret_cast<int*>(smem + (kRcNT / 64) * 64 * 2 * sizeof(float));
+      if (last_block_arrive(a.bn.ticket, gridDim.x * gridDim.y, flag, tid < 64)) bn_finalize(a.bn);
+    }
+  }
+  TSTAMP(a.tim, 21);
+  TSTAMP_RT(a.tim, 31);
+}
+
+// ---------------------------------------------------------------------------
+// backward.  256 threads, 2 blocks per CU; a unit is one half row (128
+// pixels) of the stem output; a block owns units [u0, u1) of channel group
+// blockIdx.y.  All of a unit's global reads (the 1-2 pooled rows of dpool and
+// idx it needs, the skip gradient) are issued at the unit's start, into
+// registers, and land while the conv is recomputed; the pooled rows are then
+// staged in LDS and the maxpool backward gathers from there.
+// LDS: patch (7 x 264 bf16) | Xs im2col [128][64] | Ys y/xhat [128][64] |
+//      Ds dZ [128][64] | coefficients [4][64] f32 | Pd dpool [2][65][64] | Pi idx [2][65][64] u8
+// Waves: w>>1 = GEMM (0: dZ^T im, 1: xhat^T im), w&1 = 32-channel half; each
+// wave also sums im over pixels for k in [16w, 16w+16) (MFMA against ones).
+// ---------------------------------------------------------------------------
+constexpr int kRbNT = 256;
+constexpr int kRbNPX = 128;
+typedef Patch<kRbNPX, kRbNT, 8> BwdPatch;  // 7 x 262
+constexpr int kRbTile = kRbNPX * 128;
+constexpr int kRbPatchB = 7 * BwdPatch::PITCH * 2;
+constexpr int kRbPQ = kRbNPX / 2 + 1;                 // pooled columns a unit's pixels reach
+// LDS-DMA of the pooled rows, one 16-B piece per lane: dpool [r][qi][8 pieces],
+// idx [r][qi][4 pieces]; whole 1 KiB wave instructions
+constexpr int kRbPdIns = (2 * kRbPQ * 8 + 63) / 64, kRbPiIns = (2 * kRbPQ * 4 + 63) / 64;
+constexpr int kRbPd = kRbPdIns * 1024, kRbPi = kRbPiIns * 1024;
+constexpr int kRbLds = kRbPatchB + 3 * kRbTile + 4 * 64 * 4 + kRbPd + kRbPi;
+// per-block partial: [4 waves][9 tiles][64 lanes] f32x4 | [2][64] sum dZ, sum dZ xhat
+constexpr int kRbPartF4 = 4 * 9 * 64 + 32;
+
+__global__ void __launch_bounds__(kRbNT, 2) stem_rc_bwd_kernel(StemRcArgs a, int per) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* patch = reinterpret_cast<bf16_t*>(smem);
+  char* Xs = smem + kRbPatchB;
+  char* Ys = Xs + kRbTile;
+  char* Ds = Ys + kRbTile;
+  float* cf = reinterpret_cast<float*>(Ds + kRbTile);  // [4][64] scale, shift, mean, invstd
+  char* Pd = reinterpret_cast<char*>(cf + 4 * 64);
+  char* Pi = Pd + kRbPd;
+  TSTAMP_RT(a.tim, 30);
+  TSTAMP(a.tim, 0);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15, trq = li >> 2, trp = li & 3;
+  const int cg = blockIdx.y * 64;
+  const int segs = (a.Q + kRbNPX - 1) / kRbNPX;
+  const int total = a.N * a.P * segs;
+  const int u0 = xcd_remap(blockIdx.x, gridDim.x) * per;
+  const int u1 = min(total, u0 + per);
+  const int c8 = (tid & 7) * 8;  // this thread's 8 channels in the dZ phase (every item)
+  if (tid < 64) {
+    if (a.bn.ss) {
+      cf[tid] = a.bn.ss[cg + tid];
+      cf[64 + tid] = a.bn.ss[a.Cout + cg + tid];
+    } else {  // the forward's scale / shift, recomputed from the same batch sums
+      float m, inv, var;
+      bn_scale_shift(a.bn, cg + tid, cf[tid], cf[64 + tid], m, inv, var);
+    }
+    cf[128 + tid] = a.mean[cg + tid];
+    cf[192 + tid] = a.invstd[cg + tid];
+  }
+  float s1[8], s2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
+  f32x4 gacc[2][4], bacc;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) gacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bacc = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ones[k] = (__bf16)1.0f;
+
+  BwdPatch pf;
+  auto fetch = [&](int u) {
+    const int row = u / segs, s = u - row * segs;
+    const int n = row / a.P, h = row - n * a.P;
+    pf.fetch(a.img, a.H, a.W, n, 2 * h - 3, 7, 2 * s * kRbNPX - 3);
+  };
+  if (u0 < u1) fetch(u0);
+  TSTAMP(a.tim, 1);
+  int kt = 0;
+  for (int u = u0; u < u1; ++u, ++kt) {
+    const int row = u / segs, s = u - row * segs;
+    const int n = row / a.P, h = row - n * a.P;
+    const int q0 = s * kRbNPX, Qs = min(kRbNPX, a.Q - q0);
+    const size_t rowpix = ((size_t)n * a.P + h) * a.Q;
+    // pooled rows p_lo .. p_hi, columns qlo .. qhi reach this unit's pixels
+    const int p_lo = h >= 1 ? h / 2 : 0;
+    const int p_hi = min((h + 1) / 2, a.Pp - 1);
+    const int qlo = q0 / 2, qhi = min((q0 + Qs) / 2, a.Qp - 1);
+    const int nq = qhi - qlo + 1;
+    // the unit's pooled rows straight into LDS (DMA, no registers), waited for
+    // only at the dZ phase
+    {
+      const i32x4 rd = make_rsrc_sgpr(a.dpool, (unsigned)((size_t)a.N * a.Pp * a.Qp * a.lddpool * 2));
+      const i32x4 ri = make_rsrc_sgpr(a.idx, (unsigned)((size_t)a.N * a.Pp * a.Qp * a.Cout));
+      for (int ins = wave; ins < kRbPdIns + kRbPiIns; ins += kRbNT / 64) {
+        const bool isd = ins < kRbPdIns;
+        const int e = (isd ? ins : ins - kRbPdIns) * 64 + lane;
+        const int per_q = isd ? 8 : 4;
+        const int r = e / (kRbPQ * per_q), rem = e - r * (kRbPQ * per_q), qi = rem / per_q, pc = rem - qi * per_q;
+        const bool ok = r <= p_hi - p_lo && r < 2 && qi < nq;
+        const size_t opix = ((size_t)n * a.Pp + p_lo + r) * a.Qp + qlo + qi;
+        unsigned off = kOOB;
+        if (ok) off = isd ? (unsigned)((opix * a.lddpool + cg + pc * 8) * 2) : (unsigned)(opix * a.Cout + cg + pc * 16);
+        if (isd) glds16_asm(rd, Pd + ins * 1024, off, 0);
+        else glds16_asm(ri, Pi + (ins - kRbPdIns) * 1024, off, 0);
+      }
+    }
+    uint4 addv[kRbNPX * 8 / kRbNT];
+#pragma unroll
+    for (int it = 0; it < kRbNPX * 8 / kRbNT; ++it) {
+      const int px = (tid >> 3) + it * (kRbNT / 8);
+      addv[it] = px < Qs ? *reinterpret_cast<const uint4*>(a.add + (rowpix + q0 + px) * a.ldadd + cg + c8)
+                         : make_uint4(0, 0, 0, 0);
+    }
+    lds_sync();  // previous unit's GEMM reads done
+    pf.store(patch, 7);
+    lds_sync();
+    {
+      const int px = tid & (kRbNPX - 1), half = tid >> 7;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int kr = half * 4 + c;
+        const uint4 v = px < Qs ? im2col_chunk<BwdPatch::PITCH>(patch, 0, px, kr) : make_uint4(0, 0, 0, 0);
+        *reinterpret_cast<uint4*>(Xs + tt_off(px, kr * 8)) = v;
+      }
+    }
+    lds_sync();
+    if (kt < 4) TSTAMP(a.tim, 2 + 4 * kt);
+    {  // recompute y (bf16, as the forward rounded it) -> Ys
+      bf16x8 wf[2][4];  // re-read per unit (L1/L2-resident 8 KiB): live only across the conv
+      load_wfrag(a.w, cg, wf);
+      f32x4 acc[4][2];
+      conv32(Xs, wave * 32, wf, acc);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int px = wave * 32 + j * 16 + li;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          uint2 o;
+          o.x = pack_bf2(acc[i][j][0], acc[i][j][1]);
+          o.y = pack_bf2(acc[i][j][2], acc[i][j][3]);
+          *reinterpret_cast<uint2*>(Ys + tt_off(px, i * 16 + 4 * g)) = o;
+        }
+      }
+    }
+    wait_vmcnt<0>();  // the pooled rows (and the skip gradient) have landed ...
+    lds_sync();       // ... for every wave
+    if (kt < 4) TSTAMP(a.tim, 3 + 4 * kt);
+    // dZ = [act > 0] (sum of the pooled gradients whose argmax is this pixel +
+    // the skip gradient): maxpool_bwd_kernel's expression and order
+#pragma unroll
+    for (int it = 0; it < kRbNPX * 8 / kRbNT; ++it) {
+      // items one after the other (static addv[it] indexing, no cross-item
+      // interleaving that would hold four items' temporaries at once)
+      __builtin_amdgcn_sched_barrier(0);
+      const int px = (tid >> 3) + it * (kRbNT / 8);
+      const int w = q0 + px;
+      const bool valid = px < Qs;
+      const int qa = w >= 1 ? w / 2 : 0;
+      const int qb = min((w + 1) / 2, a.Qp - 1);
+      float acc[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int p = p_lo + (jj >> 1);
+        const int q = qa + (jj & 1);
+        const int kh = h - (2 * p - 1), kw = w - (2 * q - 1);
+        const bool ok = valid && p <= p_hi && q <= qb && kh >= 0 && kh <= 2 && kw >= 0 && kw <= 2;
+        if (!ok) continue;
+        const int want = kh * 3 + kw;
+        const int slot = (p - p_lo) * kRbPQ + (q - qlo);
+        const uint2 ix = *reinterpret_cast<const uint2*>(Pi + slot * 64 + c8);
+        float gv[8];
+        unpack8(*reinterpret_cast<const uint4*>(Pd + slot * 128 + c8 * 2), gv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const unsigned word = k < 4 ? ix.x : ix.y;
+          const int b = (word >> ((k & 3) * 8)) & 0xff;
+          if (b == want) acc[k] += gv[k];
+        }
+      }
+      {
+        float r[8];
+        unpack8(addv[it], r);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += r[k];
+      }
+      float y[8];
+      unpack8(*reinterpret_cast<const uint4*>(Ys + tt_off(px, c8)), y);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] = (valid && stem_act(y[k], cf[c8 + k], cf[64 + c8 + k]) > 0.f) ? acc[k] : 0.f;
+      const uint4 o = pack8(acc);
+      *reinterpret_cast<uint4*>(Ds + tt_off(px, c8)) = o;
+      if (a.dz && valid) *reinterpret_cast<uint4*>(a.dz + (rowpix + w) * a.lddz + cg + c8) = o;
+      float dz[8], xh[8];
+      unpack8(o, dz);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        xh[k] = (y[k] - cf[128 + c8 + k]) * cf[192 + c8 + k];
+        s1[k] += dz[k];
+        s2[k] += dz[k] * xh[k];
+      }
+      // the xhat operand of the third GEMM (zero rows past the row end: their
+      // im2col rows are zero too)
+      *reinterpret_cast<uint4*>(Ys + tt_off(px, c8)) = valid ? pack8(xh) : make_uint4(0, 0, 0, 0);
+    }
+    if (u + 1 < u1) fetch(u + 1);  // next unit's input patch, in flight during the GEMMs
+    lds_sync();
+    if (kt < 4) TSTAMP(a.tim, 4 + 4 * kt);
+    // GEMMs over the unit's pixels: D[co][k] += sum_px S[px][co] im[px][k]
+    {
+      const char* S = (wave >> 1) ? Ys : Ds;
+      const int cb = (wave & 1) * 32;
+#pragma unroll 1
+      for (int kk = 0; kk < kRbNPX / 32; ++kk) {
+        const int pl = kk * 32 + 8 * g + trq;
+        bf16x8 af[2], bf[4];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int col = cb + i * 16 + 4 * trp;
+          af[i] = tr8(S + tt_off(pl, col), S + tt_off(pl + 4, col));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int col = j * 16 + 4 * trp;
+          bf[j] = tr8(Xs + tt_off(pl, col), Xs + tt_off(pl + 4, col));
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) gacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], gacc[i][j], 0, 0, 0);
+        // sum over pixels of im[.][k], k in [16 wave, 16 wave + 16)
+        const bf16x8 bw = wave == 0 ? bf[0] : wave == 1 ? bf[1] : wave == 2 ? bf[2] : bf[3];
+        bacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bw, bacc, 0, 0, 0);
+      }
+    }
+    if (kt < 4) TSTAMP(a.tim, 5 + 4 * kt);
+  }
+  TSTAMP(a.tim, 20);
+  // partials of this block: fragments lane-contiguous, then the channel sums
+  f32x4* part = reinterpret_cast<f32x4*>(a.part) + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kRbPartF4;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) part[(wave * 9 + i * 4 + j) * 64 + lane] = gacc[i][j];
+  part[(wave * 9 + 8) * 64 + lane] = bacc;
+  lds_sync();  // LDS reuse
+  float* red = reinterpret_cast<float*>(smem);  // [32 rows][2][64]
+  const int r = tid >> 3;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    red[(r * 2 + 0) * 64 + c8 + k] = s1[k];
+    red[(r * 2 + 1) * 64 + c8 + k] = s2[k];
+  }
+  lds_sync();
+  if (tid < 128) {
+    const int q = tid >> 6, c = tid & 63;
+    float v = 0.f;
+    for (int rr = 0; rr < kRbNT / 8; ++rr) v += red[(rr * 2 + q) * 64 + c];
+    reinterpret_cast<float*>(part + 4 * 9 * 64)[q * 64 + c] = v;
+  }
+  TSTAMP(a.tim, 21);
+  TSTAMP_RT(a.tim, 31);
+}
+
+// fixed-order sums of the blocks' partials, in fp64: level 1 block (chunk,
+// seg, group) sums partials [16 seg, 16 seg + 16) of f32x4 units [64 chunk,
+// 64 chunk + 64) (4 split lanes of 4 partials, added in lane order); level 2
+// sums the segments the same way.  The finalise forms dW from the totals.
+constexpr int kRbSeg = 16;
+__global__ void __launch_bounds__(256) stem_rc_sum1_kernel(StemRcArgs a, int nblk, int nseg) {
+  __shared__ double sp[4][64][4];
+  const int tid = threadIdx.x, lane = tid & 63, sl = tid >> 6;
+  const int seg = blockIdx.y, grp = blockIdx.z;
+  const f32x4* part = reinterpret_cast<const f32x4*>(a.part) + (size_t)grp * nblk * kRbPartF4;
+  const int u = blockIdx.x * 64 + lane;
+  double d[4] = {0.0, 0.0, 0.0, 0.0};
+  if (u < kRbPartF4) {
+    const int b0 = seg * kRbSeg + sl * (kRbSeg / 4);
+    f32x4 v[kRbSeg / 4];
+#pragma unroll
+    for (int q = 0; q < kRbSeg / 4; ++q)
+      v[q] = b0 + q < nblk ? part[(size_t)(b0 + q) * kRbPartF4 + u] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < kRbSeg / 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) d[e] += (double)v[q][e];
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) sp[sl][lane][e] = d[e];
+  __syncthreads();
+  if (sl == 0 && u < kRbPartF4) {
+    double* o = a.l2 + (((size_t)grp * nseg + seg) * kRbPartF4 + u) * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = ((sp[0][lane][e] + sp[1][lane][e]) + sp[2][lane][e]) + sp[3][lane][e];
+  }
+}
+
+__global__ void __launch_bounds__(256) stem_rc_sum2_kernel(StemRcArgs a, int nseg) {
+  __shared__ double sp[4][64][4];
+  const int tid = threadIdx.x, lane = tid & 63, sl = tid >> 6;
+  const int grp = blockIdx.y;
+  const int u = blockIdx.x * 64 + lane;
+  double d[4] = {0.0, 0.0, 0.0, 0.0};
+  if (u < kRbPartF4) {
+    for (int s = sl; s < nseg; s += 4) {
+      const double* o = a.l2 + (((size_t)grp * nseg + s) * kRbPartF4 + u) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) d[e] += o[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) sp[sl][lane][e] = d[e];
+  __syncthreads();
+  if (sl == 0 && u < kRbPartF4) {
+    double* o = a.tot + ((size_t)grp * kRbPartF4 + u) * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = ((sp[0][lane][e] + sp[1][lane][e]) + sp[2][lane][e]) + sp[3][lane][e];
+  }
+}
+
+// dW[co][k] = k1 (A - m1 B - m2 X), dgamma = sum dZ xhat, dbeta = sum dZ
+// (one block per 64-channel group; totals [unit][4] fp64)
+__global__ void __launch_bounds__(256) stem_rc_finalize_kernel(StemRcArgs a) {
+  __shared__ double cA[64], cM1[64], cM2[64], bsum[64];
+  const int tid = threadIdx.x, grp = blockIdx.x, cg = grp * 64;
+  const double* tot = a.tot + (size_t)grp * kRbPartF4 * 4;
+  if (tid < 64) {
+    // channel sums: floats [0, 64) sum dZ, [64, 128) sum dZ xhat after the 2304 fragment units
+    const double s1 = tot[4 * 9 * 64 * 4 + tid], s2 = tot[4 * 9 * 64 * 4 + 64 + tid];
+    const double inv_n = 1.0 / (double)a.npix;
+    const int ch = cg + tid;
+    cA[tid] = (double)__fmul_rn(a.bn.gamma[ch], a.invstd[ch]);
+    cM1[tid] = s1 * inv_n;
+    cM2[tid] = s2 * inv_n;
+    a.dgamma[ch] = (float)s2;
+    a.dbeta[ch] = (float)s1;
+  } else if (tid < 128) {
+    // sum over pixels of im[.][k]: wave w's ones-tile holds k = 16 w + li in every row
+    const int k = tid - 64, w = k >> 4, li = k & 15;
+    bsum[k] = tot[((w * 9 + 8) * 64 + li) * 4];
+  }
+  __syncthreads();
+  // fragment units (wave, tile = i*4 + j, lane): co = (wave&1)*32 + i*16 + 4g + e, k = j*16 + li;
+  // waves 0/1 hold dZ^T im, waves 2/3 the matching xhat^T im
+  for (int u = tid; u < 2 * 8 * 64; u += 256) {
+    const int lane = u & 63, t = (u >> 6) & 7, w = u >> 9;
+    const int i = t >> 2, j = t & 3, g = lane >> 4, li = lane & 15;
+    const double* A = tot + ((w * 9 + t) * 64 + lane) * 4;
+    const double* X = tot + (((w + 2) * 9 + t) * 64 + lane) * 4;
+    const int k = j * 16 + li;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int co = (w & 1) * 32 + i * 16 + 4 * g + e;
+      a.dw[(size_t)(cg + co) * 64 + k] = (float)(cA[co] * (A[e] - cM1[co] * bsum[k] - cM2[co] * X[e]));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+static int rc_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  return cus;
+}
+
+bool stem_rc_ok(int Cout, int P, int Q) {
+  return Cout % 64 == 0 && Q <= kRcNPX && Q % 2 == 0 && P % 2 == 0 && Q >= 2;
+}
+
+hipError_t launch_stem_rc_fwd(const StemRcArgs& a, int mode, hipStream_t st) {
+  if (!stem_rc_ok(a.Cout, a.P, a.Q) || a.Pp * 2 != a.P || a.Qp * 2 != a.Q || a.H != 2 * a.P || a.W != 2 * a.Q)
+    return hipErrorInvalidValue;
+  const int groups = a.Cout / 64;
+  const int total = a.N * a.Pp;
+  if (mode == 0) {
+    if (!a.stats) return hipErrorInvalidValue;
+    const int want = 2 * rc_cus() / groups;
+    const int per = std::max(1, (total + want - 1) / want);
+    const size_t lds = kRcXs + kRcPatchB + 2 * 64 * sizeof(float);
+    conv_kernel_tag("stem_rc_fwd_kernel<0>");
+    hipLaunchKernelGGL(stem_rc_fwd_kernel<0>, dim3((total + per - 1) / per, groups), dim3(kRcNT), lds, st, a, per);
+  } else {
+    if (!a.act || !a.pool || !a.idx || (a.bn.training && !a.bn.stats)) return hipErrorInvalidValue;
+    const int want = rc_cus() / groups;
+    const int per = std::max(1, (total + want - 1) / want);
+    const size_t lds = kRcRing + kRcXs + kRcPatchB + 2 * 64 * sizeof(float);
+    conv_kernel_tag("stem_rc_fwd_kernel<1>");
+    hipLaunchKernelGGL(stem_rc_fwd_kernel<1>, dim3((total + per - 1) / per, groups), dim3(kRcNT), lds, st, a, per);
+  }
+  return hipGetLastError();
+}
+
+int stem_rc_bwd_blocks(int N, int P, int Q, int Cout) {
+  const int segs = (Q + kRbNPX - 1) / kRbNPX;
+  const int total = N * P * segs;
+  const int groups = Cout / 64;
+  const int want = std::max(1, 2 * rc_cus() / groups);
+  const int per = std::max(1, (total + want - 1) / want);
+  return (total + per - 1) / per;
+}
+static int rc_nseg(int nblk) { return (nblk + kRbSeg - 1) / kRbSeg; }
+size_t stem_rc_part_bytes(int N, int P, int Q, int Cout) {
+  const int nblk = stem_rc_bwd_blocks(N, P, Q, Cout), groups = Cout / 64;
+  return (size_t)nblk * groups * kRbPartF4 * 16 + (size_t)rc_nseg(nblk) * groups * kRbPartF4 * 32;
+}
+size_t stem_rc_tot_bytes(int Cout) { return (size_t)(Cout / 64) * kRbPartF4 * 32; }
+size_t stem_rc_l2_offset(int N, int P, int Q, int Cout) {
+  return (size_t)stem_rc_bwd_blocks(N, P, Q, Cout) * (Cout / 64) * kRbPartF4 * 16;
+}
+
+hipError_t launch_stem_rc_bwd(const StemRcArgs& a, int stage, hipStream_t st) {
+  if (!stem_rc_ok(a.Cout, a.P, a.Q) || a.Pp * 2 != a.P || a.Qp * 2 != a.Q || a.H != 2 * a.P || a.W != 2 * a.Q ||
+      !a.part || !a.l2 || !a.tot || !a.dw || !a.bn.training || !a.bn.stats || a.lddpool % 8 || a.ldadd % 8)
+    return hipErrorInvalidValue;
+  const int groups = a.Cout / 64;
+  const int segs = (a.Q + kRbNPX - 1) / kRbNPX;
+  const int total = a.N * a.P * segs;
+  const int blocks = stem_rc_bwd_blocks(a.N, a.P, a.Q, a.Cout);
+  const int per = (total + blocks - 1) / blocks;
+  const int nseg = rc_nseg(blocks);
+  const int chunks = (kRbPartF4 + 63) / 64;
+  if (stage == 0) {
+    conv_kernel_tag("stem_rc_bwd_kernel");
+    hipLaunchKernelGGL(stem_rc_bwd_kernel, dim3(blocks, groups), dim3(kRbNT), kRbLds, st, a, per);
+  } else {
+    conv_kernel_tag("stem_rc_sum1/sum2/finalize");
+    hipLaunchKernelGGL(stem_rc_sum1_kernel, dim3(chunks, nseg, groups), dim3(256), 0, st, a, blocks, nseg);
+    hipLaunchKernelGGL(stem_rc_sum2_kernel, dim3(chunks, groups), dim3(256), 0, st, a, nseg);
+    hipLaunchKernelGGL(stem_rc_finalize_kernel, dim3(groups), dim3(256), 0, st, a);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace unet

@@ -86,14 +86,9 @@ def preprocess(images, masks=None, img_size: Tuple[int, int] = (256, 256), norma
     ow, oh = img_size
     x = _frames(images, device)
     n, h, w = x.shape
-    if oh > h or ow > w:
-        # cv2.resize(INTER_AREA) falls back to an area-weighted bilinear
-        # interpolation when enlarging; only the downscaling area path (the
-        # reference's microscopy frames are larger than img_size) is built
-        raise NotImplementedError(
-            f"preprocess: frames {h}x{w} are smaller than img_size {oh}x{ow}; INTER_AREA upscaling "
-            "(dataset.py:51) is not implemented on the GPU path")
     if (h, w) != (oh, ow):
+        # INTER_AREA: the area average when shrinking both axes, OpenCV's
+        # fixed-point area-mode linear resize when an axis is enlarged
         r = torch.empty((n, oh, ow), dtype=torch.uint8, device=device)
         _lib.check(lib.unet_resize_area_u8(x.data_ptr(), n, h, w, r.data_ptr(), oh, ow, st), "unet_resize_area_u8")
         x = r

@@ -26,7 +26,9 @@ are PARITY UNPINNED; numpy's percentile is pinned against numpy itself):
   integer factors: ``resizeAreaFast_`` = integer block sum * (1/area) in float,
   ``cvRound``; otherwise ``computeResizeAreaTab`` coverage weights (float
   alpha per source column / row) accumulated horizontally then vertically in
-  float, ``cvRound``.  INTER_NEAREST: ``sx = min(floor(dx * (ssize/dsize)), ssize-1)``.
+  float, ``cvRound``.  Enlarging (either axis): resizeGeneric_ with the
+  area_mode linear coefficients, fixed point (``resize_area_up_u8``).
+  INTER_NEAREST: ``sx = min(floor(dx * (ssize/dsize)), ssize-1)``.
 * ``cv2.CLAHE`` (imgproc/src/clahe.cpp, 8-bit path): tile grid 8x8 (BORDER_REFLECT_101
   padding when either side is not a multiple of the grid: both sides by
   ``grid - size % grid``, so a side that is a multiple gains a whole tile), clip limit max(int(2.0 * tileArea / 256), 1),
@@ -92,7 +94,7 @@ def resize_area_u8(img: np.ndarray, oh: int, ow: int) -> np.ndarray:
     if oh == h and ow == w:
         return img.copy()
     if oh > h or ow > w:
-        raise NotImplementedError("INTER_AREA upscaling is not on the reference path (images are downscaled)")
+        return resize_area_up_u8(img, oh, ow)
     sx, sy = _cv_scale(w, ow), _cv_scale(h, oh)
     eps = np.finfo(np.float64).eps
     if abs(sx - round(sx)) < eps and abs(sy - round(sy)) < eps:  # is_area_fast: resizeAreaFast_
@@ -122,6 +124,50 @@ def resize_area_u8(img: np.ndarray, oh: int, ow: int) -> np.ndarray:
                 acc = (acc + (buf * beta).astype(np.float32)).astype(np.float32)
         out[dy] = np.clip(_cv_round(acc), 0, 255).astype(np.uint8)
     return out
+
+
+def _area_linear_coefs(ssize: int, dsize: int):
+    """resizeGeneric's INTER_AREA (area_mode) linear coefficients of one axis:
+    sx = floor(d * scale), f = (float)((d + 1) - (sx + 1) * inv_scale),
+    f = f <= 0 ? 0 : f - floor(f); fixed point saturate_cast<short>(cbuf * 2048)
+    with cbuf = {1.f - f, f} (float); 'edge' marks sx + 1 >= ssize (the
+    horizontal pass then takes S[sx] * 2048, the vertical pass clips the row)."""
+    inv = dsize / ssize
+    scale = 1.0 / inv
+    sx = np.empty(dsize, np.int64)
+    c0 = np.empty(dsize, np.int64)
+    c1 = np.empty(dsize, np.int64)
+    for d in range(dsize):
+        s = math.floor(d * scale)
+        f = np.float32((d + 1) - (s + 1) * inv)
+        f = np.float32(0.0) if f <= 0 else np.float32(f - np.float32(math.floor(f)))
+        if s >= ssize - 1:
+            s = ssize - 1
+        sx[d] = s
+        c0[d] = int(np.rint(np.float32(np.float32(1.0) - f) * np.float32(2048.0)))
+        c1[d] = int(np.rint(f * np.float32(2048.0)))
+    return sx, c0, c1
+
+
+def resize_area_up_u8(img: np.ndarray, oh: int, ow: int) -> np.ndarray:
+    """cv2.resize(img, (ow, oh), interpolation=cv2.INTER_AREA) for uint8 when
+    either axis is enlarged: OpenCV (imgproc/src/resize.cpp, the generic
+    non-IPP path) then runs resizeGeneric_ with area_mode coefficients
+    (_area_linear_coefs) in fixed point: HResizeLinear D = S[sx] a0 + S[sx+1] a1
+    (D = S[sx] * 2048 past the last full pair), VResizeLinear
+    ((b0 (D0 >> 4)) >> 16) + ((b1 (D1 >> 4)) >> 16) + 2) >> 2 with rows
+    clip(sy + k, 0, H-1)."""
+    h, w = img.shape
+    xs, a0, a1 = _area_linear_coefs(w, ow)
+    ys, b0, b1 = _area_linear_coefs(h, oh)
+    src = img.astype(np.int64)
+    edge = xs >= w - 1
+    x1 = np.minimum(xs + 1, w - 1)
+    hres = np.where(edge[None, :], src[:, xs] * 2048, src[:, xs] * a0[None, :] + src[:, x1] * a1[None, :])
+    r0 = hres[np.minimum(ys, h - 1)]
+    r1 = hres[np.minimum(ys + 1, h - 1)]
+    out = (((b0[:, None] * (r0 >> 4)) >> 16) + ((b1[:, None] * (r1 >> 4)) >> 16) + 2) >> 2
+    return out.astype(np.uint8)
 
 
 def resize_nearest_u8(img: np.ndarray, oh: int, ow: int) -> np.ndarray:

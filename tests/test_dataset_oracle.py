@@ -46,6 +46,21 @@ def test_area_fractional_factor_preserves_constant_and_mean():
     assert abs(out.astype(np.float64).mean() - img.mean()) < 1.0
 
 
+def test_area_upscale_hand_values():
+    """INTER_AREA enlarging (OpenCV's area-mode linear coefficients, fixed
+    point): x2 and x3 repeat pixels, x1.5 blends the middle column half/half,
+    a constant image stays constant, mixed shrink/grow keeps the mean."""
+    row = np.array([[0, 100]], np.uint8)
+    assert D.resize_area_u8(row, 1, 4).tolist() == [[0, 0, 100, 100]]
+    assert D.resize_area_u8(row, 1, 6).tolist() == [[0, 0, 0, 100, 100, 100]]
+    assert D.resize_area_u8(row, 1, 3).tolist() == [[0, 50, 100]]
+    assert np.all(D.resize_area_u8(np.full((5, 7), 173, np.uint8), 9, 11) == 173)
+    rng = np.random.default_rng(3)
+    img = rng.integers(0, 256, size=(60, 30), dtype=np.uint8)
+    out = D.resize_area_u8(img, 40, 70)
+    assert out.shape == (40, 70) and abs(out.astype(np.float64).mean() - img.mean()) < 3.0
+
+
 def test_clahe_properties():
     assert np.unique(D.clahe_u8(np.full((64, 64), 90, np.uint8))).size == 1
     rng = np.random.default_rng(3)
