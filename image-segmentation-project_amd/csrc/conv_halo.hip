@@ -33,6 +33,7 @@
 // fragment (16 px of one output row x 32 c); each wave owns RW output rows x
 // COT channels (acc[RW][FN]).
 #include <cstdio>
+#include <cstdlib>
 
 #include "common.h"
 #include "kernels.h"
@@ -409,7 +410,7 @@ __device__ __forceinline__ void commit_stats(const ConvFwdArgs& a, float (&q0)[F
 // weight-stationary (C = 32 * NP <= 96)
 // ---------------------------------------------------------------------------
 template <int NP, int FN, int TH, int NW, bool FLIP>
-__global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int ntiles, int ncg) {
+__global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int ntiles, int ncg, int split) {
   constexpr int COT = FN * 16;               // output channels per block
   constexpr int RW = TH / NW;                // output rows per wave
   constexpr int HPR = ((TH + 2) * kHW + 15) / 16 * 16;
@@ -432,7 +433,12 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
   const int nslot = gridDim.x / ncg;
   const int co0 = cg * COT;
   const int tq = a.Q >> 4, tp = a.P / TH;
-  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
+  // halo DMA as inline asm (untracked by the compiler): with the builtin,
+  // hipcc puts an s_waitcnt vmcnt(0) in front of every LDS store that follows
+  // it (the BN transform of the staged halo) -- each one draining the next
+  // tile's halo AND every activation store still in flight.  The kernel
+  // waits for its DMA itself (wait_vmcnt before the tile barrier).
+  const i32x4 xr = make_rsrc_sgpr(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
   const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (unsigned)((size_t)a.Cout * 9 * a.C * 2));
 
   issue_weight_dma<COT, NW>(a, wr, wl, co0, 0, NP, wave, lane);  // all 9 taps, once
@@ -480,7 +486,7 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
       unsigned off = kOOB;
       if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
         off = (unsigned)((((n * a.H + ih) * a.W + iw) * a.ldx + hch[k]) * 2);
-      glds16(xr, dst + (wave + k * NW) * 1024, off);
+      glds16_asm(xr, dst + (wave + k * NW) * 1024, off, 0u);
     }
   };
 
@@ -501,6 +507,89 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
   __syncthreads();
   TSTAMP(a.tim, 1);
 
+  if (NW == 8 && !FLIP && split && !a.xform) {  // (dgrads: the held epilogue operands would spill)
+    // Two wave groups half a tile apart: waves 0-3 (A) and 4-7 (B) sit on the
+    // same four SIMDs (one of each per SIMD), and each half phase one group
+    // issues its MFMAs while the other runs its epilogue, so the matrix cores
+    // no longer idle through the stores / BN sums / address math.
+    //   A: | MFMA(t)     |Bar| epi(t)     |Bar'| MFMA(t+1) ...
+    //   B: | epi(t-1)    |Bar| MFMA(t)    |Bar'| epi(t)    ...
+    // Bar' (top): halo(t) landed in every wave's DMA part.  Bar: every MFMA of
+    // tile t-1 (and A's of tile t) is done, so halo(t+1) may go into the
+    // buffer tile t-1 used; it has half a tile to land.
+    const bool grpB = wave >= NW / 2;
+    const bool vec_all = (a.ldy % 8 == 0) && (!a.ysplit || (a.ldysplit % 8 == 0 && a.csplit % 8 == 0)) &&
+                         a.Cout % COT == 0;  // A's epilogue: exactly RW * FN / 2 stores per wave
+    TileEpi<FN, RW, FLIP, PREF, false> epi;  // operands of the tile whose epilogue is pending
+    size_t pix[RW];
+    f32x4 acc[RW][FN];
+    int k = 0;
+    for (; t < ntiles; ++k, t += nslot) {
+      const int b = k & 1;
+      if (k > 0) {
+        // this wave's part of halo(t) has landed; A's epilogue stores, issued
+        // after it, may stay in flight
+        if (!grpB && vec_all) wait_vmcnt<RW * FN / 2>();
+        else wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+      }
+      if (k < 9) TSTAMP(a.tim, 2 + 2 * k);
+      int n, oh0, ow0;
+      tile_origin(t, n, oh0, ow0);
+      size_t pt[RW];
+#pragma unroll
+      for (int j = 0; j < RW; ++j) pt[j] = ((size_t)n * a.P + oh0 + wave * RW + j) * a.Q + ow0 + (lane & 15);
+      const char* H = hl + b * HBUF;
+      if (!grpB) {
+        if (PREF) epi.fetch(a, pt, co0, lane);
+#pragma unroll
+        for (int j = 0; j < RW; ++j)
+#pragma unroll
+          for (int i = 0; i < FN; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int p = 0; p < (UNET_ABL == 1 ? 0 : NP); ++p)
+          mfma_panel<FN, RW, NP * COT * 64, FLIP>(acc, wl + p * COT * 64, H + p * PANEL, aoff, boff);
+#pragma unroll
+        for (int j = 0; j < RW; ++j) pix[j] = pt[j];
+      } else if (k > 0) {
+        if (!PREF) epi.fetch(a, pix, co0, lane);
+        epi.landed();
+        epi.store(a, acc, pix, co0, lane, cst, q0, q1, q2);
+      }
+      __builtin_amdgcn_s_barrier();
+      if (k < 9) TSTAMP(a.tim, 3 + 2 * k);
+      if (!grpB) {
+        if (!PREF) epi.fetch(a, pix, co0, lane);
+        epi.landed();  // before this wave's DMA part: waits for tile t's operands only
+      } else if (PREF) {
+        epi.fetch(a, pt, co0, lane);
+      }
+      if (t + nslot < ntiles && UNET_ABL != 2) {
+        int n2, oh2, ow2;
+        tile_origin(t + nslot, n2, oh2, ow2);
+        issue_halo(hl + (b ^ 1) * HBUF, n2, oh2, ow2);
+      }
+      if (!grpB) {
+        epi.store(a, acc, pix, co0, lane, cst, q0, q1, q2);
+      } else {
+#pragma unroll
+        for (int j = 0; j < RW; ++j)
+#pragma unroll
+          for (int i = 0; i < FN; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int p = 0; p < (UNET_ABL == 1 ? 0 : NP); ++p)
+          mfma_panel<FN, RW, NP * COT * 64, FLIP>(acc, wl + p * COT * 64, H + p * PANEL, aoff, boff);
+#pragma unroll
+        for (int j = 0; j < RW; ++j) pix[j] = pt[j];
+      }
+    }
+    if (grpB && k > 0) {  // B's last tile
+      if (!PREF) epi.fetch(a, pix, co0, lane);
+      epi.landed();
+      epi.store(a, acc, pix, co0, lane, cst, q0, q1, q2);
+    }
+    wait_vmcnt<0>();
+  } else
   for (int k = 0; t < ntiles; ++k, t += nslot) {
     const int b = k & 1;
     if (t + nslot < ntiles && UNET_ABL != 2) {  // lands while this tile computes
@@ -519,7 +608,11 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
       // relu(y * scale + shift) of every in-image halo pixel, in place (the
       // zero-filled conv padding stays 0); the interior is the stored activation
       char* Hb = hl + b * HBUF;
-      for (int idx = tid; idx < NP * HPR * 4; idx += NW * 64) {
+      constexpr int XI = (NP * HPR * 4 + NW * 64 - 1) / (NW * 64);  // fixed trip count: unrolled,
+#pragma unroll                                                       // every LDS read issued up front
+      for (int it = 0; it < XI; ++it) {
+        const int idx = tid + it * NW * 64;
+        if (idx >= NP * HPR * 4) break;
         const int p = idx / (HPR * 4), rem = idx - p * (HPR * 4);
         const int row = rem >> 2, ch = rem & 3;
         if (row >= (TH + 2) * kHW) continue;
@@ -536,11 +629,12 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
         for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
         const uint4 o = pack8(v);
         *q = o;
-        if (cg == 0 && hr >= 1 && hr <= TH && hc >= 1 && hc <= 16)
+        if (cg == 0 && hr >= 1 && hr <= TH && hc >= 1 && hc <= 16 && UNET_ABL != 4)
           *reinterpret_cast<uint4*>(a.xh + (((size_t)n * a.H + ih) * a.W + iw) * a.ldxh + c0) = o;
       }
       lds_barrier();  // transformed halo visible to every wave (DMA / h stores stay in flight)
     }
+    if (UNET_ABL >= 3 && k < 3) TSTAMP(a.tim, 2 + 5 * k);
     const char* H = hl + b * HBUF;
     f32x4 acc[RW][FN];
 #pragma unroll
@@ -552,17 +646,17 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
       mfma_panel<FN, RW, NP * COT * 64, FLIP>(acc, wl + p * COT * 64, H + p * PANEL, aoff, boff);
     // stamps: 2 per tile (after the MFMAs, after the epilogue); UNET_ABL == 3
     // (fine build): 4 per tile for the first 4 tiles (+ after the wait, after the barrier)
-    if (UNET_ABL >= 3 ? k < 4 : k < 9) TSTAMP(a.tim, UNET_ABL >= 3 ? 2 + 4 * k : 2 + 2 * k);
+    if (UNET_ABL >= 3 ? k < 3 : k < 9) TSTAMP(a.tim, UNET_ABL >= 3 ? 3 + 5 * k : 2 + 2 * k);
     if (!PREF) epi.fetch(a, pix, co0, lane);
     epi.landed();
     wait_vmcnt<0>();               // the next tile's halo (issued before this tile's MFMAs) has landed ...
-    if (UNET_ABL >= 3 && k < 4) TSTAMP(a.tim, 3 + 4 * k);
+    if (UNET_ABL >= 3 && k < 3) TSTAMP(a.tim, 4 + 5 * k);
     __builtin_amdgcn_s_barrier();  // ... everyone's part; buffer b is free for reuse
-    if (UNET_ABL >= 3 && k < 4) TSTAMP(a.tim, 4 + 4 * k);
+    if (UNET_ABL >= 3 && k < 3) TSTAMP(a.tim, 5 + 5 * k);
     // the stores go out AFTER the wait: they drain under the next tile's MFMAs
     // instead of being waited for here (vmcnt counts stores too)
     epi.store(a, acc, pix, co0, lane, cst, q0, q1, q2);
-    if (UNET_ABL >= 3 ? k < 4 : k < 9) TSTAMP(a.tim, UNET_ABL >= 3 ? 5 + 4 * k : 3 + 2 * k);
+    if (UNET_ABL >= 3 ? k < 3 : k < 9) TSTAMP(a.tim, UNET_ABL >= 3 ? 6 + 5 * k : 3 + 2 * k);
   }
   TSTAMP(a.tim, 20);
   if (a.stats || a.bb.sums) commit_stats<FN, NW, false>(a, q0, q1, q2, co0, smem);
@@ -973,8 +1067,12 @@ static hipError_t launch_ws(const ConvFwdArgs& a, hipStream_t st) {
   char tag[96];
   std::snprintf(tag, sizeof(tag), "conv3x3_ws_kernel<%d, %d, %d, %d, %s>", NP, FN, TH, NW, FLIP ? "true" : "false");
   conv_kernel_tag(tag);
+  // wave-group split schedule (conv3x3_ws_kernel, 8-wave shapes without the BN
+  // prologue), off by default: measured 0.5% slower end to end (2668 vs 2682 img/s,
+  // interleaved A/B); UNET_WS_SPLIT=1 selects it
+  static const int split = std::getenv("UNET_WS_SPLIT") ? std::atoi(std::getenv("UNET_WS_SPLIT")) : 0;
   hipLaunchKernelGGL((conv3x3_ws_kernel<NP, FN, TH, NW, FLIP>), dim3(slots * ncg), dim3(NW * 64), lds, st, a,
-                     ntiles, ncg);
+                     ntiles, ncg, split);
   return hipGetLastError();
 }
 
@@ -1033,6 +1131,7 @@ static hipError_t launch_halo_shape(const ConvFwdArgs& a, hipStream_t st) {
   if (wscfg == 1 && C == 64 && Co % 32 == 0 && a.P % 4 == 0) return launch_ws<2, 2, 4, 4, FLIP>(a, st);
   if (wscfg == 2 && C == 64 && Co % 32 == 0 && a.P % 8 == 0) return launch_ws<2, 2, 8, 4, FLIP>(a, st);
   if (wscfg == 3 && C == 64 && Co % 32 == 0 && a.P % 8 == 0) return launch_ws<2, 2, 8, 8, FLIP>(a, st);
+  if (wscfg == 4 && C == 64 && Co % 64 == 0 && a.P % 16 == 0) return launch_ws<2, 4, 16, 4, FLIP>(a, st);
   if (C == 64 && Co % 64 == 0 && a.P % 16 == 0) return launch_ws<2, 4, 16, 8, FLIP>(a, st);
   // decoder1 shapes (256^2, 96 / 32 channels), UNET_D1CFG sweep on the Base
   // config: 8-row tiles on 8 waves (one row each, two waves per SIMD hide each

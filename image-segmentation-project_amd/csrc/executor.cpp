@@ -1801,6 +1801,7 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     s.part = x.W<float>(p->stem_part);
     s.l2 = reinterpret_cast<double*>(s.part + stem_rc_l2_offset(N, p->y0.H, p->y0.W, p->x1.C) / sizeof(float));
     s.tot = x.W<double>(p->stem_tot);
+    s.imsum = reinterpret_cast<float*>(s.tot + (size_t)(p->x1.C / 64) * (4 * 9 * 64 + 32) * 4);
     s.dw = x.W<float>(p->convs[p->stem_conv].wacc);
     s.dgamma = sb.dgamma; s.dbeta = sb.dbeta;
     s.npix = (int64_t)N * p->y0.H * p->y0.W;

@@ -294,6 +294,7 @@ struct StemRcArgs {
   const float* mean; const float* invstd;   // saved batch statistics
   bf16_t* dz; int lddz;
   float* part; double* l2; double* tot;   // partials, fp64 level-1 sums, fp64 totals
+  float* imsum;                      // [256] fixed-order block sums of img (backward centring)
   float* dw; float* dgamma; float* dbeta;
   int64_t npix;
   unsigned long long* tim;           // phase stamps (debug build only)
@@ -303,7 +304,7 @@ hipError_t launch_stem_rc_fwd(const StemRcArgs& a, int mode, hipStream_t st);
 // stage 0: the fused backward pass; stage 1: the fixed-order reduce + finalise
 hipError_t launch_stem_rc_bwd(const StemRcArgs& a, int stage, hipStream_t st);
 size_t stem_rc_part_bytes(int N, int P, int Q, int Cout);  // a.part followed by a.l2
-size_t stem_rc_tot_bytes(int Cout);                        // a.tot
+size_t stem_rc_tot_bytes(int Cout);                        // a.tot followed by a.imsum
 size_t stem_rc_l2_offset(int N, int P, int Q, int Cout);   // bytes from a.part to a.l2
 
 // fused ConvTranspose2d(k2,s2, Cin->16) + Conv1x1(16->1): logits[2i+a,2j+b] =

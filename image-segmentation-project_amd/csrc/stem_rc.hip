@@ -19,6 +19,8 @@
 //                  dY = k1 dZ - k1 m1 - k1 m2 xhat       (k1 = gamma invstd,
 //                  m1 = mean dZ, m2 = mean dZ xhat), so
 //                  dW[co][k] = k1 (sum dZ im - m1 sum im - m2 sum xhat im)
+//                with im centred by a per-block column mean (sum dY = 0 makes
+//                dW independent of it; it keeps the m1 term from cancelling)
 //                three GEMMs over the pixels whose coefficients are only known
 //                at the end: each block leaves its partial sums (dZ^T im,
 //                xhat^T im, sum im, sum dZ, sum dZ xhat), a fixed-order reduce
@@ -353,6 +355,25 @@ __global__ void __launch_bounds__(kRcNT) stem_rc_fwd_kernel(StemRcArgs a, int pe
   TSTAMP_RT(a.tim, 31);
 }
 
+// Block sums of the input image in a fixed order (the backward's im2col
+// centring value): block b sums elements b, b + G, b + 2G, ... per thread in
+// order, then a fixed tree.
+constexpr int kRcImBlocks = 256;
+__global__ void __launch_bounds__(256) stem_rc_imsum_kernel(StemRcArgs a) {
+  __shared__ float red[256];
+  const size_t n = (size_t)a.N * a.H * a.W;
+  const size_t stride = (size_t)kRcImBlocks * 256;
+  float s = 0.f;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) s += a.img[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) a.imsum[blockIdx.x] = red[0];
+}
+
 // ---------------------------------------------------------------------------
 // backward.  256 threads, 2 blocks per CU; a unit is one half row (128
 // pixels) of the stem output; a block owns units [u0, u1) of channel group
@@ -375,7 +396,7 @@ constexpr int kRbPQ = kRbNPX / 2 + 1;                 // pooled columns a unit's
 // idx [r][qi][4 pieces]; whole 1 KiB wave instructions
 constexpr int kRbPdIns = (2 * kRbPQ * 8 + 63) / 64, kRbPiIns = (2 * kRbPQ * 4 + 63) / 64;
 constexpr int kRbPd = kRbPdIns * 1024, kRbPi = kRbPiIns * 1024;
-constexpr int kRbLds = kRbPatchB + 3 * kRbTile + 4 * 64 * 4 + kRbPd + kRbPi;
+constexpr int kRbLds = kRbPatchB + 3 * kRbTile + 5 * 64 * 4 + kRbPd + kRbPi;
 // per-block partial: [4 waves][9 tiles][64 lanes] f32x4 | [2][64] sum dZ, sum dZ xhat
 constexpr int kRbPartF4 = 4 * 9 * 64 + 32;
 
@@ -385,8 +406,9 @@ __global__ void __launch_bounds__(kRbNT, 2) stem_rc_bwd_kernel(StemRcArgs a, int
   char* Xs = smem + kRbPatchB;
   char* Ys = Xs + kRbTile;
   char* Ds = Ys + kRbTile;
-  float* cf = reinterpret_cast<float*>(Ds + kRbTile);  // [4][64] scale, shift, mean, invstd
-  char* Pd = reinterpret_cast<char*>(cf + 4 * 64);
+  // [5][64] scale, shift, mean, invstd | mu: the block's im2col column means
+  float* cf = reinterpret_cast<float*>(Ds + kRbTile);
+  char* Pd = reinterpret_cast<char*>(cf + 5 * 64);
   char* Pi = Pd + kRbPd;
   TSTAMP_RT(a.tim, 30);
   TSTAMP(a.tim, 0);
@@ -408,6 +430,15 @@ __global__ void __launch_bounds__(kRbNT, 2) stem_rc_bwd_kernel(StemRcArgs a, int
     }
     cf[128 + tid] = a.mean[cg + tid];
     cf[192 + tid] = a.invstd[cg + tid];
+    // mu[k]: the image mean (fixed-order sum of stem_rc_imsum_kernel's block
+    // sums, the same in every block) for the 49 real taps, 0 for the padding.
+    // The weight-gradient GEMMs run on im - mu: sum_px dY = 0 makes dW
+    // independent of mu, and centring removes the common mode that m1 * sum(im)
+    // would otherwise cancel against dZ^T im (fp32 accumulation).
+    double sum = 0.0;
+    for (int b = 0; b < kRcImBlocks; ++b) sum += (double)a.imsum[b];
+    const float mu = bf2f(f2bf((float)(sum / ((double)a.N * a.H * a.W))));
+    cf[256 + tid] = ((tid & 7) < 7 && (tid >> 3) < 7) ? mu : 0.f;
   }
   float s1[8], s2[8];
 #pragma unroll
@@ -558,6 +589,13 @@ __global__ void __launch_bounds__(kRbNT, 2) stem_rc_bwd_kernel(StemRcArgs a, int
       // the xhat operand of the third GEMM (zero rows past the row end: their
       // im2col rows are zero too)
       *reinterpret_cast<uint4*>(Ys + tt_off(px, c8)) = valid ? pack8(xh) : make_uint4(0, 0, 0, 0);
+      if (valid) {  // im2col row chunk of this pixel, centred (the conv has read it)
+        float im[8];
+        unpack8(*reinterpret_cast<const uint4*>(Xs + tt_off(px, c8)), im);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) im[k] -= cf[256 + c8 + k];
+        *reinterpret_cast<uint4*>(Xs + tt_off(px, c8)) = pack8(im);
+      }
     }
     if (u + 1 < u1) fetch(u + 1);  // next unit's input patch, in flight during the GEMMs
     lds_sync();
@@ -765,14 +803,14 @@ size_t stem_rc_part_bytes(int N, int P, int Q, int Cout) {
   const int nblk = stem_rc_bwd_blocks(N, P, Q, Cout), groups = Cout / 64;
   return (size_t)nblk * groups * kRbPartF4 * 16 + (size_t)rc_nseg(nblk) * groups * kRbPartF4 * 32;
 }
-size_t stem_rc_tot_bytes(int Cout) { return (size_t)(Cout / 64) * kRbPartF4 * 32; }
+size_t stem_rc_tot_bytes(int Cout) { return (size_t)(Cout / 64) * kRbPartF4 * 32 + kRcImBlocks * sizeof(float); }
 size_t stem_rc_l2_offset(int N, int P, int Q, int Cout) {
   return (size_t)stem_rc_bwd_blocks(N, P, Q, Cout) * (Cout / 64) * kRbPartF4 * 16;
 }
 
 hipError_t launch_stem_rc_bwd(const StemRcArgs& a, int stage, hipStream_t st) {
   if (!stem_rc_ok(a.Cout, a.P, a.Q) || a.Pp * 2 != a.P || a.Qp * 2 != a.Q || a.H != 2 * a.P || a.W != 2 * a.Q ||
-      !a.part || !a.l2 || !a.tot || !a.dw || !a.bn.training || !a.bn.stats || a.lddpool % 8 || a.ldadd % 8)
+      !a.part || !a.l2 || !a.tot || !a.imsum || !a.dw || !a.bn.training || !a.bn.stats || a.lddpool % 8 || a.ldadd % 8)
     return hipErrorInvalidValue;
   const int groups = a.Cout / 64;
   const int segs = (a.Q + kRbNPX - 1) / kRbNPX;
@@ -783,6 +821,7 @@ hipError_t launch_stem_rc_bwd(const StemRcArgs& a, int stage, hipStream_t st) {
   const int chunks = (kRbPartF4 + 63) / 64;
   if (stage == 0) {
     conv_kernel_tag("stem_rc_bwd_kernel");
+    hipLaunchKernelGGL(stem_rc_imsum_kernel, dim3(kRcImBlocks), dim3(256), 0, st, a);
     hipLaunchKernelGGL(stem_rc_bwd_kernel, dim3(blocks, groups), dim3(kRbNT), kRbLds, st, a, per);
   } else {
     conv_kernel_tag("stem_rc_sum1/sum2/finalize");
