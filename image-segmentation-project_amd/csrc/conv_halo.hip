@@ -1182,7 +1182,6 @@ static hipError_t launch_halo_shape(const ConvFwdArgs& a, hipStream_t st) {
   return hipErrorNotSupported;
 }
 
-static int g_halo_disabled = std::getenv("UNET_NO_HALO") != nullptr;  // A/B switch for measurements
 
 // the default weight-stationary selections of launch_halo_shape<false> (the
 // launcher checks the same; xform is only supported there)
@@ -1195,17 +1194,16 @@ static bool ws_fwd_shape(const ConvFwdArgs& a) {
 
 bool conv3x3_ws_xform_ok(const ConvFwdArgs& a) {
   static const bool wscfg = std::getenv("UNET_WSCFG") != nullptr;
-  return !g_halo_disabled && !wscfg && a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.H == a.P &&
+  return !wscfg && a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.H == a.P &&
          a.W == a.Q && a.Q % 16 == 0 && a.ldx % 8 == 0 && a.ldy % 4 == 0 && !a.x2 && !a.fold_on && !a.add &&
          !a.bb.sums && a.ldxh % 8 == 0 && ws_fwd_shape(a) && (size_t)a.N * a.H * a.W * a.ldx * 2 < 0x80000000ull;
 }
-void set_conv_ws(int on) { g_halo_disabled = on ? 0 : 1; }
 
 // 3x3 / s1 / p1 conv (mode 0) or its data gradient (mode 1, dgrad weight pack)
 // when the shape is covered; hipErrorNotSupported otherwise (the caller falls
 // back to the implicit-GEMM kernel).
 hipError_t launch_conv3x3_ws(const ConvFwdArgs& a, int mode, hipStream_t st) {
-  if (g_halo_disabled || a.x2) return hipErrorNotSupported;
+  if (a.x2) return hipErrorNotSupported;
   if (a.R != 3 || a.S != 3 || a.stride != 1 || a.pad != 1) return hipErrorNotSupported;
   if (a.H != a.P || a.W != a.Q || a.Q % 16 || a.ldx % 8 || a.ldy % 4) return hipErrorNotSupported;
   // fused BN-backward epilogue operands are read 4 channels (8 B) at a time

@@ -2455,22 +2455,20 @@ hipError_t launch_conv_fwd_f8(const ConvFwdArgs& a, hipStream_t st) {
   return launch_f8_cfg<64, 128, 3, 2, 2>(a, st);
 }
 
-static bool g_use_glds = std::getenv("UNET_CONV_V1") == nullptr;  // A/B switch for measurements
-void set_conv_impl(int glds) { g_use_glds = glds != 0; }
 
 hipError_t launch_conv_fwd(const ConvFwdArgs& a0, int mode, hipStream_t st) {
   // the folded downsample range exists only in the LDS-DMA transposed kernel
-  if (a0.x2 && (!g_use_glds || mode != MODE_TRANS || a0.C2 != a0.C || a0.stride != 2 || a0.pad != 1))
+  if (a0.x2 && (mode != MODE_TRANS || a0.C2 != a0.C || a0.stride != 2 || a0.pad != 1))
     return hipErrorInvalidValue;
-  if (a0.ysplit && (!g_use_glds || mode == MODE_STEM || mode == MODE_SHUF || a0.csplit % 4 || a0.ldysplit % 4 ||
+  if (a0.ysplit && (mode == MODE_STEM || mode == MODE_SHUF || a0.csplit % 4 || a0.ldysplit % 4 ||
                     a0.bb.sums || a0.add))
     return hipErrorInvalidValue;
-  if (a0.fold_on && (mode != MODE_FWD || a0.stats || a0.bb.sums || !g_use_glds)) return hipErrorInvalidValue;
+  if (a0.fold_on && (mode != MODE_FWD || a0.stats || a0.bb.sums)) return hipErrorInvalidValue;
   // dedicated stem kernel: 64 output channels (Base); the Wide stem (128) takes
   // the generic implicit-GEMM path below
-  if (g_use_glds && mode == MODE_STEM && a0.Cout % 64 == 0) return launch_stem_fwd(a0, st);
+  if (mode == MODE_STEM && a0.Cout % 64 == 0) return launch_stem_fwd(a0, st);
   if (mode == MODE_SHUF) {  // convT k2s2 forward: a0 holds the transposed-conv geometry
-    if (!g_use_glds || a0.R != 2 || a0.S != 2 || a0.stride != 2 || a0.pad != 0 || a0.Cout % 4 || a0.C % 32 ||
+    if (a0.R != 2 || a0.S != 2 || a0.stride != 2 || a0.pad != 0 || a0.Cout % 4 || a0.C % 32 ||
         a0.P != 2 * a0.H || a0.Q != 2 * a0.W || a0.stats || a0.add || a0.bb.sums)
       return hipErrorInvalidValue;
     if ((size_t)a0.N * a0.H * a0.W * a0.ldx * 2 >= 0x80000000ull) return hipErrorInvalidValue;
@@ -2480,7 +2478,7 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a0, int mode, hipStream_t st) {
     a.Pc = a.H; a.Qc = a.W;
     return launch_glds<MODE_SHUF>(a, 1, st);
   }
-  if (g_use_glds && mode != MODE_STEM && a0.C % 32 == 0) {
+  if (mode != MODE_STEM && a0.C % 32 == 0) {
     ConvFwdArgs a = a0;
     if ((size_t)a.N * a.H * a.W * a.ldx * 2 >= 0x80000000ull) return hipErrorInvalidValue;
     if (g_cfg_override <= 0) {
@@ -2786,7 +2784,7 @@ hipError_t launch_convt_wgrad(const ConvWgradArgs& a0, hipStream_t st) {
 // UNET_NO_S2WG=1: stride-2 weight gradients on the implicit GEMM (A/B)
 bool wgrad_s2_fold_ok(const ConvWgradArgs& a) {
   static const bool s2wg = std::getenv("UNET_NO_S2WG") == nullptr;
-  return g_use_glds && s2wg && a.R == 3 && a.S == 3 && a.stride == 2 && a.pad == 1 && a.C % 32 == 0 &&
+  return s2wg && a.R == 3 && a.S == 3 && a.stride == 2 && a.pad == 1 && a.C % 32 == 0 &&
          a.Cout % 64 == 0 && a.H == 2 * a.P && a.W == 2 * a.Q && a.Q % 16 == 0 && a.P % 8 == 0 &&
          (!a.dy2 || a.lddy2 % 8 == 0) && a.lddy % 8 == 0 && a.ldx % 8 == 0 &&
          (size_t)a.N * a.H * a.W * a.ldx * 2 < 0x80000000ull &&
@@ -2798,7 +2796,7 @@ bool wgrad_s2_fold_ok(const ConvWgradArgs& a) {
 bool wgrad_bn_fuse_ok(const ConvWgradArgs& a) {
   static const bool off = std::getenv("UNET_WGCFG") != nullptr;  // tuning runs pick their own kernel
   const BnBwdArgs& b = a.bn;
-  return !off && g_use_glds && a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.C % 64 == 0 &&
+  return !off && a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.C % 64 == 0 &&
          a.P == a.H && a.Q == a.W && ((a.Q % 32 == 0 && a.P % 4 == 0) || (a.Q % 16 == 0 && a.P % 8 == 0)) &&
          (size_t)a.N * a.H * a.W * a.ldx * 2 < 0x80000000ull && (size_t)a.N * a.P * a.Q * b.ldda * 2 < 0x80000000ull &&
          b.da && b.y && b.dy && !b.y2 && !b.coef && b.C == a.Cout && b.ldda % 8 == 0 && b.ldy % 8 == 0 &&
@@ -2816,8 +2814,8 @@ hipError_t launch_conv_wgrad(const ConvWgradArgs& a0, int stem, hipStream_t st) 
   }
   const ConvWgradArgs& a = a0;
   if (stem)
-    return g_use_glds && a.Cout % 64 == 0 ? launch_stem_wgrad(a, st) : launch_wgrad_cfg<XLOAD_STEM, 64, 64, 64, 2, 2>(a, st);
-  if (g_use_glds && a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.C % 32 == 0 && a.P == a.H &&
+    return a.Cout % 64 == 0 ? launch_stem_wgrad(a, st) : launch_wgrad_cfg<XLOAD_STEM, 64, 64, 64, 2, 2>(a, st);
+  if (a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.C % 32 == 0 && a.P == a.H &&
       a.Q == a.W && (size_t)a.N * a.H * a.W * a.ldx * 2 < 0x80000000ull &&
       (size_t)a.N * a.P * a.Q * a.lddy * 2 < 0x80000000ull) {
     static const int wcfg = std::getenv("UNET_WGCFG") ? std::atoi(std::getenv("UNET_WGCFG")) : 0;  // tuning

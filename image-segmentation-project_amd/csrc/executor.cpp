@@ -152,26 +152,13 @@ struct unet_plan {
   std::vector<std::vector<int>> bucket_convs;        // convs to unpack per bucket
   hipEvent_t events[8] = {};
   int nevents = 0;
-  // Backward on two streams: the data-gradient chain (dgrad -> BN backward ->
-  // dgrad ...) stays on the caller's stream, every weight gradient (+ split-K
-  // reduce, bias sums, unpack, bucket events) runs on `wstream`, forked after
-  // the BN-backward apply that produces its dY and joined at the end, so the
-  // HBM-bound BN passes and the reduces overlap the MFMA-bound convs.
-  // Measured slower on MI355X (8.39 vs 7.86 ms/step: the LDS-heavy wgrad and
-  // dgrad blocks contend for CUs and delay the critical dgrad chain), so it is
-  // opt-in: UNET_TWO_STREAM=1 (UNET_WS_PRIO=-1/0/1: weight-stream priority).
-  bool two_stream = std::getenv("UNET_TWO_STREAM") != nullptr;
-  hipStream_t wstream = nullptr;
-  // Split-K slab reductions on their own stream, overlapping the next conv
-  // (two slabs alternate so a wgrad never overwrites partials still being
-  // reduced).  Measured slower on MI355X (2019 vs 2201 img/s, the reductions
-  // compete with the critical dgrad chain for CUs), so it is opt-in:
-  // UNET_SIDE_REDUCE=1.
-  bool side_reduce = std::getenv("UNET_SIDE_REDUCE") != nullptr;
-  hipStream_t rstream = nullptr;
+  // The whole backward runs on the caller's stream.  Weight gradients on a
+  // second stream and split-K reduces on a third were both measured slower on
+  // MI355X (8.39 vs 7.86 ms/step; 2019 vs 2201 img/s: the LDS-heavy wgrad and
+  // reduce blocks contend for CUs with the critical dgrad chain) and were
+  // removed.  Two split-K slabs alternate so a deferred
+  // reduction never reads partials the next weight gradient overwrites.
   int slab_next = 0;
-  bool slab_busy[2] = {false, false};
-  hipEvent_t slab_ev[2] = {};
   std::vector<hipEvent_t> syncpool;
   int syncused = 0;
   bool want_events = false;  // DDP overlap: record one hipEvent per gradient bucket
@@ -981,16 +968,11 @@ int conv_dgrad(const Ctx& x, int ci, const Act& dy, const Act& dx, const Act* ad
 }
 
 // launch one weight gradient (args a, slab filled in here) and its split-K
-// reduction: the reduction goes to the reduce stream, ordered after the wgrad;
-// the slab it reads is not reused until that reduction has finished
+// reduction, deferred into the next BN-backward apply launch when possible
 int wgrad_and_reduce(const Ctx& x, ConvWgradArgs& a, int mode, const std::string& name, double flops) {
   unet_plan* p = x.p;
   const int si = p->slab_next;
   p->slab_next ^= 1;
-  if (p->slab_busy[si]) {
-    CK(hipStreamWaitEvent(x.wst, p->slab_ev[si], 0));
-    p->slab_busy[si] = false;
-  }
   a.slab = x.W<float>(p->wslab + (size_t)si * p->wslab_bytes);
   a.slab_bytes = p->wslab_bytes;
   // a reduction deferred two wgrads ago (the one between had no split-K, and
@@ -1015,15 +997,9 @@ int wgrad_and_reduce(const Ctx& x, ConvWgradArgs& a, int mode, const std::string
     }
     if (wgrad_defer()) return 0;
   }
-  if (x.rst != x.wst) RUN(stream_edge(p, x.wst, x.rst));
   {
     ProfScope pr(p, x.rst, "wgrad_reduce " + name, 0);
     CK(launch_wgrad_finish(x.rst));
-  }
-  if (x.rst != x.wst) {
-    RUN(pooled_event(p, &p->slab_ev[si]));
-    CK(hipEventRecord(p->slab_ev[si], x.rst));
-    p->slab_busy[si] = true;
   }
   return 0;
 }
@@ -1579,19 +1555,9 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
   p->wgb_names.clear();
   p->wgb_flops = 0;
   if (p->want_events) RUN(ensure_events(p));
-  if (p->two_stream && !p->wstream) {
-    int least = 0, greatest = 0;
-    CK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    const char* pe = std::getenv("UNET_WS_PRIO");
-    const int sel = pe ? std::atoi(pe) : 0;  // -1: least (lowest), 1: greatest, 0: default
-    const int prio = sel < 0 ? least : (sel > 0 ? greatest : 0);
-    CK(hipStreamCreateWithPriority(&p->wstream, hipStreamNonBlocking, prio));
-  }
-  x.wst = p->two_stream ? p->wstream : st;
-  if (p->side_reduce && !p->rstream) CK(hipStreamCreateWithFlags(&p->rstream, hipStreamNonBlocking));
-  x.rst = p->side_reduce ? p->rstream : x.wst;
+  x.wst = st;
+  x.rst = st;
   p->syncused = 0;
-  p->slab_busy[0] = p->slab_busy[1] = false;
   // fork: the weight stream starts after the zeroing of the accumulators
   auto fork = [&]() { return stream_edge(p, st, x.wst); };
   CK(hipMemsetAsync(ws + p->zero_bwd_off, 0, p->zero_bwd_bytes, st));
@@ -1888,8 +1854,6 @@ void unet_plan_destroy(unet_plan* p) {
   if (p->tim_buf) (void)hipFree(p->tim_buf);
   for (int i = 0; i < p->nevents; ++i) (void)hipEventDestroy(p->events[i]);
   for (hipEvent_t e : p->syncpool) (void)hipEventDestroy(e);
-  if (p->wstream) (void)hipStreamDestroy(p->wstream);
-  if (p->rstream) (void)hipStreamDestroy(p->rstream);
   delete p;
 }
 

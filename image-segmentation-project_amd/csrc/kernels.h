@@ -163,11 +163,9 @@ hipError_t launch_conv3x3_ws(const ConvFwdArgs& a, int mode, hipStream_t st);
 // the forward of this shape runs on the weight-stationary halo kernel, which
 // supports ConvFwdArgs::xform (the BN-apply prologue)
 bool conv3x3_ws_xform_ok(const ConvFwdArgs& a);
-void set_conv_ws(int on);
 // 3x3 / stride-2 / pad-1 data gradient by parity class on a shared dY halo
 // (conv_halo.hip), with the optional folded downsample (x2 / w2) range
 hipError_t launch_conv3x3s2_dgrad(const ConvFwdArgs& a, hipStream_t st);
-void set_conv_impl(int glds);  // 1: LDS-DMA pipelined kernels (default), 0: register-staged v1
 void set_conv_config(int cfg);  // 0: automatic tile selection, >0: fixed tile config (tuning)
 hipError_t launch_conv_wgrad(const ConvWgradArgs& a, int stem, hipStream_t st);
 // fp8 e4m3 implicit-GEMM forward conv (MODE_FWD geometry, any R/S/stride/pad,

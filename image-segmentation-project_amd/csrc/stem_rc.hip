@@ -83,6 +83,21 @@ struct Patch {
       v[j] = (r < nrows && ih >= 0 && ih < H && iw >= 0 && iw < W) ? img[((size_t)n * H + ih) * W + iw] : 0.f;
     }
   }
+  // the same through raw buffer loads: exactly PT loads per thread whatever
+  // the borders (an element outside the image or past nrows reads the kOOB
+  // zero), so a caller can count them in vmcnt
+  __device__ __forceinline__ void fetch_counted(__amdgpu_buffer_rsrc_t r, int H, int W, int n, int ih0, int nrows,
+                                                int iw0) {
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+      const int i = threadIdx.x + j * NT;
+      const int rr = i / COLS, c = i - rr * COLS;
+      const int ih = ih0 + rr, iw = iw0 + c;
+      const bool ok = rr < nrows && ih >= 0 && ih < H && iw >= 0 && iw < W;
+      const unsigned off = ok ? (unsigned)((((size_t)n * H + ih) * W + iw) * 4) : kOOB;
+      v[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+    }
+  }
   __device__ __forceinline__ void store(bf16_t* patch, int nrows) const {
 #pragma unroll
     for (int j = 0; j < PT; ++j) {
@@ -388,7 +403,8 @@ __global__ void __launch_bounds__(256) stem_rc_imsum_kernel(StemRcArgs a) {
 // ---------------------------------------------------------------------------
 constexpr int kRbNT = 256;
 constexpr int kRbNPX = 128;
-typedef Patch<kRbNPX, kRbNT, 8> BwdPatch;  // 7 x 262
+constexpr int kRbPT = 8;
+typedef Patch<kRbNPX, kRbNT, kRbPT> BwdPatch;  // 7 x 262
 constexpr int kRbTile = kRbNPX * 128;
 constexpr int kRbPatchB = 7 * BwdPatch::PITCH * 2;
 constexpr int kRbPQ = kRbNPX / 2 + 1;                 // pooled columns a unit's pixels reach
@@ -420,6 +436,19 @@ __global__ void __launch_bounds__(kRbNT, 2) stem_rc_bwd_kernel(StemRcArgs a, int
   const int u0 = xcd_remap(blockIdx.x, gridDim.x) * per;
   const int u1 = min(total, u0 + per);
   const int c8 = (tid & 7) * 8;  // this thread's 8 channels in the dZ phase (every item)
+  {
+    // image mean: the block sums of stem_rc_imsum_kernel added by a fixed fp64
+    // tree (the same value in every block), in the Ds region before first use
+    static_assert(kRcImBlocks == kRbNT, "one image-sum partial per thread");
+    double* red = reinterpret_cast<double*>(Ds);
+    red[tid] = (double)a.imsum[tid];
+#pragma unroll
+    for (int st = kRbNT / 2; st > 0; st >>= 1) {
+      lds_sync();
+      if (tid < st) red[tid] += red[tid + st];
+    }
+    lds_sync();
+  }
   if (tid < 64) {
     if (a.bn.ss) {
       cf[tid] = a.bn.ss[cg + tid];
@@ -430,13 +459,11 @@ __global__ void __launch_bounds__(kRbNT, 2) stem_rc_bwd_kernel(StemRcArgs a, int
     }
     cf[128 + tid] = a.mean[cg + tid];
     cf[192 + tid] = a.invstd[cg + tid];
-    // mu[k]: the image mean (fixed-order sum of stem_rc_imsum_kernel's block
-    // sums, the same in every block) for the 49 real taps, 0 for the padding.
-    // The weight-gradient GEMMs run on im - mu: sum_px dY = 0 makes dW
-    // independent of mu, and centring removes the common mode that m1 * sum(im)
-    // would otherwise cancel against dZ^T im (fp32 accumulation).
-    double sum = 0.0;
-    for (int b = 0; b < kRcImBlocks; ++b) sum += (double)a.imsum[b];
+    // mu[k]: the image mean for the 49 real taps, 0 for the padding.  The
+    // weight-gradient GEMMs run on im - mu: sum_px dY = 0 makes dW independent
+    // of mu, and centring removes the common mode that m1 * sum(im) would
+    // otherwise cancel against dZ^T im (fp32 accumulation).
+    const double sum = reinterpret_cast<const double*>(Ds)[0];
     const float mu = bf2f(f2bf((float)(sum / ((double)a.N * a.H * a.W))));
     cf[256 + tid] = ((tid & 7) < 7 && (tid >> 3) < 7) ? mu : 0.f;
   }
@@ -454,12 +481,47 @@ __global__ void __launch_bounds__(kRbNT, 2) stem_rc_bwd_kernel(StemRcArgs a, int
   for (int k = 0; k < 8; ++k) ones[k] = (__bf16)1.0f;
 
   BwdPatch pf;
+  const __amdgpu_buffer_rsrc_t rimg = make_rsrc(a.img, (unsigned)((size_t)a.N * a.H * a.W * 4));
   auto fetch = [&](int u) {
     const int row = u / segs, s = u - row * segs;
     const int n = row / a.P, h = row - n * a.P;
-    pf.fetch(a.img, a.H, a.W, n, 2 * h - 3, 7, 2 * s * kRbNPX - 3);
+    pf.fetch_counted(rimg, a.H, a.W, n, 2 * h - 3, 7, 2 * s * kRbNPX - 3);
   };
-  if (u0 < u1) fetch(u0);
+  // the pooled rows of unit u straight into LDS (DMA, no registers): issued
+  // one unit ahead, right after the previous unit's dZ phase (the last reader
+  // of Pd / Pi), waited for at this unit's dZ phase
+  auto pool_dma = [&](int u) {
+    const int row = u / segs, s = u - row * segs;
+    const int n = row / a.P, h = row - n * a.P;
+    const int q0 = s * kRbNPX, Qs = min(kRbNPX, a.Q - q0);
+    const int p_lo = h >= 1 ? h / 2 : 0;
+    const int p_hi = min((h + 1) / 2, a.Pp - 1);
+    const int qlo = q0 / 2, qhi = min((q0 + Qs) / 2, a.Qp - 1);
+    const int nq = qhi - qlo + 1;
+    const i32x4 rd = make_rsrc_sgpr(a.dpool, (unsigned)((size_t)a.N * a.Pp * a.Qp * a.lddpool * 2));
+    const i32x4 ri = make_rsrc_sgpr(a.idx, (unsigned)((size_t)a.N * a.Pp * a.Qp * a.Cout));
+    // (separate loops: every divisor a compile-time constant)
+    for (int ins = wave; ins < kRbPdIns; ins += kRbNT / 64) {
+      const int e = ins * 64 + lane;
+      const int r = e / (kRbPQ * 8), rem = e - r * (kRbPQ * 8), qi = rem >> 3, pc = rem & 7;
+      const bool ok = r <= p_hi - p_lo && r < 2 && qi < nq;
+      const size_t opix = ((size_t)n * a.Pp + p_lo + r) * a.Qp + qlo + qi;
+      const unsigned off = ok ? (unsigned)((opix * a.lddpool + cg + pc * 8) * 2) : kOOB;
+      glds16_asm(rd, Pd + ins * 1024, off, 0);
+    }
+    for (int ins = wave; ins < kRbPiIns; ins += kRbNT / 64) {
+      const int e = ins * 64 + lane;
+      const int r = e / (kRbPQ * 4), rem = e - r * (kRbPQ * 4), qi = rem >> 2, pc = rem & 3;
+      const bool ok = r <= p_hi - p_lo && r < 2 && qi < nq;
+      const size_t opix = ((size_t)n * a.Pp + p_lo + r) * a.Qp + qlo + qi;
+      const unsigned off = ok ? (unsigned)(opix * a.Cout + cg + pc * 16) : kOOB;
+      glds16_asm(ri, Pi + ins * 1024, off, 0);
+    }
+  };
+  if (u0 < u1) {
+    fetch(u0);
+    pool_dma(u0);
+  }
   TSTAMP(a.tim, 1);
   int kt = 0;
   for (int u = u0; u < u1; ++u, ++kt) {
@@ -467,38 +529,30 @@ __global__ void __launch_bounds__(kRbNT, 2) stem_rc_bwd_kernel(StemRcArgs a, int
     const int n = row / a.P, h = row - n * a.P;
     const int q0 = s * kRbNPX, Qs = min(kRbNPX, a.Q - q0);
     const size_t rowpix = ((size_t)n * a.P + h) * a.Q;
-    // pooled rows p_lo .. p_hi, columns qlo .. qhi reach this unit's pixels
+    // pooled rows p_lo .. p_hi, columns from qlo reach this unit's pixels
     const int p_lo = h >= 1 ? h / 2 : 0;
     const int p_hi = min((h + 1) / 2, a.Pp - 1);
-    const int qlo = q0 / 2, qhi = min((q0 + Qs) / 2, a.Qp - 1);
-    const int nq = qhi - qlo + 1;
-    // the unit's pooled rows straight into LDS (DMA, no registers), waited for
-    // only at the dZ phase
+    const int qlo = q0 / 2;
+    lds_sync();  // previous unit's GEMM reads done
+    if (kt < 2) TSTAMP(a.tim, 2 + 9 * kt);
+    pf.store(patch, 7);  // fetched earlier
+    if (kt < 2) TSTAMP(a.tim, 3 + 9 * kt);
+    // the skip gradient rows straight into Ds in its tt_off layout (DMA, no
+    // registers held): lane l of a 1 KiB wave instruction fills pixel row
+    // ins * 8 + (l >> 3), 16-B slot l & 7, i.e. channel chunk c with
+    // ((c >> 1) ^ f) * 2 + (c & 1) = slot (tt_off's swizzle f of that row)
     {
-      const i32x4 rd = make_rsrc_sgpr(a.dpool, (unsigned)((size_t)a.N * a.Pp * a.Qp * a.lddpool * 2));
-      const i32x4 ri = make_rsrc_sgpr(a.idx, (unsigned)((size_t)a.N * a.Pp * a.Qp * a.Cout));
-      for (int ins = wave; ins < kRbPdIns + kRbPiIns; ins += kRbNT / 64) {
-        const bool isd = ins < kRbPdIns;
-        const int e = (isd ? ins : ins - kRbPdIns) * 64 + lane;
-        const int per_q = isd ? 8 : 4;
-        const int r = e / (kRbPQ * per_q), rem = e - r * (kRbPQ * per_q), qi = rem / per_q, pc = rem - qi * per_q;
-        const bool ok = r <= p_hi - p_lo && r < 2 && qi < nq;
-        const size_t opix = ((size_t)n * a.Pp + p_lo + r) * a.Qp + qlo + qi;
-        unsigned off = kOOB;
-        if (ok) off = isd ? (unsigned)((opix * a.lddpool + cg + pc * 8) * 2) : (unsigned)(opix * a.Cout + cg + pc * 16);
-        if (isd) glds16_asm(rd, Pd + ins * 1024, off, 0);
-        else glds16_asm(ri, Pi + (ins - kRbPdIns) * 1024, off, 0);
+      const i32x4 ra = make_rsrc_sgpr(a.add, (unsigned)((size_t)a.N * a.P * a.Q * a.ldadd * 2));
+#pragma unroll
+      for (int ins = wave; ins < kRbNPX / 8; ins += kRbNT / 64) {
+        const int px = ins * 8 + (lane >> 3), sl = lane & 7;
+        const int f = ((px >> 1) & 1) | (((px >> 3) & 1) << 1);
+        const int c = (((sl >> 1) ^ f) << 1) | (sl & 1);
+        const unsigned off = px < Qs ? (unsigned)(((rowpix + q0 + px) * a.ldadd + cg + c * 8) * 2) : kOOB;
+        glds16_asm(ra, Ds + ins * 1024, off, 0);
       }
     }
-    uint4 addv[kRbNPX * 8 / kRbNT];
-#pragma unroll
-    for (int it = 0; it < kRbNPX * 8 / kRbNT; ++it) {
-      const int px = (tid >> 3) + it * (kRbNT / 8);
-      addv[it] = px < Qs ? *reinterpret_cast<const uint4*>(a.add + (rowpix + q0 + px) * a.ldadd + cg + c8)
-                         : make_uint4(0, 0, 0, 0);
-    }
-    lds_sync();  // previous unit's GEMM reads done
-    pf.store(patch, 7);
+    if (kt < 2) TSTAMP(a.tim, 5 + 9 * kt);
     lds_sync();
     {
       const int px = tid & (kRbNPX - 1), half = tid >> 7;
@@ -510,7 +564,7 @@ __global__ void __launch_bounds__(kRbNT, 2) stem_rc_bwd_kernel(StemRcArgs a, int
       }
     }
     lds_sync();
-    if (kt < 4) TSTAMP(a.tim, 2 + 4 * kt);
+    if (kt < 2) TSTAMP(a.tim, 6 + 9 * kt);
     {  // recompute y (bf16, as the forward rounded it) -> Ys
       bf16x8 wf[2][4];  // re-read per unit (L1/L2-resident 8 KiB): live only across the conv
       load_wfrag(a.w, cg, wf);
@@ -528,53 +582,85 @@ __global__ void __launch_bounds__(kRbNT, 2) stem_rc_bwd_kernel(StemRcArgs a, int
         }
       }
     }
-    wait_vmcnt<0>();  // the pooled rows (and the skip gradient) have landed ...
-    lds_sync();       // ... for every wave
-    if (kt < 4) TSTAMP(a.tim, 3 + 4 * kt);
+    if (kt < 2) TSTAMP(a.tim, 7 + 9 * kt);
+    // the next unit's input patch: issued after this unit's DMA, so the wait
+    // below can leave exactly these kRbPT loads in flight (the last unit
+    // fetches itself again: an unconditional fetch keeps the compiler's own
+    // vmcnt bookkeeping exact)
+    fetch(min(u + 1, u1 - 1));
+    wait_vmcnt<kRbPT>();  // the pooled rows and the skip gradient have landed ...
+    lds_sync();           // ... for every wave
+    if (kt < 2) TSTAMP(a.tim, 8 + 9 * kt);
     // dZ = [act > 0] (sum of the pooled gradients whose argmax is this pixel +
-    // the skip gradient): maxpool_bwd_kernel's expression and order
+    // the skip gradient): maxpool_bwd_kernel's expression and order.  The
+    // thread's 8 channels are the same in every item: coefficients read once.
+    // thread index made opaque here: the item addresses below are recomputed
+    // per unit instead of being hoisted out of the unit loop as live registers
+    int tdv = tid;
+    asm volatile("" : "+v"(tdv));
+    const int c8 = (tdv & 7) * 8;
 #pragma unroll
     for (int it = 0; it < kRbNPX * 8 / kRbNT; ++it) {
-      // items one after the other (static addv[it] indexing, no cross-item
-      // interleaving that would hold four items' temporaries at once)
+      // items one after the other (no cross-item interleaving that would
+      // hold four items' temporaries at once)
       __builtin_amdgcn_sched_barrier(0);
-      const int px = (tid >> 3) + it * (kRbNT / 8);
+      // pixel parity uniform per item (it & 1), so an even column has one
+      // candidate pooled column and an odd one two; the row parity is uniform
+      // per unit (h)
+      const int px = 2 * (tdv >> 3) + (it & 1) + (it >> 1) * (kRbNT / 4);
       const int w = q0 + px;
       const bool valid = px < Qs;
-      const int qa = w >= 1 ? w / 2 : 0;
-      const int qb = min((w + 1) / 2, a.Qp - 1);
+      const bool hodd = h & 1, wodd = it & 1;
+      const uint4 yv = *reinterpret_cast<const uint4*>(Ys + tt_off(px, c8));
+      const uint4 av = *reinterpret_cast<const uint4*>(Ds + tt_off(px, c8));
+      const uint4 xv = *reinterpret_cast<const uint4*>(Xs + tt_off(px, c8));
+      // the pooled cells that may have this pixel as their argmax, in
+      // maxpool_bwd_kernel's order (rows p_lo, p_lo + 1; columns qa, qa + 1):
+      // even h: row p_lo only (kh = 1); odd h: kh = 2 then kh = 0; even w:
+      // column w / 2 only (kw = 1); odd w: kw = 2 then kw = 0
+      const int qa = wodd ? (w - 1) / 2 : w / 2;
+      uint2 ix[4];
+      uint4 pd[4];
+      int want[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int rr = jj >> 1, cc = jj & 1;
+        want[jj] = -1;
+        if ((rr && !hodd) || (cc && !wodd)) continue;  // uniform: never a candidate
+        const int p = p_lo + rr, q = qa + cc;
+        const int kh = hodd ? (rr ? 0 : 2) : 1, kw = wodd ? (cc ? 0 : 2) : 1;
+        const bool ok = valid && p <= p_hi && q < a.Qp;
+        const int slot = ok ? rr * kRbPQ + (q - qlo) : 0;
+        want[jj] = ok ? kh * 3 + kw : -1;
+        ix[jj] = *reinterpret_cast<const uint2*>(Pi + slot * 64 + c8);
+        pd[jj] = *reinterpret_cast<const uint4*>(Pd + slot * 128 + c8 * 2);
+      }
       float acc[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc[k] = 0.f;
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
-        const int p = p_lo + (jj >> 1);
-        const int q = qa + (jj & 1);
-        const int kh = h - (2 * p - 1), kw = w - (2 * q - 1);
-        const bool ok = valid && p <= p_hi && q <= qb && kh >= 0 && kh <= 2 && kw >= 0 && kw <= 2;
-        if (!ok) continue;
-        const int want = kh * 3 + kw;
-        const int slot = (p - p_lo) * kRbPQ + (q - qlo);
-        const uint2 ix = *reinterpret_cast<const uint2*>(Pi + slot * 64 + c8);
+        const int rr = jj >> 1, cc = jj & 1;
+        if ((rr && !hodd) || (cc && !wodd)) continue;
         float gv[8];
-        unpack8(*reinterpret_cast<const uint4*>(Pd + slot * 128 + c8 * 2), gv);
+        unpack8(pd[jj], gv);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const unsigned word = k < 4 ? ix.x : ix.y;
-          const int b = (word >> ((k & 3) * 8)) & 0xff;
-          if (b == want) acc[k] += gv[k];
+          const unsigned word = k < 4 ? ix[jj].x : ix[jj].y;
+          const int bsel = (word >> ((k & 3) * 8)) & 0xff;
+          acc[k] = bsel == want[jj] ? acc[k] + gv[k] : acc[k];
         }
       }
       {
         float r[8];
-        unpack8(addv[it], r);
+        unpack8(av, r);
 #pragma unroll
         for (int k = 0; k < 8; ++k) acc[k] += r[k];
       }
       float y[8];
-      unpack8(*reinterpret_cast<const uint4*>(Ys + tt_off(px, c8)), y);
+      unpack8(yv, y);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] = (valid && stem_act(y[k], cf[c8 + k], cf[64 + c8 + k]) > 0.f) ? acc[k] : 0.f;
+      for (int k = 0; k < 8; ++k) acc[k] = (valid & (stem_act(y[k], cf[c8 + k], cf[64 + c8 + k]) > 0.f)) ? acc[k] : 0.f;
       const uint4 o = pack8(acc);
       *reinterpret_cast<uint4*>(Ds + tt_off(px, c8)) = o;
       if (a.dz && valid) *reinterpret_cast<uint4*>(a.dz + (rowpix + w) * a.lddz + cg + c8) = o;
@@ -591,15 +677,15 @@ __global__ void __launch_bounds__(kRbNT, 2) stem_rc_bwd_kernel(StemRcArgs a, int
       *reinterpret_cast<uint4*>(Ys + tt_off(px, c8)) = valid ? pack8(xh) : make_uint4(0, 0, 0, 0);
       if (valid) {  // im2col row chunk of this pixel, centred (the conv has read it)
         float im[8];
-        unpack8(*reinterpret_cast<const uint4*>(Xs + tt_off(px, c8)), im);
+        unpack8(xv, im);
 #pragma unroll
         for (int k = 0; k < 8; ++k) im[k] -= cf[256 + c8 + k];
         *reinterpret_cast<uint4*>(Xs + tt_off(px, c8)) = pack8(im);
       }
     }
-    if (u + 1 < u1) fetch(u + 1);  // next unit's input patch, in flight during the GEMMs
-    lds_sync();
-    if (kt < 4) TSTAMP(a.tim, 4 + 4 * kt);
+    lds_sync();  // Pd / Pi read for the last time
+    if (kt < 2) TSTAMP(a.tim, 9 + 9 * kt);
+    if (u + 1 < u1) pool_dma(u + 1);
     // GEMMs over the unit's pixels: D[co][k] += sum_px S[px][co] im[px][k]
     {
       const char* S = (wave >> 1) ? Ys : Ds;
@@ -627,7 +713,7 @@ __global__ void __launch_bounds__(kRbNT, 2) stem_rc_bwd_kernel(StemRcArgs a, int
         bacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bw, bacc, 0, 0, 0);
       }
     }
-    if (kt < 4) TSTAMP(a.tim, 5 + 4 * kt);
+    if (kt < 2) TSTAMP(a.tim, 10 + 9 * kt);
   }
   TSTAMP(a.tim, 20);
   // partials of this block: fragments lane-contiguous, then the channel sums
@@ -810,7 +896,12 @@ size_t stem_rc_l2_offset(int N, int P, int Q, int Cout) {
 
 hipError_t launch_stem_rc_bwd(const StemRcArgs& a, int stage, hipStream_t st) {
   if (!stem_rc_ok(a.Cout, a.P, a.Q) || a.Pp * 2 != a.P || a.Qp * 2 != a.Q || a.H != 2 * a.P || a.W != 2 * a.Q ||
-      !a.part || !a.l2 || !a.tot || !a.imsum || !a.dw || !a.bn.training || !a.bn.stats || a.lddpool % 8 || a.ldadd % 8)
+      !a.part || !a.l2 || !a.tot || !a.imsum || !a.dw || !a.bn.training || !a.bn.stats || a.lddpool % 8 || a.ldadd % 8 ||
+      !a.add || !a.dpool || !a.idx)
+    return hipErrorInvalidValue;
+  // 32-bit buffer offsets of the LDS-DMA (kOOB = 2^31 must lie past every range)
+  if ((size_t)a.N * a.P * a.Q * a.ldadd * 2 >= kOOB || (size_t)a.N * a.Pp * a.Qp * a.lddpool * 2 >= kOOB ||
+      (size_t)a.N * a.Pp * a.Qp * a.Cout >= kOOB || (size_t)a.N * a.H * a.W * 4 >= kOOB)
     return hipErrorInvalidValue;
   const int groups = a.Cout / 64;
   const int segs = (a.Q + kRbNPX - 1) / kRbNPX;
