@@ -38,6 +38,9 @@ SHAPES = [
     ("enc2.0_s2", 64, 128, 128, 3, 2, 1),
     ("enc3.0_s2", 128, 256, 64, 3, 2, 1),
     ("enc4.0_s2", 256, 512, 32, 3, 2, 1),
+    # ConvTranspose k2s2 data gradients = k2s2 convs of dY (dY channels in, X channels out)
+    ("up1_dgrad", 32, 64, 256, 2, 2, 0),
+    ("up2_dgrad", 64, 128, 128, 2, 2, 0),
 ]
 
 
