@@ -228,8 +228,17 @@ __device__ __forceinline__ void bn_finalize(const unet::BnLaunch& p) {
 // Per-channel BN-backward apply coefficients from the replica sums:
 // dY = A dZ + B y + C, A = k1 = gamma invstd, B = -k1 invstd m2,
 // C = k1 (invstd m2 mu - m1), m1 = mean dZ, m2 = mean dZ xhat.  Shared by
-// bn_bwd_apply_kernel and the BN-fused weight gradient (its dY side product
-// must be bit-identical to the apply pass): no contraction, fixed order.
+// bn_bwd_apply_kernel (both coefficient sources: replica sums, or the
+// finalised k1 / m1 / m2 of a ticket), the BN-fused weight gradients and the
+// stem's fused apply (side products must be bit-identical to the apply
+// pass): no contraction, fixed order (bn_bwd_coef_abc).
+__device__ __forceinline__ void bn_bwd_coef_abc(float k1, float m1, float m2, float is, float mu, float& A, float& B,
+                                                float& C) {
+  // explicit round-to-nearest operations: no context-dependent contraction
+  A = k1;
+  B = __fmul_rn(__fmul_rn(-k1, is), m2);
+  C = __fmul_rn(k1, __fsub_rn(__fmul_rn(__fmul_rn(is, m2), mu), m1));
+}
 __device__ __forceinline__ void bn_bwd_apply_coef(const unet::BnBwdArgs& a, int ch, double inv_n, float& A,
                                                   float& B, float& C, double& s1, double& s2) {
 #pragma clang fp contract(off)
@@ -240,13 +249,9 @@ __device__ __forceinline__ void bn_bwd_apply_coef(const unet::BnBwdArgs& a, int 
     s1 += a.sums[rep + ch];
     s2 += a.sums[rep + a.C + ch];
   }
-  // explicit round-to-nearest operations: no context-dependent contraction
   const float k1 = __fmul_rn(a.gamma[ch], a.invstd[ch]);
   const float m1 = (float)__dmul_rn(s1, inv_n), m2 = (float)__dmul_rn(s2, inv_n);
-  const float is = a.invstd[ch], mu = a.mean[ch];
-  A = k1;
-  B = __fmul_rn(__fmul_rn(-k1, is), m2);
-  C = __fmul_rn(k1, __fsub_rn(__fmul_rn(__fmul_rn(is, m2), mu), m1));
+  bn_bwd_coef_abc(k1, m1, m2, a.invstd[ch], a.mean[ch], A, B, C);
 }
 
 // Last block of a BN-backward reduction (bn_bwd_reduce_kernel or a fused

@@ -2117,12 +2117,9 @@ __global__ void __launch_bounds__(256, 2) stem_wgrad_kernel(ConvWgradArgs a, int
         s2 += b.sums[(size_t)r * 2 * b.C + b.C + ch];
       }
       const double inv_n = 1.0 / (double)b.npix;
-      const float k1 = b.gamma[ch] * b.invstd[ch];
-      const float m1 = (float)(s1 * inv_n), m2 = (float)(s2 * inv_n);
-      const float is = b.invstd[ch], mu = b.mean[ch];
-      coef[tid] = k1;
-      coef[64 + tid] = -k1 * is * m2;
-      coef[128 + tid] = k1 * (is * m2 * mu - m1);
+      const float k1 = __fmul_rn(b.gamma[ch], b.invstd[ch]);
+      const float m1 = (float)__dmul_rn(s1, inv_n), m2 = (float)__dmul_rn(s2, inv_n);
+      bn_bwd_coef_abc(k1, m1, m2, b.invstd[ch], b.mean[ch], coef[tid], coef[64 + tid], coef[128 + tid]);
       if (blockIdx.x == 0) {
         b.dgamma[ch] = (float)s2;
         b.dbeta[ch] = (float)s1;

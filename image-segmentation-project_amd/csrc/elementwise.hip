@@ -355,8 +355,8 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, double i
       bn_bwd_apply_coef(a, ch, inv_n, cA, cB, cC, s1, s2);
       if (TWO) {
         for (int r = 0; r < kStatRep; ++r) t2 += a.sums2[(size_t)r * 2 * a.C + a.C + ch];
-        k1b = a.gamma2[ch] * a.invstd2[ch];
-        m2b = (float)(t2 * inv_n);
+        k1b = __fmul_rn(a.gamma2[ch], a.invstd2[ch]);
+        m2b = (float)__dmul_rn(t2, inv_n);
       }
       if (bx == 0) {
         a.dgamma[ch] = (float)s2;
@@ -369,25 +369,15 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, double i
       coef[c] = cA;
       coef[CG + c] = cB;
       coef[2 * CG + c] = cC;
-      m1 = (float)(s1 * inv_n);
+      m1 = (float)__dmul_rn(s1, inv_n);
       if (TWO) {
         const float isb = a.invstd2[ch], mub = a.mean2[ch];
-        coef[3 * CG + c] = k1b;
-        coef[4 * CG + c] = -k1b * isb * m2b;
-        coef[5 * CG + c] = k1b * (isb * m2b * mub - m1);
+        bn_bwd_coef_abc(k1b, m1, m2b, isb, mub, coef[3 * CG + c], coef[4 * CG + c], coef[5 * CG + c]);
       }
       continue;
     }
-    const float is = a.invstd[ch], mu = a.mean[ch];
-    coef[c] = k1;
-    coef[CG + c] = -k1 * is * m2;
-    coef[2 * CG + c] = k1 * (is * m2 * mu - m1);
-    if (TWO) {
-      const float isb = a.invstd2[ch], mub = a.mean2[ch];
-      coef[3 * CG + c] = k1b;
-      coef[4 * CG + c] = -k1b * isb * m2b;
-      coef[5 * CG + c] = k1b * (isb * m2b * mub - m1);
-    }
+    bn_bwd_coef_abc(k1, m1, m2, a.invstd[ch], a.mean[ch], coef[c], coef[CG + c], coef[2 * CG + c]);
+    if (TWO) bn_bwd_coef_abc(k1b, m1, m2b, a.invstd2[ch], a.mean2[ch], coef[3 * CG + c], coef[4 * CG + c], coef[5 * CG + c]);
   }
   __syncthreads();
   float cA[8], cB[8], cC[8], dA[TWO ? 8 : 1], dB[TWO ? 8 : 1], dC[TWO ? 8 : 1];

@@ -74,16 +74,7 @@ struct Patch {
   static constexpr int COLS = 2 * NPX + 6;
   static constexpr int PITCH = 2 * NPX + 8;
   float v[PT];
-  __device__ __forceinline__ void fetch(const float* img, int H, int W, int n, int ih0, int nrows, int iw0) {
-#pragma unroll
-    for (int j = 0; j < PT; ++j) {
-      const int i = threadIdx.x + j * NT;
-      const int r = i / COLS, c = i - r * COLS;
-      const int ih = ih0 + r, iw = iw0 + c;
-      v[j] = (r < nrows && ih >= 0 && ih < H && iw >= 0 && iw < W) ? img[((size_t)n * H + ih) * W + iw] : 0.f;
-    }
-  }
-  // the same through raw buffer loads: exactly PT loads per thread whatever
+  // raw buffer loads with 32-bit offsets: exactly PT loads per thread whatever
   // the borders (an element outside the image or past nrows reads the kOOB
   // zero), so a caller can count them in vmcnt
   __device__ __forceinline__ void fetch_counted(__amdgpu_buffer_rsrc_t r, int H, int W, int n, int ih0, int nrows,
@@ -94,7 +85,8 @@ struct Patch {
       const int rr = i / COLS, c = i - rr * COLS;
       const int ih = ih0 + rr, iw = iw0 + c;
       const bool ok = rr < nrows && ih >= 0 && ih < H && iw >= 0 && iw < W;
-      const unsigned off = ok ? (unsigned)((((size_t)n * H + ih) * W + iw) * 4) : kOOB;
+      // 32-bit: the launchers check N * H * W * 4 < 2^31
+      const unsigned off = ok ? (unsigned)(((n * H + ih) * W + iw) * 4) : kOOB;
       v[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
     }
   }
@@ -222,9 +214,12 @@ __global__ void __launch_bounds__(kRcNT) stem_rc_fwd_kernel(StemRcArgs a, int pe
   // pooled row j: stem rows 2jp - extra .. 2jp + 1, input rows from 4jp - 3 - 2 extra
   auto extra_of = [&](int j) { return (MODE == 1 && j == j0 && (j % a.Pp) > 0) ? 1 : 0; };
   FwdPatch pf;
+  // 32-bit buffer offsets, kOOB zero-fill at the borders (no 64-bit address
+  // arithmetic or branch per element)
+  const __amdgpu_buffer_rsrc_t rimg = make_rsrc(a.img, (unsigned)((size_t)a.N * a.H * a.W * 4));
   auto fetch = [&](int j) {
     const int n = j / a.Pp, jp = j - n * a.Pp, ex = extra_of(j);
-    pf.fetch(a.img, a.H, a.W, n, 4 * jp - 3 - 2 * ex, 9 + 2 * ex, -3);
+    pf.fetch_counted(rimg, a.H, a.W, n, 4 * jp - 3 - 2 * ex, 9 + 2 * ex, -3);
   };
   if (j0 < j1) fetch(j0);
   TSTAMP(a.tim, 1);
@@ -295,31 +290,42 @@ __global__ void __launch_bounds__(kRcNT) stem_rc_fwd_kernel(StemRcArgs a, int pe
         }
       }
       // MaxPool2d(3, 2, 1) of pooled row jp: first maximum in (kh, kw) scan
-      // order wins (strict >), NaN propagates (maxpool_fwd_kernel's rule)
+      // order wins (strict >).  act = bf16(relu(.)) is never NaN and never
+      // negative (stem_act maps NaN to 0), so its bf16 bits order like its
+      // values and one unsigned max over key = bits << 4 | (15 - tap) finds
+      // the maximum and, among equal maxima, the first tap
 #pragma unroll
       for (int it = 0; it < (kRcNPX / 2) * 8 / kRcNT; ++it) {
         const int i = tid + it * kRcNT, q = i >> 3, ch = i & 7;
         if (q >= a.Qp) continue;
-        float best[8];
-        int bi[8];
+        unsigned key[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; bi[k] = -1; }
+        for (int k = 0; k < 8; ++k) key[k] = 0u;  // the (1, 1) tap is always inside
 #pragma unroll
         for (int t9 = 0; t9 < 9; ++t9) {
           const int kh = t9 / 3, kw = t9 % 3;
           const int h = 2 * jp - 1 + kh, w = 2 * q - 1 + kw;
-          if (h < 0 || w < 0 || w >= a.Q) continue;
-          float v[8];
-          unpack8(*reinterpret_cast<const uint4*>(ring + (h % 3) * (kRcNPX * 128) + ring_off(w, ch * 8)), v);
+          if (h < 0) continue;  // uniform (first pooled row)
+          const bool inw = w >= 0 && w < a.Q;
+          const uint4 r = *reinterpret_cast<const uint4*>(ring + (h % 3) * (kRcNPX * 128) + ring_off(inw ? w : 0, ch * 8));
+          const unsigned wd[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
-            const bool take = bi[k] < 0 || v[k] > best[k] || (v[k] != v[k] && best[k] == best[k]);
-            best[k] = take ? v[k] : best[k];
-            bi[k] = take ? t9 : bi[k];
+            const unsigned bits = (k & 1) ? (wd[k >> 1] >> 16) : (wd[k >> 1] & 0xffffu);
+            const unsigned cand = inw ? ((bits << 4) | (unsigned)(15 - t9)) : 0u;
+            key[k] = max(key[k], cand);
           }
         }
+        uint4 best;
+        best.x = (key[0] >> 4) | ((key[1] >> 4) << 16);
+        best.y = (key[2] >> 4) | ((key[3] >> 4) << 16);
+        best.z = (key[4] >> 4) | ((key[5] >> 4) << 16);
+        best.w = (key[6] >> 4) | ((key[7] >> 4) << 16);
+        int bi[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) bi[k] = 15 - (int)(key[k] & 15u);
         const size_t opix = ((size_t)n * a.Pp + jp) * a.Qp + q;
-        *reinterpret_cast<uint4*>(a.pool + opix * a.ldpool + cg + ch * 8) = pack8(best);
+        *reinterpret_cast<uint4*>(a.pool + opix * a.ldpool + cg + ch * 8) = best;
         uint2 ix;
         ix.x = (unsigned)bi[0] | ((unsigned)bi[1] << 8) | ((unsigned)bi[2] << 16) | ((unsigned)bi[3] << 24);
         ix.y = (unsigned)bi[4] | ((unsigned)bi[5] << 8) | ((unsigned)bi[6] << 16) | ((unsigned)bi[7] << 24);
@@ -854,7 +860,8 @@ bool stem_rc_ok(int Cout, int P, int Q) {
 }
 
 hipError_t launch_stem_rc_fwd(const StemRcArgs& a, int mode, hipStream_t st) {
-  if (!stem_rc_ok(a.Cout, a.P, a.Q) || a.Pp * 2 != a.P || a.Qp * 2 != a.Q || a.H != 2 * a.P || a.W != 2 * a.Q)
+  if (!stem_rc_ok(a.Cout, a.P, a.Q) || a.Pp * 2 != a.P || a.Qp * 2 != a.Q || a.H != 2 * a.P || a.W != 2 * a.Q ||
+      (size_t)a.N * a.H * a.W * 4 >= kOOB)
     return hipErrorInvalidValue;
   const int groups = a.Cout / 64;
   const int total = a.N * a.Pp;
