@@ -403,7 +403,11 @@ __global__ void __launch_bounds__(256) stem_rc_imsum_kernel(StemRcArgs a) {
 // registers, and land while the conv is recomputed; the pooled rows are then
 // staged in LDS and the maxpool backward gathers from there.
 // LDS: patch (7 x 264 bf16) | Xs im2col [128][64] | Ys y/xhat [128][64] |
-//      Ds dZ [128][64] | coefficients [4][64] f32 | Pd dpool [2][65][64] | Pi idx [2][65][64] u8
+//      Ds dZ [128][64] | coefficients [5][64] f32 | Pd dpool [2 slots][65][64] | Pi idx [2 slots][65][64] u8
+// Units run down the rows of one 128-column segment (u = s * N * P + n * P + h),
+// so consecutive units share pooled rows: pooled row p lives in slot p & 1 and
+// a unit loads only the rows the previous one did not have (one row every
+// other unit).
 // Waves: w>>1 = GEMM (0: dZ^T im, 1: xhat^T im), w&1 = 32-channel half; each
 // wave also sums im over pixels for k in [16w, 16w+16) (MFMA against ones).
 // ---------------------------------------------------------------------------
@@ -414,10 +418,13 @@ typedef Patch<kRbNPX, kRbNT, kRbPT> BwdPatch;  // 7 x 262
 constexpr int kRbTile = kRbNPX * 128;
 constexpr int kRbPatchB = 7 * BwdPatch::PITCH * 2;
 constexpr int kRbPQ = kRbNPX / 2 + 1;                 // pooled columns a unit's pixels reach
-// LDS-DMA of the pooled rows, one 16-B piece per lane: dpool [r][qi][8 pieces],
-// idx [r][qi][4 pieces]; whole 1 KiB wave instructions
-constexpr int kRbPdIns = (2 * kRbPQ * 8 + 63) / 64, kRbPiIns = (2 * kRbPQ * 4 + 63) / 64;
-constexpr int kRbPd = kRbPdIns * 1024, kRbPi = kRbPiIns * 1024;
+// LDS-DMA of one pooled row, one 16-B piece per lane: dpool [qi][8 pieces],
+// idx [qi][4 pieces]; the last wave instruction of a row is moved back so that
+// it ends at the row end (rewriting some pieces with the same data) instead of
+// spilling into the other slot
+constexpr int kRbPdRow = kRbPQ * 8, kRbPiRow = kRbPQ * 4;  // 16-B pieces per row
+constexpr int kRbPdIns = (kRbPdRow + 63) / 64, kRbPiIns = (kRbPiRow + 63) / 64;
+constexpr int kRbPd = 2 * kRbPdRow * 16, kRbPi = 2 * kRbPiRow * 16;
 constexpr int kRbLds = kRbPatchB + 3 * kRbTile + 5 * 64 * 4 + kRbPd + kRbPi;
 // per-block partial: [4 waves][9 tiles][64 lanes] f32x4 | [2][64] sum dZ, sum dZ xhat
 constexpr int kRbPartF4 = 4 * 9 * 64 + 32;
@@ -488,51 +495,64 @@ __global__ void __launch_bounds__(kRbNT, 2) stem_rc_bwd_kernel(StemRcArgs a, int
 
   BwdPatch pf;
   const __amdgpu_buffer_rsrc_t rimg = make_rsrc(a.img, (unsigned)((size_t)a.N * a.H * a.W * 4));
+  const int rows_total = a.N * a.P;
+  auto decode = [&](int u, int& s, int& n, int& h) {
+    s = u / rows_total;
+    const int row = u - s * rows_total;
+    n = row / a.P;
+    h = row - n * a.P;
+  };
   auto fetch = [&](int u) {
-    const int row = u / segs, s = u - row * segs;
-    const int n = row / a.P, h = row - n * a.P;
+    int s, n, h;
+    decode(u, s, n, h);
     pf.fetch_counted(rimg, a.H, a.W, n, 2 * h - 3, 7, 2 * s * kRbNPX - 3);
   };
   // the pooled rows of unit u straight into LDS (DMA, no registers): issued
   // one unit ahead, right after the previous unit's dZ phase (the last reader
-  // of Pd / Pi), waited for at this unit's dZ phase
-  auto pool_dma = [&](int u) {
-    const int row = u / segs, s = u - row * segs;
-    const int n = row / a.P, h = row - n * a.P;
+  // of Pd / Pi), waited for at this unit's dZ phase.  Rows the previous unit
+  // of this block already loaded (same segment, previous stem row) stay.
+  auto pool_dma = [&](int u, bool first) {
+    int s, n, h;
+    decode(u, s, n, h);
     const int q0 = s * kRbNPX, Qs = min(kRbNPX, a.Q - q0);
     const int p_lo = h >= 1 ? h / 2 : 0;
     const int p_hi = min((h + 1) / 2, a.Pp - 1);
     const int qlo = q0 / 2, qhi = min((q0 + Qs) / 2, a.Qp - 1);
     const int nq = qhi - qlo + 1;
+    int have = -1;  // highest pooled row already resident
+    if (!first) {
+      int sp, np, hp;
+      decode(u - 1, sp, np, hp);
+      if (sp == s && np == n && hp + 1 == h) have = min(h / 2, a.Pp - 1);  // p_hi of row h - 1
+    }
     const i32x4 rd = make_rsrc_sgpr(a.dpool, (unsigned)((size_t)a.N * a.Pp * a.Qp * a.lddpool * 2));
     const i32x4 ri = make_rsrc_sgpr(a.idx, (unsigned)((size_t)a.N * a.Pp * a.Qp * a.Cout));
-    // (separate loops: every divisor a compile-time constant)
-    for (int ins = wave; ins < kRbPdIns; ins += kRbNT / 64) {
-      const int e = ins * 64 + lane;
-      const int r = e / (kRbPQ * 8), rem = e - r * (kRbPQ * 8), qi = rem >> 3, pc = rem & 7;
-      const bool ok = r <= p_hi - p_lo && r < 2 && qi < nq;
-      const size_t opix = ((size_t)n * a.Pp + p_lo + r) * a.Qp + qlo + qi;
-      const unsigned off = ok ? (unsigned)((opix * a.lddpool + cg + pc * 8) * 2) : kOOB;
-      glds16_asm(rd, Pd + ins * 1024, off, 0);
-    }
-    for (int ins = wave; ins < kRbPiIns; ins += kRbNT / 64) {
-      const int e = ins * 64 + lane;
-      const int r = e / (kRbPQ * 4), rem = e - r * (kRbPQ * 4), qi = rem >> 2, pc = rem & 3;
-      const bool ok = r <= p_hi - p_lo && r < 2 && qi < nq;
-      const size_t opix = ((size_t)n * a.Pp + p_lo + r) * a.Qp + qlo + qi;
-      const unsigned off = ok ? (unsigned)(opix * a.Cout + cg + pc * 16) : kOOB;
-      glds16_asm(ri, Pi + ins * 1024, off, 0);
+    for (int p = p_lo; p <= p_hi; ++p) {
+      if (p <= have) continue;  // uniform
+      const size_t rowbase = ((size_t)n * a.Pp + p) * a.Qp + qlo;
+      char* pd = Pd + (p & 1) * (kRbPdRow * 16);
+      char* pi = Pi + (p & 1) * (kRbPiRow * 16);
+      for (int ins = wave; ins < kRbPdIns; ins += kRbNT / 64) {
+        const int e0 = min(ins * 64, kRbPdRow - 64), e = e0 + lane, qi = e >> 3, pc = e & 7;
+        const unsigned off = qi < nq ? (unsigned)(((rowbase + qi) * a.lddpool + cg + pc * 8) * 2) : kOOB;
+        glds16_asm(rd, pd + e0 * 16, off, 0);
+      }
+      for (int ins = wave; ins < kRbPiIns; ins += kRbNT / 64) {
+        const int e0 = min(ins * 64, kRbPiRow - 64), e = e0 + lane, qi = e >> 2, pc = e & 3;
+        const unsigned off = qi < nq ? (unsigned)((rowbase + qi) * a.Cout + cg + pc * 16) : kOOB;
+        glds16_asm(ri, pi + e0 * 16, off, 0);
+      }
     }
   };
   if (u0 < u1) {
     fetch(u0);
-    pool_dma(u0);
+    pool_dma(u0, true);
   }
   TSTAMP(a.tim, 1);
   int kt = 0;
   for (int u = u0; u < u1; ++u, ++kt) {
-    const int row = u / segs, s = u - row * segs;
-    const int n = row / a.P, h = row - n * a.P;
+    int s, n, h;
+    decode(u, s, n, h);
     const int q0 = s * kRbNPX, Qs = min(kRbNPX, a.Q - q0);
     const size_t rowpix = ((size_t)n * a.P + h) * a.Q;
     // pooled rows p_lo .. p_hi, columns from qlo reach this unit's pixels
@@ -543,19 +563,24 @@ __global__ void __launch_bounds__(kRbNT, 2) stem_rc_bwd_kernel(StemRcArgs a, int
     if (kt < 2) TSTAMP(a.tim, 2 + 9 * kt);
     pf.store(patch, 7);  // fetched earlier
     if (kt < 2) TSTAMP(a.tim, 3 + 9 * kt);
-    // the skip gradient rows straight into Ds in its tt_off layout (DMA, no
-    // registers held): lane l of a 1 KiB wave instruction fills pixel row
-    // ins * 8 + (l >> 3), 16-B slot l & 7, i.e. channel chunk c with
-    // ((c >> 1) ^ f) * 2 + (c & 1) = slot (tt_off's swizzle f of that row)
+    // conv weights (L1/L2-resident 8 KiB) re-read per unit, issued before the
+    // skip-gradient loads so that the conv's wait for them leaves those in flight
+    bf16x8 wf[2][4];
+    load_wfrag(a.w, cg, wf);
+    // the skip gradient of this thread's dZ items (plain loads, consumed in the
+    // dZ phase; the tdv mapping below)
+    uint4 addv[kRbNPX * 8 / kRbNT];
     {
-      const i32x4 ra = make_rsrc_sgpr(a.add, (unsigned)((size_t)a.N * a.P * a.Q * a.ldadd * 2));
+      const __amdgpu_buffer_rsrc_t radd = make_rsrc(a.add, (unsigned)((size_t)a.N * a.P * a.Q * a.ldadd * 2));
+      int tdl = tid;
+      asm volatile("" : "+v"(tdl));
 #pragma unroll
-      for (int ins = wave; ins < kRbNPX / 8; ins += kRbNT / 64) {
-        const int px = ins * 8 + (lane >> 3), sl = lane & 7;
-        const int f = ((px >> 1) & 1) | (((px >> 3) & 1) << 1);
-        const int c = (((sl >> 1) ^ f) << 1) | (sl & 1);
-        const unsigned off = px < Qs ? (unsigned)(((rowpix + q0 + px) * a.ldadd + cg + c * 8) * 2) : kOOB;
-        glds16_asm(ra, Ds + ins * 1024, off, 0);
+      for (int it = 0; it < kRbNPX * 8 / kRbNT; ++it) {
+        const int px = 2 * (tdl >> 3) + (it & 1) + (it >> 1) * (kRbNT / 4);
+        // raw buffer load (kOOB zero past the row end): always issued, so the
+        // compiler's vmcnt bookkeeping stays exact
+        const unsigned off = px < Qs ? (unsigned)(((rowpix + q0 + px) * a.ldadd + cg + (tdl & 7) * 8) * 2) : kOOB;
+        addv[it] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(radd, (int)off, 0, 0));
       }
     }
     if (kt < 2) TSTAMP(a.tim, 5 + 9 * kt);
@@ -572,8 +597,6 @@ __global__ void __launch_bounds__(kRbNT, 2) stem_rc_bwd_kernel(StemRcArgs a, int
     lds_sync();
     if (kt < 2) TSTAMP(a.tim, 6 + 9 * kt);
     {  // recompute y (bf16, as the forward rounded it) -> Ys
-      bf16x8 wf[2][4];  // re-read per unit (L1/L2-resident 8 KiB): live only across the conv
-      load_wfrag(a.w, cg, wf);
       f32x4 acc[4][2];
       conv32(Xs, wave * 32, wf, acc);
 #pragma unroll
@@ -618,7 +641,7 @@ __global__ void __launch_bounds__(kRbNT, 2) stem_rc_bwd_kernel(StemRcArgs a, int
       const bool valid = px < Qs;
       const bool hodd = h & 1, wodd = it & 1;
       const uint4 yv = *reinterpret_cast<const uint4*>(Ys + tt_off(px, c8));
-      const uint4 av = *reinterpret_cast<const uint4*>(Ds + tt_off(px, c8));
+      const uint4 av = addv[it];
       const uint4 xv = *reinterpret_cast<const uint4*>(Xs + tt_off(px, c8));
       // the pooled cells that may have this pixel as their argmax, in
       // maxpool_bwd_kernel's order (rows p_lo, p_lo + 1; columns qa, qa + 1):
@@ -636,7 +659,7 @@ __global__ void __launch_bounds__(kRbNT, 2) stem_rc_bwd_kernel(StemRcArgs a, int
         const int p = p_lo + rr, q = qa + cc;
         const int kh = hodd ? (rr ? 0 : 2) : 1, kw = wodd ? (cc ? 0 : 2) : 1;
         const bool ok = valid && p <= p_hi && q < a.Qp;
-        const int slot = ok ? rr * kRbPQ + (q - qlo) : 0;
+        const int slot = ok ? (p & 1) * kRbPQ + (q - qlo) : 0;
         want[jj] = ok ? kh * 3 + kw : -1;
         ix[jj] = *reinterpret_cast<const uint2*>(Pi + slot * 64 + c8);
         pd[jj] = *reinterpret_cast<const uint4*>(Pd + slot * 128 + c8 * 2);
@@ -691,7 +714,7 @@ __global__ void __launch_bounds__(kRbNT, 2) stem_rc_bwd_kernel(StemRcArgs a, int
     }
     lds_sync();  // Pd / Pi read for the last time
     if (kt < 2) TSTAMP(a.tim, 9 + 9 * kt);
-    if (u + 1 < u1) pool_dma(u + 1);
+    if (u + 1 < u1) pool_dma(u + 1, false);
     // GEMMs over the unit's pixels: D[co][k] += sum_px S[px][co] im[px][k]
     {
       const char* S = (wave >> 1) ? Ys : Ds;
