@@ -1964,12 +1964,16 @@ int unet_profile_report(unet_plan* p, char* buf, int64_t buflen) {
   if (!p->recs.empty()) {
     if (hipEventSynchronize(p->evpool[p->recs.back().e1]) != hipSuccess) { set_err("event sync failed"); return -1; }
   }
-  char line[256];
+  char num[64];
   for (const auto& r : p->recs) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, p->evpool[r.e0], p->evpool[r.e1]) != hipSuccess) ms = -1.f;
-    std::snprintf(line, sizeof(line), "%s\t%.6f\t%.6e\t%s\n", r.name.c_str(), ms, r.flops, r.kernel.c_str());
-    out += line;
+    // names of batched launches list every layer: no fixed-size line buffer
+    std::snprintf(num, sizeof(num), "\t%.6f\t%.6e\t", ms, r.flops);
+    out += r.name;
+    out += num;
+    out += r.kernel;
+    out += '\n';
   }
   if (buf && buflen > 0) std::snprintf(buf, (size_t)buflen, "%s", out.c_str());
   return (int)out.size() + 1;
