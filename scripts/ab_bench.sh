@@ -11,7 +11,7 @@ for r in $(seq 1 $R); do
   i=0
   for kv in "$@"; do
     i=$((i+1))
-    v=$(env $(envs "$kv") timeout -k 10 120 python3 bench.py --no-cpu-baseline --steps 30 --warmup 10 2>/dev/null \
+    v=$(env $(envs "$kv") timeout -k 10 120 python3 bench.py --no-cpu-baseline --no-parity --steps 30 --warmup 10 2>/dev/null \
         | grep -o '"value": [0-9.]*' | grep -o '[0-9.]*$') || exit 1
     echo "round $r setting $i [$kv] $v" | tee -a gpurun_out/ab_bench.txt
   done
