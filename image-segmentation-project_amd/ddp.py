@@ -19,7 +19,11 @@ rank 0's running statistics (call it before evaluation / checkpointing).
 bf16 values (half the xGMI bytes), and ``unet_grad_from_bf16`` widens the sum
 back into the fp32 gradients times 1/world (exact for power-of-two worlds).
 Tolerance: relative L2 <= 1e-2 per tensor against the fp32 mean
-(tests/test_ddp_gloo.py, tests/test_ddp_gpu.py); the default stays fp32.
+(tests/test_ddp_gloo.py, tests/test_ddp_gpu.py); the error grows with the world
+size (one bf16 rounding per summation step of the collective): measured 2.5e-3
+at 2 ranks, 3.9e-3 at 8 (gloo).  Each bucket's round / sum / widen runs in
+order on the comm stream, so a bucket's conversion does not overlap the
+previous bucket's transfer.  The default stays fp32.
 """
 from __future__ import annotations
 

@@ -148,17 +148,23 @@ def _bf16_worker(rank, world, port, q):
         ddp.GradBucketReducer(ranges, grad_dtype="bf16").reduce(flat, lambda b, s: order.append(b))
         mean = sum(per_rank) / world
         rel = ((flat - mean).norm() / mean.norm()).item()
-        # world 2: a bf16 sum of two bf16 values is one rounding of their exact sum
+        # world 2: a bf16 sum of two bf16 values is one rounding of their exact sum;
+        # larger worlds round at every step of the collective's own summation
+        # order, so only the error bar applies there
         exact = (sum(t.bfloat16().float() for t in per_rank)).bfloat16().float() / world
-        q.put((rank, order == [0, 1, 2, 3], rel, bool(torch.equal(flat, exact))))
+        q.put((rank, order == [0, 1, 2, 3], rel, bool(torch.equal(flat, exact)) or world > 2))
     finally:
         dist.destroy_process_group()
 
 
-def test_bucket_reducer_bf16_exchange_gloo():
+@pytest.mark.parametrize("world", [2, 8])
+def test_bucket_reducer_bf16_exchange_gloo(world):
     """Opt-in bf16 gradient exchange (ddp.py): relative L2 <= 1e-2 against the
-    fp32 mean (measured ~3e-3), bit-equal to its own bf16 emulation."""
-    res = _spawn(_bf16_worker, 2)
+    fp32 mean, bit-equal to its own bf16 emulation at two ranks.  The error
+    grows with the world size (one bf16 rounding per summation step): measured
+    2.5e-3 at 2 ranks and 3.9e-3 at 8 (the largest world the bench launches;
+    gloo's summation order, RCCL's ring order differs), both under the 1e-2 bar."""
+    res = _spawn(_bf16_worker, world)
     print(res)
     for rank, order_ok, rel, exact in res:
         assert order_ok and exact and rel <= 1e-2, (rank, order_ok, rel, exact)
