@@ -410,7 +410,7 @@ __device__ __forceinline__ void commit_stats(const ConvFwdArgs& a, float (&q0)[F
 // weight-stationary (C = 32 * NP <= 96)
 // ---------------------------------------------------------------------------
 template <int NP, int FN, int TH, int NW, bool FLIP>
-__global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int ntiles, int ncg, int split) {
+__global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int ntiles, int ncg) {
   constexpr int COT = FN * 16;               // output channels per block
   constexpr int RW = TH / NW;                // output rows per wave
   constexpr int HPR = ((TH + 2) * kHW + 15) / 16 * 16;
@@ -507,89 +507,6 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
   __syncthreads();
   TSTAMP(a.tim, 1);
 
-  if (NW == 8 && !FLIP && split && !a.xform) {  // (dgrads: the held epilogue operands would spill)
-    // Two wave groups half a tile apart: waves 0-3 (A) and 4-7 (B) sit on the
-    // same four SIMDs (one of each per SIMD), and each half phase one group
-    // issues its MFMAs while the other runs its epilogue, so the matrix cores
-    // no longer idle through the stores / BN sums / address math.
-    //   A: | MFMA(t)     |Bar| epi(t)     |Bar'| MFMA(t+1) ...
-    //   B: | epi(t-1)    |Bar| MFMA(t)    |Bar'| epi(t)    ...
-    // Bar' (top): halo(t) landed in every wave's DMA part.  Bar: every MFMA of
-    // tile t-1 (and A's of tile t) is done, so halo(t+1) may go into the
-    // buffer tile t-1 used; it has half a tile to land.
-    const bool grpB = wave >= NW / 2;
-    const bool vec_all = (a.ldy % 8 == 0) && (!a.ysplit || (a.ldysplit % 8 == 0 && a.csplit % 8 == 0)) &&
-                         a.Cout % COT == 0;  // A's epilogue: exactly RW * FN / 2 stores per wave
-    TileEpi<FN, RW, FLIP, PREF, false> epi;  // operands of the tile whose epilogue is pending
-    size_t pix[RW];
-    f32x4 acc[RW][FN];
-    int k = 0;
-    for (; t < ntiles; ++k, t += nslot) {
-      const int b = k & 1;
-      if (k > 0) {
-        // this wave's part of halo(t) has landed; A's epilogue stores, issued
-        // after it, may stay in flight
-        if (!grpB && vec_all) wait_vmcnt<RW * FN / 2>();
-        else wait_vmcnt<0>();
-        __builtin_amdgcn_s_barrier();
-      }
-      if (k < 9) TSTAMP(a.tim, 2 + 2 * k);
-      int n, oh0, ow0;
-      tile_origin(t, n, oh0, ow0);
-      size_t pt[RW];
-#pragma unroll
-      for (int j = 0; j < RW; ++j) pt[j] = ((size_t)n * a.P + oh0 + wave * RW + j) * a.Q + ow0 + (lane & 15);
-      const char* H = hl + b * HBUF;
-      if (!grpB) {
-        if (PREF) epi.fetch(a, pt, co0, lane);
-#pragma unroll
-        for (int j = 0; j < RW; ++j)
-#pragma unroll
-          for (int i = 0; i < FN; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int p = 0; p < (UNET_ABL == 1 ? 0 : NP); ++p)
-          mfma_panel<FN, RW, NP * COT * 64, FLIP>(acc, wl + p * COT * 64, H + p * PANEL, aoff, boff);
-#pragma unroll
-        for (int j = 0; j < RW; ++j) pix[j] = pt[j];
-      } else if (k > 0) {
-        if (!PREF) epi.fetch(a, pix, co0, lane);
-        epi.landed();
-        epi.store(a, acc, pix, co0, lane, cst, q0, q1, q2);
-      }
-      __builtin_amdgcn_s_barrier();
-      if (k < 9) TSTAMP(a.tim, 3 + 2 * k);
-      if (!grpB) {
-        if (!PREF) epi.fetch(a, pix, co0, lane);
-        epi.landed();  // before this wave's DMA part: waits for tile t's operands only
-      } else if (PREF) {
-        epi.fetch(a, pt, co0, lane);
-      }
-      if (t + nslot < ntiles && UNET_ABL != 2) {
-        int n2, oh2, ow2;
-        tile_origin(t + nslot, n2, oh2, ow2);
-        issue_halo(hl + (b ^ 1) * HBUF, n2, oh2, ow2);
-      }
-      if (!grpB) {
-        epi.store(a, acc, pix, co0, lane, cst, q0, q1, q2);
-      } else {
-#pragma unroll
-        for (int j = 0; j < RW; ++j)
-#pragma unroll
-          for (int i = 0; i < FN; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int p = 0; p < (UNET_ABL == 1 ? 0 : NP); ++p)
-          mfma_panel<FN, RW, NP * COT * 64, FLIP>(acc, wl + p * COT * 64, H + p * PANEL, aoff, boff);
-#pragma unroll
-        for (int j = 0; j < RW; ++j) pix[j] = pt[j];
-      }
-    }
-    if (grpB && k > 0) {  // B's last tile
-      if (!PREF) epi.fetch(a, pix, co0, lane);
-      epi.landed();
-      epi.store(a, acc, pix, co0, lane, cst, q0, q1, q2);
-    }
-    wait_vmcnt<0>();
-  } else
   for (int k = 0; t < ntiles; ++k, t += nslot) {
     const int b = k & 1;
     if (t + nslot < ntiles && UNET_ABL != 2) {  // lands while this tile computes
@@ -1067,12 +984,8 @@ static hipError_t launch_ws(const ConvFwdArgs& a, hipStream_t st) {
   char tag[96];
   std::snprintf(tag, sizeof(tag), "conv3x3_ws_kernel<%d, %d, %d, %d, %s>", NP, FN, TH, NW, FLIP ? "true" : "false");
   conv_kernel_tag(tag);
-  // wave-group split schedule (conv3x3_ws_kernel, 8-wave shapes without the BN
-  // prologue), off by default: measured 0.5% slower end to end (2668 vs 2682 img/s,
-  // interleaved A/B); UNET_WS_SPLIT=1 selects it
-  static const int split = std::getenv("UNET_WS_SPLIT") ? std::atoi(std::getenv("UNET_WS_SPLIT")) : 0;
   hipLaunchKernelGGL((conv3x3_ws_kernel<NP, FN, TH, NW, FLIP>), dim3(slots * ncg), dim3(NW * 64), lds, st, a,
-                     ntiles, ncg, split);
+                     ntiles, ncg);
   return hipGetLastError();
 }
 

@@ -899,17 +899,27 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(HeadArgs a) {
   }
 }
 
-__global__ void head_grads_kernel(HeadArgs a) {
-  const double S = a.usum[a.Cin * 4];
-  for (int t = threadIdx.x; t < a.Cin * a.Co * 4; t += blockDim.x) {
+constexpr int kHeadMaxW0 = kHeadMaxCin * 32 * 4;  // Cin x Co x 4 (Wide: 64 x 32)
+__global__ void __launch_bounds__(256) head_grads_kernel(HeadArgs a) {
+  // usum and w0 staged in LDS first: the serial per-output loops below then
+  // read LDS instead of one dependent global load per term (same order, same
+  // arithmetic as before)
+  __shared__ double us[kHeadMaxCin * 4 + 1];
+  __shared__ float w0s[kHeadMaxW0];
+  const int nw = a.Cin * a.Co * 4;
+  for (int t = threadIdx.x; t <= a.Cin * 4; t += blockDim.x) us[t] = a.usum[t];
+  for (int t = threadIdx.x; t < nw; t += blockDim.x) w0s[t] = a.w0[t];
+  __syncthreads();
+  const double S = us[a.Cin * 4];
+  for (int t = threadIdx.x; t < nw; t += blockDim.x) {
     const int ab = t & 3, o = (t >> 2) % a.Co, c = (t >> 2) / a.Co;
-    a.gw0[t] = (float)((double)a.wf[o] * a.usum[c * 4 + ab]);
+    a.gw0[t] = (float)((double)a.wf[o] * us[c * 4 + ab]);
   }
   for (int o = threadIdx.x; o < a.Co; o += blockDim.x) {
     a.gb0[o] = (float)((double)a.wf[o] * S);
     double g = (double)a.b0[o] * S;
     for (int c = 0; c < a.Cin; ++c)
-      for (int ab = 0; ab < 4; ++ab) g += (double)a.w0[((size_t)c * a.Co + o) * 4 + ab] * a.usum[c * 4 + ab];
+      for (int ab = 0; ab < 4; ++ab) g += (double)w0s[(c * a.Co + o) * 4 + ab] * us[c * 4 + ab];
     a.gwf[o] = (float)g;
   }
   if (threadIdx.x == 0) a.gbf[0] = (float)S;
@@ -931,6 +941,7 @@ hipError_t launch_head_bwd(const HeadArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 hipError_t launch_head_grads(const HeadArgs& a, hipStream_t st) {
+  if (a.Cin > kHeadMaxCin || a.Cin * a.Co * 4 > kHeadMaxW0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(head_grads_kernel, dim3(1), dim3(256), 0, st, a);
   return hipGetLastError();
 }
@@ -1225,8 +1236,12 @@ __device__ __forceinline__ void loss_accum(float v, float y, int from_prob, floa
   s[7] += (1.f - pred) * (1.f - y);
 }
 
-__global__ void __launch_bounds__(256) loss_sums_kernel(const float* x, const float* t, int64_t n,
-                                                       double* sums, int from_prob) {
+// 1024 threads per block: 16 waves per CU hide the exp/log chains of the BCE
+// terms (at 4 waves the kernel took 37 us for 4.2 M pixels); the block count
+// stays at <= 256 (same-address fp64 atomics are serialised)
+constexpr int kLossNT = 1024;
+__global__ void __launch_bounds__(kLossNT) loss_sums_kernel(const float* x, const float* t, int64_t n,
+                                                            double* sums, int from_prob) {
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1256,7 +1271,7 @@ __global__ void __launch_bounds__(256) loss_sums_kernel(const float* x, const fl
     done = n4 << 2;
   }
   for (int64_t i = done + tid; i < n; i += nthr) loss_accum(x[i], t[i], from_prob, s);
-  __shared__ double red[4][8];
+  __shared__ double red[kLossNT / 64][8];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -1266,13 +1281,15 @@ __global__ void __launch_bounds__(256) loss_sums_kernel(const float* x, const fl
   __syncthreads();
   if (threadIdx.x < 8) {
     const int k = threadIdx.x;
-    atomicAdd(sums + k, red[0][k] + red[1][k] + red[2][k] + red[3][k]);
+    double v = 0.0;
+    for (int w = 0; w < kLossNT / 64; ++w) v += red[w][k];
+    atomicAdd(sums + k, v);
   }
 }
 
 hipError_t launch_loss_sums(const float* logits, const float* target, int64_t n, double* sums, int from_prob,
                             hipStream_t st) {
-  hipLaunchKernelGGL(loss_sums_kernel, dim3(grid_for(n, 256 * 16, 256)), dim3(256), 0, st, logits, target, n,
+  hipLaunchKernelGGL(loss_sums_kernel, dim3(grid_for(n, kLossNT * 16, 256)), dim3(kLossNT), 0, st, logits, target, n,
                      sums, from_prob);
   return hipGetLastError();
 }

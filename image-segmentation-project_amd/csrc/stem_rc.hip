@@ -380,15 +380,30 @@ __global__ void __launch_bounds__(kRcNT) stem_rc_fwd_kernel(StemRcArgs a, int pe
 // centring value): block b sums elements b, b + G, b + 2G, ... per thread in
 // order, then a fixed tree.
 constexpr int kRcImBlocks = 256;
-__global__ void __launch_bounds__(256) stem_rc_imsum_kernel(StemRcArgs a) {
-  __shared__ float red[256];
-  const size_t n = (size_t)a.N * a.H * a.W;
-  const size_t stride = (size_t)kRcImBlocks * 256;
+constexpr int kRcImNT = 1024;
+__global__ void __launch_bounds__(kRcImNT) stem_rc_imsum_kernel(StemRcArgs a) {
+  // 1024 threads x float4 x 4 in flight per block (the one-load-at-a-time
+  // scalar loop took 27 us for 16.8 MB); fixed order: per thread, then a tree
+  __shared__ float red[kRcImNT];
+  const size_t n = (size_t)a.N * a.H * a.W;  // a multiple of 4 (W even, H even)
+  const size_t n4 = n >> 2;
+  const float4* img4 = reinterpret_cast<const float4*>(a.img);
+  const size_t stride = (size_t)kRcImBlocks * kRcImNT;
   float s = 0.f;
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) s += a.img[i];
+  if ((reinterpret_cast<uintptr_t>(a.img) & 15) == 0) {
+    for (size_t i = (size_t)blockIdx.x * kRcImNT + threadIdx.x; i < n4; i += 4 * stride) {
+      float4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = i + k * stride < n4 ? img4[i + k * stride] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+    }
+  } else {  // a misaligned image view: scalar loads
+    for (size_t i = (size_t)blockIdx.x * kRcImNT + threadIdx.x; i < n; i += stride) s += a.img[i];
+  }
   red[threadIdx.x] = s;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
+  for (int o = kRcImNT / 2; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
     __syncthreads();
   }
@@ -942,7 +957,7 @@ hipError_t launch_stem_rc_bwd(const StemRcArgs& a, int stage, hipStream_t st) {
   const int chunks = (kRbPartF4 + 63) / 64;
   if (stage == 0) {
     conv_kernel_tag("stem_rc_bwd_kernel");
-    hipLaunchKernelGGL(stem_rc_imsum_kernel, dim3(kRcImBlocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(stem_rc_imsum_kernel, dim3(kRcImBlocks), dim3(kRcImNT), 0, st, a);
     hipLaunchKernelGGL(stem_rc_bwd_kernel, dim3(blocks, groups), dim3(kRbNT), kRbLds, st, a, per);
   } else {
     conv_kernel_tag("stem_rc_sum1/sum2/finalize");
