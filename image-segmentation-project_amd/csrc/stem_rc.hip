@@ -413,10 +413,13 @@ __global__ void __launch_bounds__(kRcImNT) stem_rc_imsum_kernel(StemRcArgs a) {
 // ---------------------------------------------------------------------------
 // backward.  256 threads, 2 blocks per CU; a unit is one half row (128
 // pixels) of the stem output; a block owns units [u0, u1) of channel group
-// blockIdx.y.  All of a unit's global reads (the 1-2 pooled rows of dpool and
-// idx it needs, the skip gradient) are issued at the unit's start, into
-// registers, and land while the conv is recomputed; the pooled rows are then
-// staged in LDS and the maxpool backward gathers from there.
+// blockIdx.y.  Per unit: the input patch (prefetched by counted buffer loads
+// while the previous unit ran) is stored to LDS and expanded to im2col; the
+// skip gradient is loaded into registers; the conv is recomputed; the dZ phase
+// gathers the maxpool backward from the pooled rows (LDS-DMA issued one unit
+// ahead, after the previous unit's dZ phase), adds the skip gradient, applies
+// the ReLU mask and forms the BN-backward sums, xhat and the centred im2col;
+// then the two weight-gradient GEMMs.
 // LDS: patch (7 x 264 bf16) | Xs im2col [128][64] | Ys y/xhat [128][64] |
 //      Ds dZ [128][64] | coefficients [5][64] f32 | Pd dpool [2 slots][65][64] | Pi idx [2 slots][65][64] u8
 // Units run down the rows of one 128-column segment (u = s * N * P + n * P + h),
