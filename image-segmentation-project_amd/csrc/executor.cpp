@@ -827,8 +827,11 @@ struct Ctx {
   float* const* buf;
   hipStream_t st;
   int training;
-  hipStream_t wst = nullptr;  // weight-gradient stream (== st when single-stream)
-  hipStream_t rst = nullptr;  // split-K reduction stream (== wst when serial)
+  // weight-gradient and split-K reduction streams: both are st (the backward
+  // is single-stream since the two-stream variants were removed);
+  // kept as names so the launch sites say which role a launch plays
+  hipStream_t wst = nullptr;
+  hipStream_t rst = nullptr;
   bf16_t* A(const Act& a) const { return reinterpret_cast<bf16_t*>(ws + a.off); }
   template <class T> T* W(size_t off) const { return reinterpret_cast<T*>(ws + off); }
 };
