@@ -157,18 +157,25 @@ def launch_ranks(n: int) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
-def miou_parity(model, x, y, width: int, attention: bool, backbone: str = "resnet34"):
+def miou_parity(model, x, y, width: int, attention: bool, backbone: str = "resnet34", reference: bool = True):
     """North-star parity on the bench batch: foreground IoU of the HIP train-mode
     forward vs the oracle (fp32 CPU restatement of the reference) on the same
-    weights and images, reference aggregation (utils.py:120-151)."""
-    import oracle
+    weights and images, reference aggregation (utils.py:120-151).  Every rank
+    runs the HIP forward (it moves the BN running statistics and the fp8
+    delayed-amax state, so all ranks must take it before the timed steps);
+    only the rank with reference=True runs the oracle."""
     pkg = importlib.import_module("image-segmentation-project_amd")
-    ref = oracle.ReferenceUNet(width=width, use_attention=attention, backbone=backbone)
-    ref.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()})
-    ref.train()
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()} if reference else None
     with torch.no_grad():
         out = model(x)
         miou = pkg.calculate_metrics_from_logits(out, y)["iou"]
+    if not reference:
+        return miou, None
+    import oracle
+    ref = oracle.ReferenceUNet(width=width, use_attention=attention, backbone=backbone)
+    ref.load_state_dict(sd)
+    ref.train()
+    with torch.no_grad():
         rl = ref(x.cpu())
         miou_ref = oracle.calculate_metrics(torch.sigmoid(rl), y.cpu())["iou"]
     return miou, miou_ref
@@ -239,8 +246,10 @@ def main():
     y = torch.from_numpy(ms).to(dev)
     model.train()
     parity = None
-    if rank == 0 and not args.no_parity:
-        parity = miou_parity(model, x, y, args.width, args.attention, args.backbone)  # step-0 weights
+    if not args.no_parity:  # step-0 weights; the HIP forward on every rank, the oracle on rank 0
+        parity = miou_parity(model, x, y, args.width, args.attention, args.backbone, reference=rank == 0)
+        if rank != 0:
+            parity = None
     if world > 1:
         dist.barrier()
 

@@ -119,6 +119,61 @@ __device__ __forceinline__ void mfma_panel(f32x4 (&acc)[RW][FN], const char* W, 
     }
 }
 
+// ---- full-line staging (64 reduction channels = one 128-B line per pixel /
+// weight row): an LDS-DMA piece of 64 B fetches half a line, and the per-CU
+// L2 -> LDS rate is set by lines, not bytes (scripts/micro/dma_rate.hip,
+// profiles/r05: 32 B/clk/CU for 64-B pieces, 54 for whole lines from L2; 3.5
+// vs 6.7 TB/s chip-wide from HBM).  A 128-B LDS row holds both 32-channel
+// panels; 16-B chunk q = 4 p + c of row r sits at physical chunk q ^ (r & 6),
+// which keeps every ds_read_b128 lane group of a 16-row fragment on 16
+// distinct bank slots for any start row and either panel (exhaustive search
+// over the gfx950 lane groups).  Panel 1 of a row = panel 0's offset ^ 64.
+__device__ __forceinline__ int fl_off(int row, int chunk) {  // byte offset of panel-0 chunk `chunk` of `row`
+  return row * 128 + ((chunk ^ (row & 6)) << 4);
+}
+
+// all 9 taps x COT output rows x 64 reduction channels (weights [Cout][9][64],
+// full lines), LDS layout [tap][co][128 B]
+template <int COT, int NW>
+__device__ __forceinline__ void issue_weight_dma_fl(const ConvFwdArgs& a, __amdgpu_buffer_rsrc_t wr, char* dst, int co0,
+                                                    int wave, int lane) {
+  const int K = a.C;
+  constexpr int nins = 9 * COT / 8;
+  for (int ins = wave; ins < nins; ins += NW) {
+    const int rowg = ins * 8 + (lane >> 3);
+    const int co = rowg % COT, tap = rowg / COT;
+    const int q = (lane & 7) ^ (co & 6);  // logical 16-B chunk = 8 channels
+    unsigned off = kOOB;
+    if (co0 + co < a.Cout) off = (unsigned)(((co0 + co) * 9 * K + tap * K + q * 8) * 2);
+    glds16(wr, dst + ins * 1024, off);
+  }
+}
+
+// both panels of a full-line stage: 9 taps x RW rows x FN channel fragments
+// per panel; aoff / boff are panel-0 offsets (fl_off)
+template <int FN, int RW, int COT, bool FLIP>
+__device__ __forceinline__ void mfma_fl(f32x4 (&acc)[RW][FN], const char* W, const char* H, int aoff,
+                                        const int (&boff)[RW + 2][3]) {
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        bf16x8 A[FN];
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+          A[i] = *reinterpret_cast<const bf16x8*>(W + (r * 3 + s) * COT * 128 + i * 2048 + (aoff ^ (p << 6)));
+        const int dr = FLIP ? 2 - r : r, ds = FLIP ? 2 - s : s;
+#pragma unroll
+        for (int j = 0; j < RW; ++j) {
+          const bf16x8 B = *reinterpret_cast<const bf16x8*>(H + (boff[j + dr][ds] ^ (p << 6)));
+#pragma unroll
+          for (int i = 0; i < FN; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B, acc[j][i], 0, 0, 0);
+        }
+      }
+}
+
 // Epilogue of one tile: bias, addend, ReLU mask (fused BN backward), bf16
 // store, BN sums accumulated in registers (q0, q1).  cst = LDS [3][COT]
 // bias | mean | invstd.  The per-pixel operands of a dgrad (addend, forward
@@ -441,7 +496,10 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
   const i32x4 xr = make_rsrc_sgpr(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
   const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (unsigned)((size_t)a.Cout * 9 * a.C * 2));
 
-  issue_weight_dma<COT, NW>(a, wr, wl, co0, 0, NP, wave, lane);  // all 9 taps, once
+  // NP == 2 (64 channels): full-line staging of the weights and the halo (fl_off)
+  constexpr bool FL = NP == 2;
+  if constexpr (FL) issue_weight_dma_fl<COT, NW>(a, wr, wl, co0, wave, lane);  // all 9 taps, once
+  else issue_weight_dma<COT, NW>(a, wr, wl, co0, 0, NP, wave, lane);
   load_epi_constants<COT>(a, cst, co0, tid, NW * 64);
   if (!FLIP && a.xform) {  // the previous BN's affine map (bn_apply's coefficients)
     for (int c = tid; c < NP * 32; c += NW * 64) {
@@ -458,25 +516,36 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
 
   // loop-invariant fragment offsets: weights (16 co rows from co = 0) and the
   // halo rows this wave's output rows need for every tap shift
-  const int aoff = ws_off(lane & 15, lane >> 4);
+  const int aoff = FL ? fl_off(lane & 15, lane >> 4) : ws_off(lane & 15, lane >> 4);
   int boff[RW + 2][3];
 #pragma unroll
   for (int h = 0; h < RW + 2; ++h)
 #pragma unroll
-    for (int d = 0; d < 3; ++d) boff[h][d] = ws_off((wave * RW + h) * kHW + d + (lane & 15), lane >> 4);
+    for (int d = 0; d < 3; ++d) {
+      const int row = (wave * RW + h) * kHW + d + (lane & 15);
+      boff[h][d] = FL ? fl_off(row, lane >> 4) : ws_off(row, lane >> 4);
+    }
 
   // per-lane constant part of the halo DMA (pixel of the halo, channel
-  // offset); per tile only the image bounds test and the address remain
-  constexpr int H_NINS = NP * HPR / 16, H_PER = (H_NINS + NW - 1) / NW;
+  // offset); per tile only the image bounds test and the address remain.
+  // FL: 8 pixels x 128 B per instruction, else 16 pixels x 64 B of one panel
+  constexpr int H_NINS = FL ? HPR / 8 : NP * HPR / 16, H_PER = (H_NINS + NW - 1) / NW;
   int hrow[H_PER], hcol[H_PER], hch[H_PER];
 #pragma unroll
   for (int k = 0; k < H_PER; ++k) {
-    const int rowg = (wave + k * NW) * 16 + (lane >> 2);
-    const int p = rowg / HPR, hp = rowg - p * HPR;
-    const int lchunk = (lane & 3) ^ ((hp >> 1) & 2);
+    int hp, ch;
+    if constexpr (FL) {
+      hp = (wave + k * NW) * 8 + (lane >> 3);
+      ch = ((lane & 7) ^ (hp & 6)) * 8;
+    } else {
+      const int rowg = (wave + k * NW) * 16 + (lane >> 2);
+      const int p = rowg / HPR;
+      hp = rowg - p * HPR;
+      ch = p * 32 + ((lane & 3) ^ ((hp >> 1) & 2)) * 8;
+    }
     hrow[k] = hp < (TH + 2) * kHW ? hp / kHW - 1 : -(1 << 20);  // invalid rows fail the bounds test
     hcol[k] = hp - (hp / kHW) * kHW - 1;
-    hch[k] = p * 32 + lchunk * 8;
+    hch[k] = ch;
   }
   auto issue_halo = [&](char* dst, int n, int oh0, int ow0) {
 #pragma unroll
@@ -530,14 +599,23 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
       for (int it = 0; it < XI; ++it) {
         const int idx = tid + it * NW * 64;
         if (idx >= NP * HPR * 4) break;
-        const int p = idx / (HPR * 4), rem = idx - p * (HPR * 4);
-        const int row = rem >> 2, ch = rem & 3;
+        int row, c0;
+        uint4* q;
+        if constexpr (FL) {  // physical chunk idx & 7 of row idx >> 3 holds channels 8 (phys ^ (row & 6))
+          row = idx >> 3;
+          q = reinterpret_cast<uint4*>(Hb + idx * 16);
+          c0 = ((idx & 7) ^ (row & 6)) * 8;
+        } else {
+          const int p = idx / (HPR * 4), rem = idx - p * (HPR * 4);
+          const int ch = rem & 3;
+          row = rem >> 2;
+          q = reinterpret_cast<uint4*>(Hb + p * PANEL + ws_off(row, ch));
+          c0 = p * 32 + ch * 8;
+        }
         if (row >= (TH + 2) * kHW) continue;
         const int hr = row / kHW, hc = row - hr * kHW;
         const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
         if ((unsigned)ih >= (unsigned)a.H || (unsigned)iw >= (unsigned)a.W) continue;
-        uint4* q = reinterpret_cast<uint4*>(Hb + p * PANEL + ws_off(row, ch));
-        const int c0 = p * 32 + ch * 8;
         float v[8];
         unpack8(*q, v);
 #pragma unroll
@@ -558,9 +636,13 @@ __global__ void __launch_bounds__(NW * 64) conv3x3_ws_kernel(ConvFwdArgs a, int 
     for (int j = 0; j < RW; ++j)
 #pragma unroll
       for (int i = 0; i < FN; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (FL) {
+      if (UNET_ABL != 1) mfma_fl<FN, RW, COT, FLIP>(acc, wl, H, aoff, boff);
+    } else {
 #pragma unroll
-    for (int p = 0; p < (UNET_ABL == 1 ? 0 : NP); ++p)
-      mfma_panel<FN, RW, NP * COT * 64, FLIP>(acc, wl + p * COT * 64, H + p * PANEL, aoff, boff);
+      for (int p = 0; p < (UNET_ABL == 1 ? 0 : NP); ++p)
+        mfma_panel<FN, RW, NP * COT * 64, FLIP>(acc, wl + p * COT * 64, H + p * PANEL, aoff, boff);
+    }
     // stamps: 2 per tile (after the MFMAs, after the epilogue); UNET_ABL == 3
     // (fine build): 4 per tile for the first 4 tiles (+ after the wait, after the barrier)
     if (UNET_ABL >= 3 ? k < 3 : k < 9) TSTAMP(a.tim, UNET_ABL >= 3 ? 3 + 5 * k : 2 + 2 * k);

@@ -1440,6 +1440,29 @@ constexpr int kWlStage = kWlA + kWlB;     // 53,248 B; 3 stages = 159,744 B of L
 constexpr int kWlHIns = 32;               // halo DMA instructions per stage (30 used + 2 zero-fill)
 constexpr int kWlLps = 16 / kWlNL + kWlHIns / kWlNL;  // LDS-DMA per loader wave per stage
 
+// Output-pixel tile geometry of the batched weight gradient (TW x TH = 128
+// pixels = one 128-row dY image per item).  TW = 32: 32 x 4 tiles, a 6 x 34
+// halo at a pitch of 48 LDS rows (the layout of wgrad3x3_ld_kernel).  TW = 16
+// (Q = 16 layers, enc4 at 512^2): 16 x 8 tiles, a 10 x 18 halo stored densely
+// (pitch 18; 180 rows + 12 zero rows = 24 DMA instructions).  Both swizzle a
+// halo pixel's 32-B units by its COLUMN (tr_off<64> of the column), so an image
+// row is a constant byte offset and every fragment read is base + immediate;
+// an even pitch keeps a half-wave's 8 rows on distinct banks (tr_off<64>).
+template <int TW>
+struct WbGeo;
+template <>
+struct WbGeo<32> {
+  static constexpr int TH = 4, HIR = 6, PITCH = kWlHP, HINS = kWlHIns, B = kWlB;
+};
+template <>
+struct WbGeo<16> {
+  static constexpr int TH = 8, HIR = 10, PITCH = 18, HINS = 24, B = 24 * 1024;
+};
+template <int TW>
+constexpr int wb_stage() { return kWlA + WbGeo<TW>::B; }
+template <int TW>
+constexpr int wb_lps() { return 16 / kWlNL + WbGeo<TW>::HINS / kWlNL; }
+
 __global__ void __launch_bounds__((kWlNW + kWlNL) * 64)
 wgrad3x3_ld_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
   constexpr int TW = 32, TH = 4;
@@ -1631,7 +1654,9 @@ __device__ __forceinline__ long long wb_begin(const WgBatchArgs& a, int b) { ret
 
 // the loaders' position, with the current layer's fields and the tile origin
 // kept incrementally (no per-stage divisions or kernel-argument loads)
+template <int TW>
 struct WbLoad {
+  static constexpr int TH = WbGeo<TW>::TH;
   int l, tile, cob, cib, n, oh0, ow0;
   const bf16_t* dy;
   const bf16_t* x;
@@ -1650,17 +1675,17 @@ struct WbLoad {
     tile = p.tile;
     cob = p.combo % co_blocks;
     cib = p.combo / co_blocks;
-    const int tq = W / 32, tp = H / 4;
+    const int tq = W / TW, tp = H / TH;
     n = tile / (tp * tq);
     const int rem = tile - n * (tp * tq);
-    oh0 = (rem / tq) * 4;
-    ow0 = (rem % tq) * 32;
+    oh0 = (rem / tq) * TH;
+    ow0 = (rem % tq) * TW;
   }
   __device__ __forceinline__ void next(const WgBatchArgs& a) {
-    ow0 += 32;
+    ow0 += TW;
     if (ow0 == W) {
       ow0 = 0;
-      oh0 += 4;
+      oh0 += TH;
       if (oh0 == H) {
         oh0 = 0;
         ++n;
@@ -1679,8 +1704,10 @@ struct WbLoad {
   }
 };
 
+template <int TW>
 __global__ void __launch_bounds__((kWlNW + kWlNL) * 64) wgrad3x3_batch_kernel(WgBatchArgs a) {
-  constexpr int TW = 32;
+  typedef WbGeo<TW> G;
+  constexpr int STAGE = wb_stage<TW>(), LPS = wb_lps<TW>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   typedef TrTile<64, 64, 128> TA;
   TSTAMP_RT(a.tim, 30);
@@ -1693,8 +1720,9 @@ __global__ void __launch_bounds__((kWlNW + kWlNL) * 64) wgrad3x3_batch_kernel(Wg
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
   if (wave >= kWlNW) {
-    // ---- loader wave lw (the instruction split of wgrad3x3_ld_kernel) ----
-    constexpr int AI = 16 / kWlNL, HI = kWlHIns / kWlNL;
+    // ---- loader wave lw: dY instructions 4 lw .. 4 lw + 3 of 16, halo
+    // instructions HI lw .. HI lw + HI - 1 of G::HINS ----
+    constexpr int AI = 16 / kWlNL, HI = G::HINS / kWlNL;
     const int lw = wave - kWlNW;
     const int lrow = lane >> 3, lslot = lane & 7;
     int arow[AI], alch[AI];
@@ -1709,16 +1737,28 @@ __global__ void __launch_bounds__((kWlNW + kWlNL) * 64) wgrad3x3_batch_kernel(Wg
 #pragma unroll
     for (int j = 0; j < HI; ++j) {
       const int idx = lw * HI + j;
-      const bool pad = idx >= 30;
-      const int ir = pad ? idx - 30 : idx / 5;
-      const int col = (pad ? 40 : (idx % 5) * 8) + lrow;
-      const int f = ((col >> 1) & 1) | (((col >> 3) & 1) << 1);
+      int hr, hc, dst;
+      bool ok;
+      if constexpr (TW == 32) {  // image row idx / 5, 8-column block idx % 5; 30, 31 zero-fill
+        const bool pad = idx >= 30;  // the never-read padding rows 40-47 of image rows 0 and 1
+        hr = pad ? idx - 30 : idx / 5;
+        hc = (pad ? 40 : (idx % 5) * 8) + lrow;
+        ok = !pad && hc < TW + 2;
+        dst = (hr * G::PITCH + (pad ? 40 : (idx % 5) * 8)) * 128;
+      } else {  // dense: LDS row 8 idx + lrow = halo pixel (row / 18, row % 18)
+        const int row = idx * 8 + lrow;
+        hr = row / G::PITCH;
+        hc = row - hr * G::PITCH;
+        ok = row < G::HIR * G::PITCH;
+        dst = idx * 1024;
+      }
+      const int f = ((hc >> 1) & 1) | (((hc >> 3) & 1) << 1);  // the column's swizzle (tr_off<64>)
       hlch[j] = (((lslot >> 1) ^ f) << 1) | (lslot & 1);
-      hrr[j] = (!pad && col < TW + 2) ? ir - 1 : -(1 << 20);
-      hcc[j] = col - 1;
-      hdst[j] = (ir * kWlHP + (pad ? 40 : (idx % 5) * 8)) * 128;
+      hrr[j] = ok ? hr - 1 : -(1 << 20);  // rows past the halo fail the bounds test
+      hcc[j] = hc - 1;
+      hdst[j] = dst;
     }
-    WbLoad pos;
+    WbLoad<TW> pos;
     pos.locate(a, i0);
     auto issue = [&](int buf) {  // the stage of item `pos`, then advance
       const int H = pos.H, W = pos.W, lddy = pos.lddy, ldx = pos.ldx;
@@ -1726,7 +1766,7 @@ __global__ void __launch_bounds__((kWlNW + kWlNL) * 64) wgrad3x3_batch_kernel(Wg
       const int co0 = pos.cob * 64, c0 = pos.cib * 64;
       const i32x4 dyr = make_rsrc_sgpr(pos.dy, (unsigned)((size_t)a.N * H * W * lddy * 2));
       const i32x4 xr = make_rsrc_sgpr(pos.x, (unsigned)((size_t)a.N * H * W * ldx * 2));
-      char* As = smem + buf * kWlStage;
+      char* As = smem + buf * STAGE;
       char* Bs = As + kWlA;
       const unsigned abase = (unsigned)(((n * H + oh0) * W + ow0) * lddy) * 2u;
 #pragma unroll
@@ -1747,7 +1787,7 @@ __global__ void __launch_bounds__((kWlNW + kWlNL) * 64) wgrad3x3_batch_kernel(Wg
     for (int s = 0; s < kWlNS - 1; ++s)
       if (s < KT) issue(s);
     for (int kt = 0; kt < KT; ++kt) {
-      if (KT - 1 - kt >= kWlNS - 2) wait_vmcnt<(kWlNS - 2) * kWlLps>();
+      if (KT - 1 - kt >= kWlNS - 2) wait_vmcnt<(kWlNS - 2) * LPS>();
       else wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
       if (kt + kWlNS - 1 < KT && UNET_ABL != 2) issue((kt + kWlNS - 1) % kWlNS);
@@ -1758,13 +1798,23 @@ __global__ void __launch_bounds__((kWlNW + kWlNL) * 64) wgrad3x3_batch_kernel(Wg
   // ---- compute waves ----
   const int wm = wave & 1, wn = wave >> 1;
   const int g = lane >> 4, li = lane & 15, trq = li >> 2, trp = li & 3;
+  // dY pixel 8g + trq (+4) of k-step 0 (a k-step adds 32 pixel rows = 4096 B).
+  // Halo: k-step kk, tap (r, s) reads, for k = pixel 8g + j of the k-step, the
+  // halo pixel of tile pixel 32 kk + 8g + j shifted by (r, s).  TW = 32: image
+  // row kk + r, column 8g + j + s; TW = 16: image row 2 kk + (g >> 1) + r,
+  // column 8 (g & 1) + j + s.  boff holds the column part (+ the g >> 1 row),
+  // an image row adds PITCH LDS rows.
   int aoff[2][2], boff[3][2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) aoff[i][h] = TA::off(8 * g + trq + 4 * h, wm * 32 + i * 16 + 4 * trp);
 #pragma unroll
-    for (int s = 0; s < 3; ++s) boff[s][h] = tr_off<64>(8 * g + trq + s + 4 * h, wn * 16 + 4 * trp);
+    for (int s = 0; s < 3; ++s) {
+      if constexpr (TW == 32) boff[s][h] = tr_off<64>(8 * g + trq + s + 4 * h, wn * 16 + 4 * trp);
+      else
+        boff[s][h] = (g >> 1) * G::PITCH * 128 + tr_off<64>(8 * (g & 1) + trq + s + 4 * h, wn * 16 + 4 * trp);
+    }
   }
   WbPos pos;
   pos.locate(a, i0);
@@ -1778,7 +1828,7 @@ __global__ void __launch_bounds__((kWlNW + kWlNL) * 64) wgrad3x3_batch_kernel(Wg
   for (int kt = 0; kt < KT; ++kt) {
     __builtin_amdgcn_s_barrier();  // the loaders have waited for stage kt
     if (kt < 16) TSTAMP(a.tim, 2 + kt);
-    const char* As = smem + (kt % kWlNS) * kWlStage;
+    const char* As = smem + (kt % kWlNS) * STAGE;
     const char* Bs = As + kWlA;
     if (UNET_ABL != 1) {
       bf16x8 af[4][2];
@@ -1786,19 +1836,25 @@ __global__ void __launch_bounds__((kWlNW + kWlNL) * 64) wgrad3x3_batch_kernel(Wg
       for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
         for (int i = 0; i < 2; ++i) af[kk][i] = tr_read8(As + aoff[i][0] + kk * 4096, As + aoff[i][1] + kk * 4096);
+      // halo image row h serves the (k-step kk, tap row r) pairs with h = kk + r
+      // (TW = 32) or h = 2 kk + r (TW = 16): each fragment is read once
+      constexpr int KS = TW == 32 ? 1 : 2, NH = 3 * KS + 3;
 #pragma unroll
-      for (int h = 0; h < 6; ++h) {
+      for (int h = 0; h < NH; ++h) {
         bf16x8 bfr[3];
 #pragma unroll
-        for (int s = 0; s < 3; ++s) bfr[s] = tr_read8(Bs + boff[s][0] + h * 6144, Bs + boff[s][1] + h * 6144);
+        for (int s = 0; s < 3; ++s)
+          bfr[s] = tr_read8(Bs + boff[s][0] + h * G::PITCH * 128, Bs + boff[s][1] + h * G::PITCH * 128);
 #pragma unroll
-        for (int kk = (h > 2 ? h - 2 : 0); kk <= (h < 3 ? h : 3); ++kk)
+        for (int kk = 0; kk < 4; ++kk) {
+          const int r = h - KS * kk;
+          if (r < 0 || r > 2) continue;
 #pragma unroll
           for (int s = 0; s < 3; ++s)
 #pragma unroll
             for (int i = 0; i < 2; ++i)
-              acc[(h - kk) * 3 + s][i] =
-                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[s], acc[(h - kk) * 3 + s][i], 0, 0, 0);
+              acc[r * 3 + s][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[s], acc[r * 3 + s][i], 0, 0, 0);
+        }
       }
     }
     if (pos.tile == tiles - 1 || kt == KT - 1) {  // the unit's last item in this block
@@ -2652,9 +2708,15 @@ static hipError_t launch_wgrad_ld(const ConvWgradArgs& a0, hipStream_t st) {
   return hipGetLastError();
 }
 
+int wgrad_batch_tw(const ConvWgradArgs& a) {
+  if (a.Q % 32 == 0 && a.P % 4 == 0) return 32;
+  if (a.Q % 16 == 0 && a.P % 8 == 0) return 16;
+  return 0;
+}
+
 bool wgrad_batch_ok(const ConvWgradArgs& a) {
   return a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.C % 64 == 0 && a.Cout % 64 == 0 && a.P == a.H &&
-         a.Q == a.W && a.Q % 32 == 0 && a.P % 4 == 0 && !a.dy2 && !a.bn_fuse && a.lddy % 8 == 0 &&
+         a.Q == a.W && wgrad_batch_tw(a) != 0 && !a.dy2 && !a.bn_fuse && a.lddy % 8 == 0 &&
          a.ldx % 8 == 0 && (size_t)a.N * a.H * a.W * a.ldx * 2 < 0x80000000ull &&
          (size_t)a.N * a.P * a.Q * a.lddy * 2 < 0x80000000ull;
 }
@@ -2685,10 +2747,18 @@ int wgrad_batch_maxseg(const WgBatchArgs& a) {
   return m;
 }
 
+template <int TW>
+static void launch_wgrad_batch_tw(const WgBatchArgs& a, hipStream_t st) {
+  constexpr size_t lds = (size_t)kWlNS * wb_stage<TW>();
+  static_assert(lds <= 163840, "LDS");
+  set_kernel_tag("wgrad3x3_batch_kernel<%d>", TW);
+  hipLaunchKernelGGL(wgrad3x3_batch_kernel<TW>, dim3(a.grid), dim3((kWlNW + kWlNL) * 64), lds, st, a);
+}
+
 hipError_t launch_wgrad_batch(const WgBatchArgs& a, hipStream_t st) {
-  constexpr size_t lds = (size_t)kWlNS * kWlStage;
-  set_kernel_tag("wgrad3x3_batch_kernel");
-  hipLaunchKernelGGL(wgrad3x3_batch_kernel, dim3(a.grid), dim3((kWlNW + kWlNL) * 64), lds, st, a);
+  if (a.tw == 32) launch_wgrad_batch_tw<32>(a, st);
+  else if (a.tw == 16) launch_wgrad_batch_tw<16>(a, st);
+  else return hipErrorInvalidValue;
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(wgrad_batch_reduce_kernel, dim3(a.units, (unsigned)(kWbPartBytes / 16 / 256)), dim3(256), 0, st,

@@ -1066,13 +1066,16 @@ int flush_wgrad_batch(const Ctx& x) {
   const size_t cap = 2 * p->wslab_bytes / kWbPartBytes;  // slab slots
   size_t first = 0;
   while (first < p->wgb.size()) {
-    // as many layers as the table and the slab hold
-    size_t n = std::min(p->wgb.size() - first, (size_t)kWbMaxLayers);
+    // as many layers of one tile geometry as the table and the slab hold
+    const int tw = wgrad_batch_tw(p->wgb[first]);
+    size_t n = 0;
+    while (first + n < p->wgb.size() && n < (size_t)kWbMaxLayers && wgrad_batch_tw(p->wgb[first + n]) == tw) ++n;
     WgBatchArgs b;
     for (;;) {
       b = WgBatchArgs{};
       b.grid = grid;
       b.N = p->cfg.N;
+      b.tw = tw;
       long long items = 0;
       int units = 0;
       for (size_t j = 0; j < n; ++j) {
@@ -1080,7 +1083,7 @@ int flush_wgrad_batch(const Ctx& x) {
         WgBatchLayer& L = b.L[j];
         L.dy = a.dy; L.x = a.x; L.dw = a.dw;
         L.H = a.H; L.W = a.W; L.C = a.C; L.Cout = a.Cout; L.lddy = a.lddy; L.ldx = a.ldx;
-        L.tq = a.Q / 32; L.tp = a.P / 4;
+        L.tq = a.Q / tw; L.tp = a.P / (128 / tw);
         L.co_blocks = a.Cout / 64; L.c_blocks = a.C / 64;
         L.tiles = a.N * L.tp * L.tq;
         L.unit0 = units; L.item0 = items;
@@ -1770,7 +1773,7 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     s.part = x.W<float>(p->stem_part);
     s.l2 = reinterpret_cast<double*>(s.part + stem_rc_l2_offset(N, p->y0.H, p->y0.W, p->x1.C) / sizeof(float));
     s.tot = x.W<double>(p->stem_tot);
-    s.imsum = reinterpret_cast<float*>(s.tot + (size_t)(p->x1.C / 64) * (4 * 9 * 64 + 32) * 4);
+    s.imsum = reinterpret_cast<float*>(reinterpret_cast<char*>(s.tot) + stem_rc_imsum_offset(p->x1.C));
     s.dw = x.W<float>(p->convs[p->stem_conv].wacc);
     s.dgamma = sb.dgamma; s.dbeta = sb.dbeta;
     s.npix = (int64_t)N * p->y0.H * p->y0.W;

@@ -209,7 +209,7 @@ hipError_t launch_slab_reduce(const ReduceTail& r, hipStream_t st);  // r on its
 // Batched 3x3 / stride-1 weight gradients (wgrad3x3_batch_kernel): the weight
 // gradients of several layers (wgrad_batch_ok) in ONE stream-K launch.  Layer l
 // has co_blocks x c_blocks units of 64 x 64 channels, each a K loop over `tiles`
-// 32 x 4 output-pixel tiles; the units' items (unit, tile) are numbered layer by
+// 128-pixel output tiles (32 x 4, or 16 x 8 for Q = 16: one geometry per launch); the units' items (unit, tile) are numbered layer by
 // layer, unit by unit, and block b of the grid runs items [b I / G, (b+1) I / G).
 // A unit inside one block is written to dW directly; a unit spread over blocks
 // b0..b1 leaves one partial per block in the slab (slot b * maxseg + the unit's
@@ -224,11 +224,13 @@ struct WgBatchLayer {
 struct WgBatchArgs {
   WgBatchLayer L[kWbMaxLayers];
   int nl, grid, maxseg, units, N;
+  int tw;                    // tile width of every layer: 32 (32 x 4 tiles) or 16 (16 x 8, Q = 16 layers)
   long long items;
   float* slab;               // grid * maxseg partials of 147,456 B
   unsigned long long* tim;   // phase stamps (debug build only)
 };
 bool wgrad_batch_ok(const ConvWgradArgs& a);
+int wgrad_batch_tw(const ConvWgradArgs& a);  // the batch tile width of a layer (0: not batchable)
 constexpr size_t kWbPartBytes = 8 * 18 * 64 * 16;  // one block's 64 x 64 x 9 fp32 partial (SLAB_HALO layout)
 // the grid of a batch (one block per CU) and the largest slab slot count it needs
 int wgrad_batch_grid();
@@ -303,6 +305,7 @@ hipError_t launch_stem_rc_fwd(const StemRcArgs& a, int mode, hipStream_t st);
 hipError_t launch_stem_rc_bwd(const StemRcArgs& a, int stage, hipStream_t st);
 size_t stem_rc_part_bytes(int N, int P, int Q, int Cout);  // a.part followed by a.l2
 size_t stem_rc_tot_bytes(int Cout);                        // a.tot followed by a.imsum
+size_t stem_rc_imsum_offset(int Cout);                     // bytes from a.tot to a.imsum
 size_t stem_rc_l2_offset(int N, int P, int Q, int Cout);   // bytes from a.part to a.l2
 
 // fused ConvTranspose2d(k2,s2, Cin->16) + Conv1x1(16->1): logits[2i+a,2j+b] =

@@ -937,7 +937,8 @@ size_t stem_rc_part_bytes(int N, int P, int Q, int Cout) {
   const int nblk = stem_rc_bwd_blocks(N, P, Q, Cout), groups = Cout / 64;
   return (size_t)nblk * groups * kRbPartF4 * 16 + (size_t)rc_nseg(nblk) * groups * kRbPartF4 * 32;
 }
-size_t stem_rc_tot_bytes(int Cout) { return (size_t)(Cout / 64) * kRbPartF4 * 32 + kRcImBlocks * sizeof(float); }
+size_t stem_rc_imsum_offset(int Cout) { return (size_t)(Cout / 64) * kRbPartF4 * 32; }
+size_t stem_rc_tot_bytes(int Cout) { return stem_rc_imsum_offset(Cout) + kRcImBlocks * sizeof(float); }
 size_t stem_rc_l2_offset(int N, int P, int Q, int Cout) {
   return (size_t)stem_rc_bwd_blocks(N, P, Q, Cout) * (Cout / 64) * kRbPartF4 * 16;
 }

@@ -31,21 +31,33 @@ def test_bn_prologue_bit_identical(pkg, cuda, monkeypatch):
     x, y = torch.from_numpy(xs).cuda(), torch.from_numpy(ms).cuda()
     monkeypatch.delenv("UNET_NO_BN_XFORM", raising=False)
     fused = _run(pkg, sd, x, y)
+    fused2 = _run(pkg, sd, x, y)
     monkeypatch.setenv("UNET_NO_BN_XFORM", "1")  # read when the native plan is created
     plain = _run(pkg, sd, x, y)
+    plain2 = _run(pkg, sd, x, y)
     assert torch.equal(fused[0], plain[0])
     for k in ["enc1.0.h", "enc1.1.h", "enc1.2.h", "dec2.h", "dec1.h"]:
         assert torch.equal(fused[1][k], plain[1][k]), k
     for k, v in plain[3].items():
         assert torch.equal(fused[3][k], v), k
-    # the backward reads the same tensors; its BN-backward sums are fp64 atomic
-    # adds of per-block fp32 partials whose accumulation order follows the
-    # launch timing, which the prologue changes.  A last-bit change of one
-    # BN coefficient (measured: 4 of 131072 elements of enc1.2's dY2, 1.9e-9)
-    # flips bf16 roundings of every dZ upstream, so the gradients agree to
-    # bf16 resolution (measured <= 2.5e-3 relative L2, the stem weight), not
-    # bit for bit
+    # each path on its own is bit-reproducible (fixed-order weight-gradient
+    # reductions; BN / loss sums are fp64 accumulations of fp32 partials)
+    for a, b in ((fused, fused2), (plain, plain2)):
+        diff = [k for k, v in a[2].items() if not torch.equal(v, b[2][k])]
+        assert not diff, diff
+    # across the two paths the backward reads bit-identical tensors, so every
+    # BN-backward sum is the same set of fp32 block partials; they enter fp64
+    # replica accumulators by atomic adds whose arrival order differs between
+    # the two kernel sequences.  Where such an fp64 sum is not exact (partials
+    # more than 2^29 apart in magnitude) its last bit follows that order, and a
+    # one-ulp change of an fp32 BN coefficient (measured: 4 of 131072 elements of
+    # enc1.2's dY2, 1.9e-9) flips bf16 roundings of the dZ upstream, so the two
+    # paths agree to bf16 resolution (measured <= 2.5e-3 relative L2, the stem
+    # weight), not bit for bit
+    worst = 0.0
     for k, v in plain[2].items():
         g = fused[2][k]
         rel = ((g.double() - v.double()).norm() / v.double().norm().clamp_min(1e-30)).item()
+        worst = max(worst, rel)
         assert rel <= 1e-2, (k, rel)
+    print("fused vs plain gradients: worst relative L2", worst)

@@ -221,16 +221,18 @@ def test_base_512_step_properties(pkg, cuda):
         assert torch.isfinite(p.grad).all(), k
 
 
-@pytest.mark.parametrize("attention", [False, True], ids=["plain", "attention"])
-def test_backward_is_bit_reproducible(pkg, cuda, attention):
+@pytest.mark.parametrize("attention,batch,size", [(False, 4, 128), (True, 4, 128), (False, 2, 512)],
+                         ids=["plain", "attention", "plain_2x512"])
+def test_backward_is_bit_reproducible(pkg, cuda, attention, batch, size):
     """Two backward passes of the same step give bit-identical gradients: every
     weight gradient is a split-K partial slab summed in a fixed split order
     (no fp32 atomics); BN / loss / attention pooling sums are fp64
     accumulations of fp32 partials, exact to far below the fp32 result they
-    round to."""
+    round to.  2x512: the production stem (recompute) and the 16-wide batched
+    weight gradients of enc4 (16 x 16 maps) run."""
     torch.manual_seed(0)
     m = pkg.UNetWithBackbone(pretrained=False, use_attention=attention).cuda().train()
-    xs, ms = pkg.synthetic_cells(4, 128, 128, seed=12)
+    xs, ms = pkg.synthetic_cells(batch, size, size, seed=12)
     x, y = torch.from_numpy(xs).cuda(), torch.from_numpy(ms).cuda()
     crit = pkg.get_loss_function({"loss_fn": "bce"})
     sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
