@@ -1,0 +1,508 @@
+// Full-line halo convolution: the 3x3 / stride-1 / pad-1 forward conv and its
+// data gradient for C % 128 == 0 and Cout % 64 == 0 (SURVEY.md §8(a) rows a3 /
+// a6: enc2-4 BasicBlocks, decoder4 / decoder3; reference
+// advanced_models.py:84-87,197-205).
+//
+// Why a separate kernel: the per-CU L2 -> LDS rate of LDS-DMA is set by cache
+// LINES, not bytes (scripts/micro/dma_rate.hip, profiles/r05/s1/dma_rate.txt:
+// 64-B pieces of 128-B lines 32 B/clk/CU, whole lines 54 B/clk/CU).  The
+// halo-streamed kernel (conv_halo.hip) stages 32 channels = 64 B per pixel and
+// per weight row, so its stages ran at the DMA rate of half lines (~2.9k cycles
+// per stage for ~2.0k cycles of MFMA, profiles/r04/s1 conv_timing*), and its
+// epilogue read its operands in 32-B pieces.  Here every global access moves
+// whole lines:
+//  * halo: 64-channel super-chunks, one 128-B LDS row per halo pixel holding
+//    both 32-channel panels (fl_off swizzle, conv_halo.hip);
+//  * weights: a chunk-major pack [C/32][9][Cout][32] (PK_CONV_*_CH, pack_kernel):
+//    one 32-channel sub-stage of a 64-output-channel block is 9 contiguous
+//    4 KB runs;
+//  * epilogue: the accumulators are transposed through LDS so that a lane owns
+//    (pixel, 8 channels): operand loads and stores are 16 B per lane, 8 lanes per
+//    128-B line.
+// One 512-thread block per CU (158 KB LDS): a 16 x 16 pixel x 64 channel output
+// tile, 8 waves x (2 rows x 4 channel fragments); per 32-channel sub-stage
+// 72 v_mfma_f32_16x16x32_bf16 per wave (2304 MFMA cycles per SIMD) against
+// ~58 KB of whole-line DMA (~1.1k cycles at 54 B/clk/CU).  The grid is
+// persistent (one block per CU): the next tile's first super-chunk and weights
+// stage under this tile's last sub-stage and epilogue; BN sums are kept per
+// thread across tiles and committed once.
+//
+// LDS: H0 | W0 | W1 | H1 | constants.  Sub-stage t of a tile reads panel t & 1
+// of halo H[(t >> 1) & 1] and weights W[t & 1]; C / 64 is even, so every tile
+// starts on H0 / W0 and ends on W1 / H1, which the epilogue then uses as its
+// 64 KB transpose buffer while the next tile's first stage lands in H0 / W0.
+#include <cstdio>
+#include <cstdlib>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace unet {
+
+void conv_kernel_tag(const char* tag);  // conv_kernels.hip: per-launch profiler column
+
+namespace {
+
+// 4 compute waves (MFMA + epilogue) and 4 loader waves (all LDS-DMA): a wave
+// that issues LDS-DMA pays ~100-200 cycles per instruction beside its MFMAs
+// (MI355X_MICROARCH.md, LDS-DMA piece issue cost; the all-waves-issue form of
+// this kernel measured 3.7-5.3k cycles per sub-stage against 2.3k of MFMA,
+// profiles/r05/s1), and a compute wave that issues none keeps every load it
+// makes visible to the compiler's waitcnt pass.  One compute and one loader
+// wave per SIMD.
+constexpr int kNC = 4, kNL = 4, kNW = kNC + kNL, kCOT = 64, kRW = 4, kFN = 4, kTH = 16;
+constexpr int kHW = 18;                       // halo width
+constexpr int kHPix = (kTH + 2) * kHW;        // 324 halo pixels
+constexpr int kHIns = (kHPix + 7) / 8;        // 41 DMA instructions of 8 x 128 B
+constexpr int kHBytes = kHIns * 1024;         // 41,984
+constexpr int kWIns = 9 * kCOT / 16;          // 36 DMA instructions of 16 x 64 B
+constexpr int kWBytes = kWIns * 1024;         // 36,864
+constexpr int kOffH0 = 0, kOffW0 = kHBytes, kOffW1 = kOffW0 + kWBytes, kOffH1 = kOffW1 + kWBytes;
+constexpr int kOffCst = kOffH1 + kHBytes;     // 157,696
+constexpr int kNCst = 5;                      // bias|shift', scale|mean, invstd, mean2, invstd2
+constexpr int kLds = kOffCst + kNCst * kCOT * 4;
+static_assert(kLds <= 163840, "LDS");
+static_assert(256 * 256 <= kWBytes + kHBytes, "transpose buffer fits W1 | H1");
+static_assert(kTH == kNC * kRW, "rows");
+constexpr int kItems = 4;  // epilogue items (pixel, 8 channels): 2 x 4 per loader thread
+constexpr int kWPer = kWIns / kNL;                         // 9 weight DMA per loader wave
+constexpr int kHPer = (kHIns + kNL - 1) / kNL;             // <= 11 halo DMA per loader wave
+static_assert(kWIns % kNL == 0, "weight DMA per loader");
+
+__device__ __forceinline__ int fl_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 6)) << 4); }
+__device__ __forceinline__ int ws_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 1) & 2)) << 4); }
+// transpose buffer [256 px][64 f32]: 16-B chunk c of pixel px at c ^ (px & 15)
+// (conflict-free for the accumulator writes and the (pixel, 8-channel) reads)
+__device__ __forceinline__ int tp_off(int px, int c16) { return px * 256 + ((c16 ^ (px & 15)) << 4); }
+
+__device__ __forceinline__ void wait_vm_h(int n) {  // loader: all but its n halo DMA of the sub-stage
+  if (n == 11) wait_vmcnt<11>();
+  else wait_vmcnt<10>();
+}
+__device__ __forceinline__ void barrier_lds() {  // this wave's LDS reads/writes done, then the barrier
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+}  // namespace
+
+// One epilogue item: 8 channels q8 .. q8 + 7 of pixel slot px (transpose
+// buffer T) / global pixel pix -- bias or eval fold, addend, ReLU mask of the
+// fused BN backward, bf16 store, BN sums (register accumulators s0 / s1 / s2)
+template <bool FLIP, bool TWO>
+__device__ __forceinline__ void fl_item(const ConvFwdArgs& a, const char* T, const float* cst, int q8, int px,
+                                        int pix, int cob, bool fold, bool want_add, bool fbwd, bool stats,
+                                        const uint4& uadd, const uint4& uact, const uint4& uy, const uint4& uy2,
+                                        float (&s0)[8], float (&s1)[8], float (&s2)[8]) {
+  const f32x4 lo = *reinterpret_cast<const f32x4*>(T + tp_off(px, 2 * (q8 >> 3)));
+  const f32x4 hi = *reinterpret_cast<const f32x4*>(T + tp_off(px, 2 * (q8 >> 3) + 1));
+  float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  const f32x4 b0 = *reinterpret_cast<const f32x4*>(cst + q8), b1 = *reinterpret_cast<const f32x4*>(cst + q8 + 4);
+  const float kb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+  if (fold) {
+    const f32x4 m0 = *reinterpret_cast<const f32x4*>(cst + kCOT + q8);
+    const f32x4 m1 = *reinterpret_cast<const f32x4*>(cst + kCOT + q8 + 4);
+    const float km[8] = {m0[0], m0[1], m0[2], m0[3], m1[0], m1[1], m1[2], m1[3]};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = v[e] * km[e] + kb[e];
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += kb[e];
+  }
+  if (want_add) {
+    float ad[8];
+    unpack8(uadd, ad);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += ad[e];
+  }
+  if (!FLIP && a.fold_relu) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+  }
+  if (fbwd) {
+    float m[8];
+    unpack8(uact, m);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (!(m[e] > 0.f)) v[e] = 0.f;
+  }
+  const uint4 ob = pack8(v);
+  if (UNET_ABL != 4) *reinterpret_cast<uint4*>(a.y + (size_t)pix * a.ldy + cob * kCOT + q8) = ob;
+  if (fbwd) {  // sums of the stored bf16 dZ, as bn_bwd_reduce_kernel would read them
+    float dz[8], yv[8];
+    unpack8(ob, dz);
+    unpack8(uy, yv);
+    const f32x4 mu0 = *reinterpret_cast<const f32x4*>(cst + kCOT + q8);
+    const f32x4 mu1 = *reinterpret_cast<const f32x4*>(cst + kCOT + q8 + 4);
+    const f32x4 is0 = *reinterpret_cast<const f32x4*>(cst + 2 * kCOT + q8);
+    const f32x4 is1 = *reinterpret_cast<const f32x4*>(cst + 2 * kCOT + q8 + 4);
+    const float mu[8] = {mu0[0], mu0[1], mu0[2], mu0[3], mu1[0], mu1[1], mu1[2], mu1[3]};
+    const float is[8] = {is0[0], is0[1], is0[2], is0[3], is1[0], is1[1], is1[2], is1[3]};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s0[e] += dz[e];
+      s1[e] += dz[e] * (yv[e] - mu[e]) * is[e];
+    }
+    if constexpr (TWO) {
+      float y2[8];
+      unpack8(uy2, y2);
+      const f32x4 n0 = *reinterpret_cast<const f32x4*>(cst + 3 * kCOT + q8);
+      const f32x4 n1 = *reinterpret_cast<const f32x4*>(cst + 3 * kCOT + q8 + 4);
+      const f32x4 j0 = *reinterpret_cast<const f32x4*>(cst + 4 * kCOT + q8);
+      const f32x4 j1 = *reinterpret_cast<const f32x4*>(cst + 4 * kCOT + q8 + 4);
+      const float mu2[8] = {n0[0], n0[1], n0[2], n0[3], n1[0], n1[1], n1[2], n1[3]};
+      const float is2[8] = {j0[0], j0[1], j0[2], j0[3], j1[0], j1[1], j1[2], j1[3]};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s2[e] += dz[e] * (y2[e] - mu2[e]) * is2[e];
+    }
+  } else if (stats) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s0[e] += v[e]; s1[e] += v[e] * v[e]; }
+  }
+}
+
+// FLIP: data gradient (dgrad pack, taps mirrored); TWO: two-BN fused backward
+// epilogue (downsample blocks); grid = persistent slots, work item = spatial
+// tile * ncb + output-channel block.
+//
+// Roles and barriers.  Per item both roles pass B_0 .. B_{NSUB-1} (sub-stage s
+// may start) and F (every compute wave is done reading W1 / H1); after the
+// last item one more barrier Z.  Compute waves: MFMAs of sub-stage s after
+// B_s; after F they write their accumulators to the transpose buffer T (W1 |
+// H1) and go on to the next item's B_0.  Loader waves: before B_s they wait
+// for sub-stage s's DMA and after it issue the next one; they own the whole
+// epilogue: its operands are fetched at B_{NSUB-1} (before the next item's
+// DMA, so the in-order waits stay exact), and the epilogue of item i runs right
+// after the next item's B_0 -- beside that item's first sub-stage, which reads
+// only W0 / H0 -- or after Z; only then do they refill W1 / H1 (= T).
+template <bool FLIP, bool TWO>
+__global__ void __launch_bounds__(kNW * 64) conv3x3_fl_kernel(ConvFwdArgs a, int ncb, int nitems) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* cst = reinterpret_cast<float*>(smem + kOffCst);
+  TSTAMP_RT(a.tim, 30);
+  TSTAMP(a.tim, 0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int slot = xcd_remap(blockIdx.x, gridDim.x);
+  int item = slot;
+  if (item >= nitems) return;
+  const int tq = a.Q >> 4, tp = a.P / kTH;
+  const int NSUB = a.C >> 5;  // 32-channel sub-stages per item (even)
+  const bool fbwd = FLIP && a.bb.sums != nullptr;
+  const bool stats = a.stats != nullptr || fbwd;
+  const bool fold = !FLIP && a.fold_on;
+  const int cob = item % ncb;  // fixed per block: gridDim % ncb == 0 (launcher)
+
+  if (wave < kNC) {
+    // ================= compute waves: MFMAs, accumulators to T =================
+    const int aoff = ws_off(lane & 15, lane >> 4);
+    int boff[kRW + 2][3];
+#pragma unroll
+    for (int h = 0; h < kRW + 2; ++h)
+#pragma unroll
+      for (int d = 0; d < 3; ++d) boff[h][d] = fl_off((wave * kRW + h) * kHW + d + (lane & 15), lane >> 4);
+    TSTAMP(a.tim, 1);
+    int stg = 0;
+    for (;;) {
+      f32x4 acc[kRW][kFN];
+#pragma unroll
+      for (int j = 0; j < kRW; ++j)
+#pragma unroll
+        for (int i = 0; i < kFN; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < NSUB; ++s, ++stg) {
+        barrier_lds();  // B_s: the loaders have waited for sub-stage s
+        if (stg < 16) TSTAMP(a.tim, 2 + stg);
+        const char* W = smem + ((s & 1) ? kOffW1 : kOffW0);
+        const char* H = smem + (((s >> 1) & 1) ? kOffH1 : kOffH0);
+        const int pb = (s & 1) << 6;  // panel: byte offset ^ 64
+        if (UNET_ABL == 1) continue;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            bf16x8 A[kFN];
+#pragma unroll
+            for (int i = 0; i < kFN; ++i)
+              A[i] = *reinterpret_cast<const bf16x8*>(W + ((r * 3 + c) * kCOT + i * 16) * 64 + aoff);
+            const int dr = FLIP ? 2 - r : r, dc = FLIP ? 2 - c : c;
+#pragma unroll
+            for (int j = 0; j < kRW; ++j) {
+              const bf16x8 B = *reinterpret_cast<const bf16x8*>(H + (boff[j + dr][dc] ^ pb));
+#pragma unroll
+              for (int i = 0; i < kFN; ++i)
+                acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B, acc[j][i], 0, 0, 0);
+            }
+          }
+      }
+      TSTAMP(a.tim, 20);
+      barrier_lds();  // F: every compute wave is done reading W1 / H1
+      char* T = smem + kOffW1;
+#pragma unroll
+      for (int j = 0; j < kRW; ++j)
+#pragma unroll
+        for (int i = 0; i < kFN; ++i) {
+          const int px = (wave * kRW + j) * 16 + (lane & 15);
+          *reinterpret_cast<f32x4*>(T + tp_off(px, i * 4 + (lane >> 4))) = acc[j][i];
+        }
+      item += gridDim.x;
+      if (item >= nitems) break;
+    }
+    barrier_lds();  // Z: T holds the last item
+    if (stats) {  // the loaders' reduction barriers
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_s_barrier();
+      const unsigned* tk = fbwd ? a.bb.ticket : a.bn.ticket;
+      if (tk) {
+        int* flag = reinterpret_cast<int*>(smem + kOffH0 + 32 * kCOT * 3 * sizeof(float));
+        if (last_block_arrive(const_cast<unsigned*>(tk), gridDim.x, flag, false)) {
+          if (fbwd) bn_bwd_finalize(a.bb);
+          else bn_finalize(a.bn);
+        }
+      }
+    }
+    return;
+  }
+
+  // ================= loader waves: all LDS-DMA (inline asm, glds16_asm: hipcc's
+  // waitcnt pass would otherwise drain the halo still in flight) + epilogue =====
+  const int lw = wave - kNC, lt = tid - kNC * 64;
+  const int nh = (kHIns - lw + kNL - 1) / kNL;  // 11 or 10
+  const i32x4 xr = make_rsrc_sgpr(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
+  const i32x4 wr = make_rsrc_sgpr(a.wch, (unsigned)((size_t)a.C * 9 * a.Cout * 2));
+  unsigned woff[kWPer], hoff[kHPer];
+#pragma unroll
+  for (int k = 0; k < kWPer; ++k) {
+    const int ins = lw + k * kNL;
+    const int tap = ins >> 2, co = (ins & 3) * 16 + (lane >> 2);
+    const int lch = (lane & 3) ^ ((co >> 1) & 2);
+    woff[k] = (unsigned)(((tap * a.Cout + cob * kCOT + co) * 32 + lch * 8) * 2);
+  }
+  auto set_hoff = [&](int it) {
+    const int t = it / ncb;
+    const int n = t / (tp * tq), rem = t - n * (tp * tq);
+    const int oh0 = (rem / tq) * kTH, ow0 = (rem % tq) << 4;
+#pragma unroll
+    for (int k = 0; k < kHPer; ++k) {
+      const int hp = (lw + k * kNL) * 8 + (lane >> 3);
+      const int hr = hp / kHW, hc = hp - hr * kHW;
+      const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
+      const int q = (lane & 7) ^ (hp & 6);
+      hoff[k] = kOOB;
+      if (hp < kHPix && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+        hoff[k] = (unsigned)((((n * a.H + ih) * a.W + iw) * a.ldx + q * 8) * 2);
+    }
+  };
+  auto issue_w = [&](int t, int b) {  // sub-stage t's weights (32 channels, 9 taps) into W[b]
+    char* dst = smem + (b ? kOffW1 : kOffW0);
+    const unsigned so = (unsigned)t * 9u * (unsigned)a.Cout * 64u;
+#pragma unroll
+    for (int k = 0; k < kWPer; ++k) glds16_asm(wr, dst + (lw + k * kNL) * 1024, woff[k], so);
+  };
+  auto issue_h = [&](int sc, int b) {  // super-chunk sc's halo (64 channels) into H[b]
+    char* dst = smem + (b ? kOffH1 : kOffH0);
+    const unsigned so = (unsigned)sc * 128u;
+#pragma unroll
+    for (int k = 0; k < kHPer; ++k)
+      if (k < nh) glds16_asm(xr, dst + (lw + k * kNL) * 1024, hoff[k], so);
+  };
+  set_hoff(item);
+  issue_w(0, 0);
+  issue_h(0, 0);
+  if (lt < kCOT) {  // per-channel epilogue constants of the block's output channels
+    const int c = lt, co = cob * kCOT + c;
+    float b = a.bias ? a.bias[co] : 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f, c4 = 0.f;
+    if (fold) {
+      float sc, sh, m, is, var;
+      bn_scale_shift(a.fold, co, sc, sh, m, is, var);
+      b = b * sc + sh;
+      c1 = sc;
+    } else if (fbwd) {
+      c1 = a.bb.mean[co];
+      c2 = a.bb.invstd[co];
+      if (TWO) { c3 = a.bb.mean2[co]; c4 = a.bb.invstd2[co]; }
+    }
+    cst[c] = b; cst[kCOT + c] = c1; cst[2 * kCOT + c] = c2; cst[3 * kCOT + c] = c3; cst[4 * kCOT + c] = c4;
+  }
+  // epilogue: loader wave lw owns the pixels px with (px >> 2) & 3 == lw -- the
+  // T rows in the 1-KB stripes that its own DMA refills (stripe = px >> 2,
+  // DMA instructions lw + 4 k of W1 and H1, T = W1 | H1), so no other wave's
+  // DMA can overwrite a row it has not read yet; lane l owns channels
+  // 8 (l & 7) .. + 7 of pixel slot j = (l >> 3) + 8 k (k < 8), 4 consecutive
+  // pixels per 512 B
+  const int q8 = (lane & 7) * 8;
+  auto px_of = [&](int k) {
+    const int j = (lane >> 3) + 8 * k;
+    return 16 * (j >> 2) + 4 * lw + (j & 3);
+  };
+  const bool want_add = a.add != nullptr;
+  float s0[8], s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s0[e] = s1[e] = s2[e] = 0.f;
+  constexpr int NI = 2 * kItems;  // 8 items per loader thread
+  int pix[NI];                    // the pending epilogue's pixels (N * P * Q < 2^31: launcher)
+  uint4 opa[NI], opm[NI], opy[NI], opy2[TWO ? NI : 1];
+  // the epilogue of the item whose accumulators are in T (its operands fetched)
+  auto epilogue = [&]() {
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+      fl_item<FLIP, TWO>(a, smem + kOffW1, cst, q8, px_of(k), pix[k], cob, fold, want_add, fbwd, stats,
+                         opa[k], opm[k], opy[k], opy2[TWO ? k : 0], s0, s1, s2);
+      asm volatile("" ::: "memory");  // one item at a time: bounded registers
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's T rows are read before its DMA refills them
+  };
+  bool pending = false;  // an epilogue waits for the next B_0 / Z
+  for (;;) {
+    const int next = item + gridDim.x;
+    // s = 0 (peeled): everything landed; then the previous item's epilogue,
+    // beside this item's first sub-stage; then the refill of W1 / H1 (= T)
+    wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();  // B_0
+    if (pending) epilogue();
+    if (UNET_ABL != 2) {
+      issue_w(1, 1);
+      if (2 < NSUB) issue_h(1, 1);
+    }
+    // s = 1 .. NSUB - 2: at odd s all but the next super-chunk's halo (issued
+    // after this sub-stage's weights) has landed; at even s everything
+    for (int s = 1; s < NSUB - 1; ++s) {
+      if (s & 1) wait_vm_h(nh);
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();  // B_s: sub-stage s - 1 is no longer read
+      if (UNET_ABL != 2) {
+        issue_w(s + 1, (s + 1) & 1);
+        if (!(s & 1) && s + 2 < NSUB) issue_h((s >> 1) + 1, ((s >> 1) + 1) & 1);
+      }
+    }
+    // s = NSUB - 1 (peeled): everything landed; this item's epilogue operands
+    // (whole lines), then the next item's first stage (H0 / W0 are free)
+    wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();  // B_{NSUB-1}
+    {
+      const int t = item / ncb;
+      const int n = t / (tp * tq), rem = t - n * (tp * tq);
+      const int oh0 = (rem / tq) * kTH, ow0 = (rem % tq) << 4;
+#pragma unroll
+      for (int k = 0; k < NI; ++k) {
+        const int px = px_of(k);
+        pix[k] = (n * a.P + oh0 + (px >> 4)) * a.Q + ow0 + (px & 15);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+      const size_t pp = (size_t)pix[k];
+      const int co = cob * kCOT + q8;
+      opa[k] = want_add ? *reinterpret_cast<const uint4*>(a.add + pp * a.ldadd + co) : make_uint4(0, 0, 0, 0);
+      opm[k] = fbwd ? *reinterpret_cast<const uint4*>(a.bb.act + pp * a.bb.ldact + co) : make_uint4(0, 0, 0, 0);
+      opy[k] = fbwd ? *reinterpret_cast<const uint4*>(a.bb.y + pp * a.bb.ldy + co) : make_uint4(0, 0, 0, 0);
+      if constexpr (TWO)
+        opy2[k] = fbwd ? *reinterpret_cast<const uint4*>(a.bb.y2 + pp * a.bb.ldy2 + co) : make_uint4(0, 0, 0, 0);
+    }
+    if (next < nitems) {
+      set_hoff(next);
+      issue_w(0, 0);
+      issue_h(0, 0);
+    }
+    __builtin_amdgcn_s_barrier();  // F
+    pending = true;
+    item = next;
+    if (item >= nitems) break;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // Z: T holds the last item
+  epilogue();
+  TSTAMP(a.tim, 21);
+  if (!stats) return;
+  // ---- BN sums: [32 pixel slots][64 channels][3] in H0 (no DMA in flight any
+  // more), summed over the slots in a fixed order (4 independent partial sums),
+  // fp64 atomics into replica blockIdx % kStatRep ----
+  float* red = reinterpret_cast<float*>(smem + kOffH0);
+  {
+    const int sl = lt >> 3;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(sl * kCOT + q8 + e) * 3 + 0] = s0[e];
+      red[(sl * kCOT + q8 + e) * 3 + 1] = s1[e];
+      red[(sl * kCOT + q8 + e) * 3 + 2] = s2[e];
+    }
+  }
+  barrier_lds();  // R1
+  if (lt < (TWO ? 3 : 2) * kCOT) {
+    const int c = lt % kCOT, which = lt / kCOT;
+    float p[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int sl = 0; sl < 32; ++sl) p[sl & 3] += red[(sl * kCOT + c) * 3 + which];
+    const float tsum = (p[0] + p[1]) + (p[2] + p[3]);
+    const int co = cob * kCOT + c;
+    const size_t rep = (size_t)(blockIdx.x % kStatRep) * 2 * a.Cout;
+    if (which == 2) atomicAdd(a.bb.sums2 + rep + a.Cout + co, (double)tsum);
+    else atomicAdd((fbwd ? a.bb.sums : a.stats) + rep + which * a.Cout + co, (double)tsum);
+  }
+  __builtin_amdgcn_s_barrier();  // R2
+  const unsigned* tk = fbwd ? a.bb.ticket : a.bn.ticket;
+  if (tk) {
+    int* flag = reinterpret_cast<int*>(smem + kOffH0 + 32 * kCOT * 3 * sizeof(float));
+    if (last_block_arrive(const_cast<unsigned*>(tk), gridDim.x, flag, lt < 3 * kCOT)) {
+      if (fbwd) bn_bwd_finalize(a.bb);
+      else bn_finalize(a.bn);
+    }
+  }
+  TSTAMP(a.tim, 22);
+  TSTAMP_RT(a.tim, 31);
+}
+
+static int g_cus = 0;
+static int cu_count() {
+  if (!g_cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || g_cus <= 0)
+      g_cus = 256;
+  }
+  return g_cus;
+}
+
+// shapes the kernel covers AND fills: at least one 16 x 16 x 64 work item per
+// CU (enc4 at 512^2 has 128: it stays on the 32-channel halo-streamed kernel)
+bool conv3x3_fl_shape(int N, int C, int Cout, int P, int Q) {
+  static const bool off = std::getenv("UNET_NO_FL") != nullptr;  // A/B: the halo-streamed kernel
+  if (off || C % 128 || Cout % kCOT || P % kTH || Q % 16) return false;
+  return (long long)N * (P / kTH) * (Q / 16) * (Cout / kCOT) >= cu_count();
+}
+
+// a.wch: the chunk-major weight pack (PK_CONV_FWD_CH / PK_CONV_DGRAD_CH)
+hipError_t launch_conv3x3_fl(const ConvFwdArgs& a, int mode, hipStream_t st) {
+  const bool flip = mode == 1;
+  if (!a.wch || a.R != 3 || a.S != 3 || a.stride != 1 || a.pad != 1 || a.x2 || a.ysplit || a.xform)
+    return hipErrorInvalidValue;
+  if (a.H != a.P || a.W != a.Q || !conv3x3_fl_shape(a.N, a.C, a.Cout, a.P, a.Q)) return hipErrorInvalidValue;
+  if (a.ldx % 8 || a.ldy % 8 || (a.add && a.ldadd % 8)) return hipErrorInvalidValue;
+  if (flip && (a.fold_on || a.stats || (a.bb.sums && (a.bb.ldact % 8 || a.bb.ldy % 8 ||
+                                                     (a.bb.y2 && a.bb.ldy2 % 8)))))
+    return hipErrorInvalidValue;
+  if (!flip && a.bb.sums) return hipErrorInvalidValue;
+  if ((size_t)a.N * a.H * a.W * a.ldx * 2 >= 0x80000000ull || (size_t)a.C * 9 * a.Cout * 2 >= 0x80000000ull ||
+      (size_t)a.N * a.P * a.Q >= 0x80000000ull)
+    return hipErrorInvalidValue;
+  const int ncb = a.Cout / kCOT;
+  const int nitems = a.N * (a.P / kTH) * (a.Q / 16) * ncb;
+  // persistent grid: one block per CU, a multiple of ncb so that every block
+  // keeps one output-channel block
+  int grid = cu_count() / ncb * ncb;
+  if (grid < ncb) grid = ncb;
+  if (grid > nitems) grid = nitems;
+  const bool two = flip && a.bb.sums && a.bb.y2;
+  char tag[96];
+  std::snprintf(tag, sizeof(tag), "conv3x3_fl_kernel<%s, %s>", flip ? "true" : "false", two ? "true" : "false");
+  conv_kernel_tag(tag);
+  if (!flip)
+    hipLaunchKernelGGL((conv3x3_fl_kernel<false, false>), dim3(grid), dim3(kNW * 64), kLds, st, a, ncb, nitems);
+  else if (two)
+    hipLaunchKernelGGL((conv3x3_fl_kernel<true, true>), dim3(grid), dim3(kNW * 64), kLds, st, a, ncb, nitems);
+  else
+    hipLaunchKernelGGL((conv3x3_fl_kernel<true, false>), dim3(grid), dim3(kNW * 64), kLds, st, a, ncb, nitems);
+  return hipGetLastError();
+}
+
+}  // namespace unet

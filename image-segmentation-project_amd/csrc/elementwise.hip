@@ -1042,7 +1042,10 @@ __global__ void __launch_bounds__(256) pack_kernel(PackTable t) {
   }
   const bool convt = e.kind == PK_CONVT_FWD || e.kind == PK_CONVT_DGRAD;
   const int A = convt ? e.Ci : e.Co, B = convt ? e.Co : e.Ci, T = e.R * e.S;
-  const bool full = e.kind == PK_CONV_DGRAD || e.kind == PK_CONVT_FWD;
+  const bool full = e.kind == PK_CONV_DGRAD || e.kind == PK_CONVT_FWD || e.kind == PK_CONV_DGRAD_CH;
+  // chunk-major 3x3 packs (conv3x3_fl_kernel): fwd dst[b/32][t][a][b%32],
+  // dgrad dst[a/32][t][b][a%32]
+  const bool chunk = e.kind == PK_CONV_FWD_CH || e.kind == PK_CONV_DGRAD_CH;
   // every load of a pass is issued before the first LDS store (no per-load
   // round trip to L2)
   if (!full) {  // one a-row [B][T] -> [T][B] per block iteration, in b-chunks of <= 512
@@ -1064,9 +1067,17 @@ __global__ void __launch_bounds__(256) pack_kernel(PackTable t) {
           if (i < m) lds[i] = v[k];
         }
         __syncthreads();
-        bf16_t* dst = e.dst + (size_t)a * n + b0;
-        for (int tt = 0; tt < T; ++tt)
-          for (int b = threadIdx.x; b < nb; b += blockDim.x) dst[tt * B + b] = f2bf(lds[b * T + tt]);
+        if (chunk) {
+          for (int tt = 0; tt < T; ++tt)
+            for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+              const int bg = b0 + b;
+              e.dst[((size_t)((bg >> 5) * T + tt) * A + a) * 32 + (bg & 31)] = f2bf(lds[b * T + tt]);
+            }
+        } else {
+          bf16_t* dst = e.dst + (size_t)a * n + b0;
+          for (int tt = 0; tt < T; ++tt)
+            for (int b = threadIdx.x; b < nb; b += blockDim.x) dst[tt * B + b] = f2bf(lds[b * T + tt]);
+        }
         __syncthreads();
       }
     }
@@ -1100,8 +1111,17 @@ __global__ void __launch_bounds__(256) pack_kernel(PackTable t) {
       }
     __syncthreads();
     if (a0 + lane < A) {
-      bf16_t* dst = e.dst + (size_t)b0 * T * A + a0 + lane;
-      for (int j = sub; j < run; j += 4) dst[(size_t)j * A] = f2bf(lds[j * LD + lane]);
+      if (chunk) {
+        const int ag = a0 + lane;
+        bf16_t* dst = e.dst + (size_t)(ag >> 5) * T * B * 32 + (ag & 31);
+        for (int j = sub; j < run; j += 4) {
+          const int bl = j / T, t = j - bl * T;
+          dst[((size_t)t * B + b0 + bl) * 32] = f2bf(lds[j * LD + lane]);
+        }
+      } else {
+        bf16_t* dst = e.dst + (size_t)b0 * T * A + a0 + lane;
+        for (int j = sub; j < run; j += 4) dst[(size_t)j * A] = f2bf(lds[j * LD + lane]);
+      }
     }
     __syncthreads();
   }

@@ -66,6 +66,9 @@ struct Conv {
   size_t pk_fwd = 0, pk_dgrad = 0, wacc = 0;  // ws offsets
   size_t bias_acc = 0;                        // fp64 [kStatRep][Co] (convT bias grads)
   bool f8 = false;                            // forward in fp8 e4m3 (cfg.fp8, C >= 128)
+  // forward / data gradient on conv3x3_fl_kernel: pk_fwd / pk_dgrad hold the
+  // chunk-major packs (PK_CONV_FWD_CH / PK_CONV_DGRAD_CH) instead
+  bool fl_fwd = false, fl_dgrad = false;
   size_t f8w = 0;                             // ws offset: e4m3 [Co][R*S*Ci]
   int f8st = -1;                              // F8State index of the weight
 };
@@ -649,6 +652,25 @@ static int build_plan(unet_plan* p) {
     p->f8_done.assign(p->f8acts.size(), 0);
   }
 
+  // 3x3 / s1 convs on the full-line halo kernel (conv_fl.hip): their packs
+  // are chunk-major, every launch of them goes to that kernel
+  {
+    auto fl_mark = [&](int ci, const Act& in) {
+      Conv& cv = p->convs[ci];
+      if (cv.kind != L_CONV || cv.R != 3 || cv.S != 3 || cv.stride != 1 || cv.pad != 1) return;
+      cv.fl_fwd = !cv.f8 && conv3x3_fl_shape(N, cv.Ci, cv.Co, in.H, in.W);
+      cv.fl_dgrad = conv3x3_fl_shape(N, cv.Co, cv.Ci, in.H, in.W);
+    };
+    for (auto& b : p->blocks) {
+      fl_mark(b.conv1, b.in);
+      fl_mark(b.conv2, b.h);
+    }
+    for (auto& d : p->decs) {
+      fl_mark(d.conv1, d.cat);
+      fl_mark(d.conv2, d.h);
+    }
+  }
+
   // backward gradient tensors
   for (int l = 3; l >= 0; --l) {
     Dec& d = p->decs[l];
@@ -916,6 +938,12 @@ int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for
     return 0;
   }
   a.tim = tim_slot(x.p, "fwd " + pname(x, cv.w));
+  if (cv.fl_fwd) {  // chunk-major pack: only conv3x3_fl_kernel reads it
+    a.wch = a.w;
+    a.w = nullptr;
+    CK(launch_conv3x3_fl(a, 0, x.st));
+    return 0;
+  }
   CK(launch_conv_fwd(a, cv.kind == L_CONVT ? MODE_SHUF : MODE_FWD, x.st));
   return 0;
 }
@@ -966,6 +994,12 @@ int conv_dgrad(const Ctx& x, int ci, const Act& dy, const Act& dx, const Act* ad
   a.C = cv.Co; a.Cout = cv.Ci;
   // convT: an ordinary k2s2 conv of dY; conv: the transposed gather
   a.tim = tim_slot(x.p, "dgrad " + pname(x, cv.w));
+  if (cv.fl_dgrad) {  // chunk-major pack: only conv3x3_fl_kernel reads it
+    a.wch = a.w;
+    a.w = nullptr;
+    CK(launch_conv3x3_fl(a, 1, x.st));
+    return 0;
+  }
   CK(launch_conv_fwd(a, cv.kind == L_CONVT ? MODE_FWD : MODE_TRANS, x.st));
   return 0;
 }
@@ -1401,9 +1435,13 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
       if (cv.kind == L_STEM) {
         t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_fwd), PK_STEM, cv.Co, 1, 7, 7};
       } else if (cv.kind == L_CONV) {
-        if (!cv.f8) t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_fwd), PK_CONV_FWD, cv.Co, cv.Ci, cv.R, cv.S};
+        if (!cv.f8)
+          t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_fwd), cv.fl_fwd ? PK_CONV_FWD_CH : PK_CONV_FWD, cv.Co,
+                                 cv.Ci, cv.R, cv.S};
         if (t.n == kMaxPack) RUN(flush());
-        if (training) t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_dgrad), PK_CONV_DGRAD, cv.Co, cv.Ci, cv.R, cv.S};
+        if (training)
+          t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_dgrad), cv.fl_dgrad ? PK_CONV_DGRAD_CH : PK_CONV_DGRAD,
+                                 cv.Co, cv.Ci, cv.R, cv.S};
       } else {
         t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_fwd), PK_CONVT_FWD, cv.Co, cv.Ci, cv.R, cv.S};
         if (t.n == kMaxPack) RUN(flush());

@@ -65,6 +65,7 @@ struct F8State { unsigned prev_bits; unsigned cur_bits; int code; int pad; };
 struct ConvFwdArgs {
   const bf16_t* x; int ldx;      // input NHWC bf16, channel stride ldx (stem: fp32 [N,H,W])
   const bf16_t* w;               // packed weights [Cout][R*S*C] (stem: [64][64])
+  const bf16_t* wch;             // chunk-major 3x3 pack [C/32][9][Cout][32] (conv3x3_fl_kernel)
   bf16_t* y; int ldy;            // output NHWC bf16
   const float* bias;             // [Cout] or null
   const bf16_t* add; int ldadd;  // optional addend (same pixel grid as y)
@@ -163,6 +164,12 @@ hipError_t launch_conv3x3_ws(const ConvFwdArgs& a, int mode, hipStream_t st);
 // the forward of this shape runs on the weight-stationary halo kernel, which
 // supports ConvFwdArgs::xform (the BN-apply prologue)
 bool conv3x3_ws_xform_ok(const ConvFwdArgs& a);
+// full-line halo kernel (conv_fl.hip) for 3x3/s1/p1 layers with C % 128 == 0,
+// Cout % 64 == 0 (P, Q multiples of 16): a.wch holds the chunk-major pack
+// (PK_CONV_FWD_CH / PK_CONV_DGRAD_CH); mode 0 conv, 1 dgrad.  The plan packs
+// those convs chunk-major exactly when conv3x3_fl_shape holds (UNET_NO_FL=1: never)
+bool conv3x3_fl_shape(int N, int C, int Cout, int P, int Q);
+hipError_t launch_conv3x3_fl(const ConvFwdArgs& a, int mode, hipStream_t st);
 // 3x3 / stride-2 / pad-1 data gradient by parity class on a shared dY halo
 // (conv_halo.hip), with the optional folded downsample (x2 / w2) range
 hipError_t launch_conv3x3s2_dgrad(const ConvFwdArgs& a, hipStream_t st);
@@ -339,7 +346,10 @@ hipError_t launch_d2f(const double* src, float* dst, int n, hipStream_t st);
 hipError_t launch_d2f_strided(const double* src, float* dst, int n, int stride, hipStream_t st);
 
 // weight (un)packing between torch fp32 layouts and kernel bf16 layouts
-enum { PK_CONV_FWD = 0, PK_CONV_DGRAD = 1, PK_CONVT_FWD = 2, PK_CONVT_DGRAD = 3, PK_STEM = 4 };
+// PK_CONV_*_CH: 3x3 convs of conv3x3_fl_kernel, chunk-major [K/32][9][Cout'][32]
+// (forward: K = Ci, Cout' = Co; data gradient: K = Co, Cout' = Ci)
+enum { PK_CONV_FWD = 0, PK_CONV_DGRAD = 1, PK_CONVT_FWD = 2, PK_CONVT_DGRAD = 3, PK_STEM = 4, PK_CONV_FWD_CH = 5,
+       PK_CONV_DGRAD_CH = 6 };
 struct PackEntry { const float* src; bf16_t* dst; int kind, Co, Ci, R, S; };
 enum { UP_CONV = 0, UP_CONVT = 1, UP_STEM = 2, UP_ZERO = 3 };  // UP_ZERO: dst[0 .. Co) = 0
 struct UnpackEntry { const float* acc; float* dst; int kind, Co, Ci, R, S; };

@@ -47,15 +47,18 @@ def local_bn_bwd(y, dout, mod, out=None, extra=None):
 
 
 @pytest.fixture(scope="module", params=[(1, None), (2, None), (1, (1, 64, 96)), (1, (2, 256, 256)),
-                                        (1, (1, 512, 512))],
-                ids=["base", "wide", "n1_64x96", "n2_256", "n1_512"])
+                                        (1, (1, 512, 512)), (1, (16, 256, 256))],
+                ids=["base", "wide", "n1_64x96", "n2_256", "n1_512", "n16_256"])
 def run(pkg, golden, cuda, request):
     """width 1 = Base topology; width 2 = the Wide config (every channel x2);
     n1_64x96 = a ragged case: batch 1, non-square, a 2x3 deepest level (the
     kernels' partial-tile and fallback paths); n2_256 = 256x256, large enough
     for the stride-2 halo weight gradients (enc2.0 / enc3.0 conv1 with the
     downsample's weight gradient folded in); n1_512 = one 512x512 image: the
-    Base geometry, so enc4 (16 x 16) runs the 16-wide batched weight gradient."""
+    Base geometry, so enc4 (16 x 16) runs the 16-wide batched weight gradient;
+    n16_256 = 16 images of 256x256: enc2 / enc3 / decoder4 / decoder3 fill the
+    chip with 16 x 16 x 64 work items, so they run on the full-line kernel
+    (conv_fl.hip), persistent (enc2: 2 items per block) and two-BN (enc3.1)."""
     width, shape = request.param
     # the stem runs by recompute (stem_rc.hip) and stores neither its raw conv
     # output y0 nor the maxpool/BN dZ; keep both for the teacher-forced rows
