@@ -1025,20 +1025,10 @@ hipError_t launch_conv3x3s2_dgrad(const ConvFwdArgs& a, hipStream_t st) {
   if ((size_t)a.N * a.H * a.W * a.ldx * 2 >= 0x80000000ull) return hipErrorNotSupported;
   if (a.x2 && (size_t)a.N * a.H * a.W * a.ldx2 * 2 >= 0x80000000ull) return hipErrorNotSupported;
   if ((size_t)a.Cout * 9 * a.C * 2 >= 0x80000000ull) return hipErrorNotSupported;
-  static const int forced = std::getenv("UNET_S2CFG") ? std::atoi(std::getenv("UNET_S2CFG")) : 0;  // tuning
-  auto fits = [&](int ti) { return a.H % ti == 0; };
-  switch (forced) {
-    case 1: if (fits(16)) return launch_s2d_ext<4, 2, 8>(a, st); break;
-    case 2: if (fits(8)) return launch_s2d_ext<4, 1, 8>(a, st); break;
-    case 3: if (fits(4)) return launch_s2d_ext<4, 1, 4>(a, st); break;
-    case 4: if (fits(8)) return launch_s2d_ext<2, 1, 8>(a, st); break;
-    case 5: if (fits(8)) return launch_s2d_ext<2, 2, 4>(a, st); break;
-    case 6: if (fits(4)) return launch_s2d_ext<2, 1, 4>(a, st); break;
-    default: break;
-  }
   const long long ncb = a.Cout / 64;
+  auto fits = [&](int ti) { return a.H % ti == 0; };
   auto blocks = [&](int ti) { return (long long)a.N * (a.H / ti) * (a.W / 16) * ncb; };
-  // measured (16 x 512^2 Base, UNET_S2CFG sweep): 16-row tiles while they fill
+  // measured (16 x 512^2 Base, round-2 tile sweep): 16-row tiles while they fill
   // the chip (enc2.0: 51 us, was 79 on the implicit-GEMM kernel), else 32-channel
   // blocks of 8 rows (enc3.0 36 us, was 49; enc4.0 33 us, was 52)
   if (fits(16) && blocks(16) >= 256) return launch_s2d_ext<4, 2, 8>(a, st);
@@ -1081,8 +1071,8 @@ static hipError_t launch_hs(const ConvFwdArgs& a, hipStream_t st) {
   const int ncb = a.Cout / COT;
   const int ntiles = a.N * (a.P / TH) * (a.Q / 16);
   // two 80 KB blocks per CU: past 512 blocks the grid stays at 512 and each
-  // block walks several tiles (UNET_HS_SLOTS overrides, 0 = one tile per block)
-  static const int slots_env = std::getenv("UNET_HS_SLOTS") ? std::atoi(std::getenv("UNET_HS_SLOTS")) : 512;
+  // block walks several tiles
+  constexpr int slots_env = 512;
   // (forward only: the multi-tile data gradient holds its fused BN-backward
   // epilogue operands across tiles, 324 VGPRs, one block per CU)
   long long grid = (long long)ntiles * ncb;
@@ -1111,57 +1101,34 @@ static hipError_t launch_halo_shape(const ConvFwdArgs& a, hipStream_t st) {
   // the halo-streamed kernel with the two-BN epilogue
   if (FLIP && a.bb.sums && a.bb.y2) {
     if (!(C % 32 == 0 && C >= 128 && Co % 64 == 0)) return hipErrorNotSupported;
-    static const int tcfg = std::getenv("UNET_HSTWO") ? std::atoi(std::getenv("UNET_HSTWO")) : 0;  // tuning
-    if (tcfg == 1 && a.P % 16 == 0) return launch_hs<2, 16, 4, true, true>(a, st);
     // 32-channel blocks, 8 waves (two blocks per CU): enc2-4 downsample-block
     // dgrads 63 / 49 / 42 -> 56 / 40 / 35 us (Base, measured)
-    if (tcfg != 9 && a.P % 16 == 0 && Co % 32 == 0) return launch_hs<2, 16, 8, true, true>(a, st);
+    if (a.P % 16 == 0 && Co % 32 == 0) return launch_hs<2, 16, 8, true, true>(a, st);
     const long long t16 = (long long)a.N * (a.P / 16) * (a.Q / 16) * (Co / 64);
     if (a.P % 16 == 0 && t16 >= 256) return launch_hs<4, 16, 8, true, true>(a, st);
     if (a.P % 8 == 0) return launch_hs<4, 8, 4, true, true>(a, st);
     return hipErrorNotSupported;
   }
   // weight-stationary: every tap of the block's channels fits in LDS
-  static const int wscfg = std::getenv("UNET_WSCFG") ? std::atoi(std::getenv("UNET_WSCFG")) : 0;  // tuning
-  if (wscfg == 1 && C == 64 && Co % 32 == 0 && a.P % 4 == 0) return launch_ws<2, 2, 4, 4, FLIP>(a, st);
-  if (wscfg == 2 && C == 64 && Co % 32 == 0 && a.P % 8 == 0) return launch_ws<2, 2, 8, 4, FLIP>(a, st);
-  if (wscfg == 3 && C == 64 && Co % 32 == 0 && a.P % 8 == 0) return launch_ws<2, 2, 8, 8, FLIP>(a, st);
-  if (wscfg == 4 && C == 64 && Co % 64 == 0 && a.P % 16 == 0) return launch_ws<2, 4, 16, 4, FLIP>(a, st);
   if (C == 64 && Co % 64 == 0 && a.P % 16 == 0) return launch_ws<2, 4, 16, 8, FLIP>(a, st);
-  // decoder1 shapes (256^2, 96 / 32 channels), UNET_D1CFG sweep on the Base
+  // decoder1 shapes (256^2, 96 / 32 channels), round-3 sweep on the Base
   // config: 8-row tiles on 8 waves (one row each, two waves per SIMD hide each
   // other's LDS latency) beat the 4-wave and 16-row tiles except for the 32->32
   // forward (decoder1.0 dgrad 140 -> 111 us: the FN = 6 block spilled 36
   // VGPRs; decoder1.0 fwd 121 -> 104, decoder1.3 dgrad 60 -> 55)
-  static const int d1 = std::getenv("UNET_D1CFG") ? std::atoi(std::getenv("UNET_D1CFG")) : 0;  // tuning
   if (C == 32 && Co == 32 && a.P % 16 == 0) {
-    if (d1 == 1) return launch_ws<1, 2, 16, 8, FLIP>(a, st);
-    if (d1 == 2) return launch_ws<1, 2, 8, 4, FLIP>(a, st);
-    if (FLIP || d1 == 3) return launch_ws<1, 2, 8, 8, FLIP>(a, st);
+    if (FLIP) return launch_ws<1, 2, 8, 8, FLIP>(a, st);
     return launch_ws<1, 2, 16, 4, FLIP>(a, st);
   }
-  if (C == 32 && Co == 96 && a.P % 16 == 0) {
-    if (d1 == 1) return launch_ws<1, 2, 16, 8, FLIP>(a, st);
-    if (d1 == 2) return launch_ws<1, 6, 16, 4, FLIP>(a, st);
-    if (d1 == 4) return launch_ws<1, 6, 16, 8, FLIP>(a, st);
-    return launch_ws<1, 2, 8, 8, FLIP>(a, st);
-  }
+  if (C == 32 && Co == 96 && a.P % 16 == 0) return launch_ws<1, 2, 8, 8, FLIP>(a, st);
   if (C == 32 && Co % 64 == 0 && a.P % 16 == 0) return launch_ws<1, 4, 16, 8, FLIP>(a, st);
-  if (C == 96 && Co == 32 && a.P % 8 == 0) {
-    if (d1 == 2 && a.P % 4 == 0) return launch_ws<3, 2, 4, 4, FLIP>(a, st);
-    if (d1 == 4) return launch_ws<3, 2, 8, 4, FLIP>(a, st);
-    return launch_ws<3, 2, 8, 8, FLIP>(a, st);
-  }
+  if (C == 96 && Co == 32 && a.P % 8 == 0) return launch_ws<3, 2, 8, 8, FLIP>(a, st);
   // halo-streamed: 256-pixel tiles while they still give >= ~1 block per CU
   if (C % 32 == 0 && C >= 128 && Co % 64 == 0) {
     const long long t16 = (long long)a.N * (a.P / 16) * (a.Q / 16) * (Co / 64);
     // round 1 ran the C = 128 forwards (enc2, decoder3.3) as a 128x128 im2col
     // tile (faster than the 64-channel halo blocks then); the 32-channel
-    // halo blocks below beat it (37-43 -> 31 us).  UNET_C128GLDS=1: old choice
-    static const bool c128_glds = std::getenv("UNET_C128GLDS") != nullptr;  // A/B
-    if (c128_glds && !FLIP && C == 128 && t16 > 256 && t16 <= 512) return hipErrorNotSupported;
-    static const int hcfg = std::getenv("UNET_HSCFG") ? std::atoi(std::getenv("UNET_HSCFG")) : 0;  // tuning
-    if (hcfg == 9 && a.P % 16 == 0 && t16 >= 256) return launch_hs<4, 16, 8, FLIP, false>(a, st);  // round-1 choice
+    // halo blocks below beat it (37-43 -> 31 us)
     // 32-channel output blocks (80 KB of LDS: two blocks per CU, so one
     // block's epilogue overlaps the other's MFMAs; measured on the Base
     // config: enc3/decoder4 dgrads -5..-7 %, enc4 -11..-19 %): 8 waves when
@@ -1188,8 +1155,7 @@ static bool ws_fwd_shape(const ConvFwdArgs& a) {
 }
 
 bool conv3x3_ws_xform_ok(const ConvFwdArgs& a) {
-  static const bool wscfg = std::getenv("UNET_WSCFG") != nullptr;
-  return !wscfg && a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.H == a.P &&
+  return a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.H == a.P &&
          a.W == a.Q && a.Q % 16 == 0 && a.ldx % 8 == 0 && a.ldy % 4 == 0 && !a.x2 && !a.fold_on && !a.add &&
          !a.bb.sums && a.ldxh % 8 == 0 && ws_fwd_shape(a) && (size_t)a.N * a.H * a.W * a.ldx * 2 < 0x80000000ull;
 }

@@ -1052,30 +1052,7 @@ constexpr int wgrad_halo_rows() {  // LDS halo capacity (rows), a multiple of on
 // DSF (SD = 2): the block's downsample weight gradient rides in the same
 // stages: a dY2 tile beside dY, one more A fragment pair at the centre tap,
 // two more accumulator fragments (slab frags 18, 19).
-// FUSE (SD = 1, CI = 64; a.bn_fuse): the BN-backward apply of the BN after
-// this conv runs here instead of in its own pass.  The A tile staged is dZ
-// (a.dy = bn.da); y is loaded into registers one stage ahead; at the end of
-// the previous stage every thread rewrites the two 16-B chunks it staged as
-// dY = A dZ + B y + C (bn_bwd_apply_kernel's coefficients and expression, so
-// bit-identical), the blocks of input-channel block 0 store them to bn.dy (the
-// dgrad's input, the side product); the next stage barrier publishes the tile.
-__device__ __forceinline__ void lds_barrier_wg() {  // LDS only: outstanding global ops stay in flight
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-// 16-B store the compiler does not count (the kernel's hand-counted vmcnt
-// waits include it).  The s_nop is the VMEM-store data hazard: a VALU write to a
-// data VGPR of a >8-B store in the next cycle can land before the store reads
-// it (hipcc pads its own stores; measured without it: the chunk's first dword
-// replaced by the next instruction's result)
-__device__ __forceinline__ void st_u4_asm(void* p, const uint4& u) {
-  const u32x4 v = {u.x, u.y, u.z, u.w};
-  asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-}
-
-template <int TW, int NS, int CI, bool CO32 = false, int SD = 1, bool DSF = false, bool FUSE = false>
+template <int TW, int NS, int CI, bool CO32 = false, int SD = 1, bool DSF = false>
 __global__ void __launch_bounds__(CI * 8)
 wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
   constexpr int NW = CI / 8;            // waves
@@ -1093,7 +1070,6 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
   static_assert(HROWS <= HCAP && HCAP % (HRPI * NW) == 0, "halo rows");
   static_assert(SD == 1 || (CI == 32 && !CO32 && TW % 8 == 0), "stride-2 variant");
   static_assert(!DSF || SD == 2, "downsample fold: stride-2 kernel only");
-  static_assert(!FUSE || (SD == 1 && !CO32 && !DSF && CI == 64), "BN-fused variant");
   constexpr int D_BYTES = DSF ? A_BYTES : 0;  // dY2 tile
   constexpr int STAGE = A_BYTES + B_BYTES + D_BYTES;
   constexpr int NF = DSF ? 20 : 18;           // accumulator fragments per wave
@@ -1136,40 +1112,6 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
   // tile's (wave-uniform, non-negative) origin passed as the scalar offset;
   // the halo keeps a per-stage bounds test on precomputed (row, col).
   unsigned arel[A_INS], arel2[DSF ? A_INS : 1];
-  // FUSE: y / dY offsets (elements) of the same chunks and their coefficients
-  constexpr int FJ = FUSE ? A_INS : 1;
-  unsigned yrel[FJ], drel[FJ], crel[FJ];  // crel: the chunk's first channel in the coefficient table
-  const float* fcoef = reinterpret_cast<const float*>(smem + NS * STAGE);  // [3][64]: A | B | C
-  const bool store_dy = FUSE && cib == 0;
-  if constexpr (FUSE) {  // coefficient table of the block's 64 channels (before any LDS-DMA is issued)
-    float* fc = reinterpret_cast<float*>(smem + NS * STAGE);
-    if (tid < 64) {
-      const int ch = co0 + tid;
-      float A = 0.f, B = 0.f, C = 0.f;
-      if (ch < a.Cout) {
-        double s1, s2;
-        bn_bwd_apply_coef(a.bn, ch, 1.0 / (double)a.bn.npix, A, B, C, s1, s2);
-        if (split == 0 && cib == 0) {  // the apply pass's block-0 parameter gradients
-          a.bn.dgamma[ch] = (float)s2;
-          a.bn.dbeta[ch] = (float)s1;
-        }
-      }
-      fc[tid] = A;
-      fc[64 + tid] = B;
-      fc[128 + tid] = C;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < FJ; ++j) {
-      const int row = (wave * A_INS + j) * 8 + arow;
-      const int f = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
-      const int lchunk = ((((aslot >> 1) ^ f)) << 1) | (aslot & 1);
-      const unsigned rp = (unsigned)((row / TW) * a.Q + row % TW);
-      yrel[j] = rp * (unsigned)a.bn.ldy + co0 + lchunk * 8;
-      drel[j] = rp * (unsigned)a.bn.lddy + co0 + lchunk * 8;
-      crel[j] = lchunk * 8;
-    }
-  }
 #pragma unroll
   for (int j = 0; j < A_INS; ++j) {
     const int row = (wave * A_INS + j) * 8 + arow;  // pixel in tile
@@ -1225,78 +1167,18 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
 #pragma unroll
   for (int i = 0; i < (DSF ? 2 : 1); ++i) acc2[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // FUSE: stage s is transformed at the end of iteration s - 1 (after that
-  // iteration's MFMAs): its y chunks are loaded into registers at the top of
-  // the same iteration (compiler-tracked loads: an untracked asm load's
-  // destination registers may be copied by the allocator before the data
-  // lands -- measured: half of a dY tensor wrong),
-  // its dZ chunks were staged by this thread's own LDS-DMA, and the barrier at
-  // the top of iteration s publishes the rewritten tile.
-  auto tile_base = [&](int kt) {  // pixel index of the stage's tile origin
-    const int t = t0 + kt;
-    const int n = t / (tp * tq);
-    const int rem = t - n * (tp * tq);
-    return ((size_t)n * a.P + (rem / tq) * TH) * a.Q + (rem % tq) * TW;
-  };
-  auto issue_y = [&](int kt, uint4 (&yv)[FJ]) {
-    const size_t pb = tile_base(kt);
-#pragma unroll
-    for (int j = 0; j < FJ; ++j) yv[j] = *reinterpret_cast<const uint4*>(a.bn.y + pb * a.bn.ldy + yrel[j]);
-  };
-  // dY = A dZ + B y + C over the chunks this thread staged for stage kt (its
-  // LDS-DMA and the y loads have landed), in place, and the side-product store
-  auto transform = [&](int kt, uint4 (&yv)[FJ]) {
-    char* Aw = smem + (kt % NS) * STAGE;
-    const size_t pb = tile_base(kt);
-#pragma unroll
-    for (int j = 0; j < FJ; ++j) {
-      uint4* q = reinterpret_cast<uint4*>(Aw + (wave * A_INS + j) * 1024 + lane * 16);
-      float dz[8], yy[8], o[8], cA[8], cB[8], cC[8];
-      unpack8(*q, dz);
-      unpack8(yv[j], yy);
-#pragma unroll
-      for (int k = 0; k < 8; k += 4) {
-        *reinterpret_cast<float4*>(cA + k) = *reinterpret_cast<const float4*>(fcoef + crel[j] + k);
-        *reinterpret_cast<float4*>(cB + k) = *reinterpret_cast<const float4*>(fcoef + 64 + crel[j] + k);
-        *reinterpret_cast<float4*>(cC + k) = *reinterpret_cast<const float4*>(fcoef + 128 + crel[j] + k);
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] = fmaf(cA[k], dz[k], fmaf(cB[k], yy[k], cC[k]));
-      const uint4 ov = pack8(o);
-      *q = ov;
-      if (store_dy) st_u4_asm(a.bn.dy + pb * a.bn.lddy + drel[j], ov);
-    }
-  };
-
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
     if (s < KT) issue(s, s);
-  if constexpr (FUSE) {
-    static_assert(NS == 3, "FUSE wait counts assume one stage of DMA ahead");
-    if (KT > 0) {
-      uint4 y0[FJ];
-      issue_y(0, y0);
-      wait_vmcnt<0>();  // DMA(0), DMA(1), y(0)
-      transform(0, y0);
-    }
-  }
   const int g = lane >> 4, li = lane & 15, trq = li >> 2, trp = li & 3;
   TSTAMP(a.tim, 1);
   for (int kt = 0; kt < KT; ++kt) {
     const int ahead = KT - 1 - kt;
-    if constexpr (FUSE) {
-      lds_barrier_wg();  // stage kt (staged, landed and transformed last iteration) visible to every wave
-    } else {
-      if (ahead >= NS - 2) wait_vmcnt<(NS - 2) * LPS>();
-      else if (NS > 3 && ahead == 1) wait_vmcnt<LPS>();
-      else wait_vmcnt<0>();
-      __builtin_amdgcn_s_barrier();
-    }
+    if (ahead >= NS - 2) wait_vmcnt<(NS - 2) * LPS>();
+    else if (NS > 3 && ahead == 1) wait_vmcnt<LPS>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
     if (kt < 16) TSTAMP(a.tim, 2 + kt);
-    uint4 ynext[FJ];
-    if constexpr (FUSE) {
-      if (kt + 1 < KT) issue_y(kt + 1, ynext);
-    }
     if (kt + NS - 1 < KT && UNET_ABL != 2) issue(kt + NS - 1, (kt + NS - 1) % NS);
     const char* As = smem + (kt % NS) * STAGE;
     const char* Bs = As + A_BYTES;
@@ -1333,14 +1215,6 @@ wgrad3x3_halo_kernel(ConvWgradArgs a, int tiles_total, int tiles_per_split) {
             }
           }
         }
-    }
-    if constexpr (FUSE) {
-      if (kt + 1 < KT) {
-        // DMA(kt+1) (issued last iteration) and y(kt+1) landed; younger: DMA(kt+2)
-        if (kt + NS - 1 < KT) wait_vmcnt<LPS>();
-        else wait_vmcnt<0>();
-        transform(kt + 1, ynext);
-      }
     }
   }
   wait_vmcnt<0>();
@@ -2637,13 +2511,13 @@ static void halo_geometry(const ConvWgradArgs& a, int& blocks_xy, int& tiles, in
   constexpr int TH = 128 / TW;
   blocks_xy = (CO32 ? a.Cout / 32 : (a.Cout + 63) / 64) * (a.C / CI);
   tiles = a.N * (a.P / TH) * (a.Q / TW);
-  static const int target = std::getenv("UNET_WG_TARGET") ? std::atoi(std::getenv("UNET_WG_TARGET")) : 256;  // tuning
+  constexpr int target = 256;  // split-K blocks aimed for
   splits = std::max(1, std::min(tiles, target / blocks_xy));
   per = (tiles + splits - 1) / splits;
   splits = (tiles + per - 1) / per;
 }
 
-template <int TW, int CI, bool CO32 = false, int NSO = 0, int SD = 1, bool DSF = false, bool FUSE = false>
+template <int TW, int CI, bool CO32 = false, int NSO = 0, int SD = 1, bool DSF = false>
 static hipError_t launch_wgrad_halo(const ConvWgradArgs& a0, hipStream_t st) {
   ConvWgradArgs a = a0;
   a.co_blocks = CO32 ? a.Cout / 32 : (a.Cout + 63) / 64;
@@ -2661,13 +2535,12 @@ static hipError_t launch_wgrad_halo(const ConvWgradArgs& a0, hipStream_t st) {
     splits = (tiles + per - 1) / per;
   }
   constexpr int NS = NSO ? NSO : (CI == 64 ? 3 : 4);
-  constexpr size_t lds = (size_t)NS * (128 * 128 * (DSF ? 2 : 1) + wgrad_halo_rows<TW, CI, SD>() * CI * 2) +
-                         (FUSE ? 3 * 64 * sizeof(float) : 0);
+  constexpr size_t lds = (size_t)NS * (128 * 128 * (DSF ? 2 : 1) + wgrad_halo_rows<TW, CI, SD>() * CI * 2);
   static_assert(lds <= 163840, "LDS");
   // the full template argument list, as rocprofv3 spells the kernel
-  set_kernel_tag("wgrad3x3_halo_kernel<%d, %d, %d, %s, %d, %s, %s>", TW, NS, CI, CO32 ? "true" : "false", SD,
-                 DSF ? "true" : "false", FUSE ? "true" : "false");
-  hipLaunchKernelGGL((wgrad3x3_halo_kernel<TW, NS, CI, CO32, SD, DSF, FUSE>), dim3(blocks_xy * splits), dim3(CI * 8),
+  set_kernel_tag("wgrad3x3_halo_kernel<%d, %d, %d, %s, %d, %s>", TW, NS, CI, CO32 ? "true" : "false", SD,
+                 DSF ? "true" : "false");
+  hipLaunchKernelGGL((wgrad3x3_halo_kernel<TW, NS, CI, CO32, SD, DSF>), dim3(blocks_xy * splits), dim3(CI * 8),
                      lds, st, a, tiles, per);
   if (a.slab && splits > 1) {
     SlabLayout L = {};
@@ -2859,56 +2732,24 @@ bool wgrad_s2_fold_ok(const ConvWgradArgs& a) {
          (size_t)a.N * a.P * a.Q * (a.lddy > a.lddy2 ? a.lddy : a.lddy2) * 2 < 0x80000000ull;
 }
 
-// the BN-backward apply can ride in this 3x3 / s1 weight gradient (a.bn set):
-// the same shape test as the 64-channel halo choice below
-bool wgrad_bn_fuse_ok(const ConvWgradArgs& a) {
-  static const bool off = std::getenv("UNET_WGCFG") != nullptr;  // tuning runs pick their own kernel
-  const BnBwdArgs& b = a.bn;
-  return !off && a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.C % 64 == 0 &&
-         a.P == a.H && a.Q == a.W && ((a.Q % 32 == 0 && a.P % 4 == 0) || (a.Q % 16 == 0 && a.P % 8 == 0)) &&
-         (size_t)a.N * a.H * a.W * a.ldx * 2 < 0x80000000ull && (size_t)a.N * a.P * a.Q * b.ldda * 2 < 0x80000000ull &&
-         b.da && b.y && b.dy && !b.y2 && !b.coef && b.C == a.Cout && b.ldda % 8 == 0 && b.ldy % 8 == 0 &&
-         b.lddy % 8 == 0 && b.npix == (int64_t)a.N * a.P * a.Q;
-}
-
 hipError_t launch_conv_wgrad(const ConvWgradArgs& a0, int stem, hipStream_t st) {
-  if (a0.bn_fuse && !stem) {  // dZ staged in place of dY, dY stored as a side product
-    if (!wgrad_bn_fuse_ok(a0)) return hipErrorInvalidValue;
-    ConvWgradArgs a = a0;
-    a.dy = a.bn.da;
-    a.lddy = a.bn.ldda;
-    if (a.Q % 32 == 0 && a.P % 4 == 0) return launch_wgrad_halo<32, 64, false, 0, 1, false, true>(a, st);
-    return launch_wgrad_halo<16, 64, false, 0, 1, false, true>(a, st);
-  }
   const ConvWgradArgs& a = a0;
   if (stem)
     return a.Cout % 64 == 0 ? launch_stem_wgrad(a, st) : launch_wgrad_cfg<XLOAD_STEM, 64, 64, 64, 2, 2>(a, st);
   if (a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.C % 32 == 0 && a.P == a.H &&
       a.Q == a.W && (size_t)a.N * a.H * a.W * a.ldx * 2 < 0x80000000ull &&
       (size_t)a.N * a.P * a.Q * a.lddy * 2 < 0x80000000ull) {
-    static const int wcfg = std::getenv("UNET_WGCFG") ? std::atoi(std::getenv("UNET_WGCFG")) : 0;  // tuning
-    if (a.Q % 32 == 0 && a.P % 4 == 0) {
-      if (wcfg == 1 && a.C % 64 == 0) return launch_wgrad_halo<32, 64, false, 2>(a, st);
-      if (wcfg == 2) return launch_wgrad_halo<32, 32, false, 2>(a, st);
-      if (wcfg == 3) return launch_wgrad_halo<32, 32, false, 3>(a, st);
-    }
     if (a.C % 64 == 0) {
       // loader-wave kernel where blocks share their tiles (C or Cout >= 128:
       // enc2-3, decoder2-4 first convs), the all-waves-issue kernel for the
       // 64 x 64-channel layers (enc1, decoder2.3), where the loader form
-      // measured slower (profiles/r04/s1).  UNET_WG_LD=0: never, 1: always (A/B)
-      static const int ld = std::getenv("UNET_WG_LD") ? std::atoi(std::getenv("UNET_WG_LD")) : 2;
-      if (ld && (ld != 2 || a.C >= 128 || a.Cout >= 128) && a.Cout % 64 == 0 && a.Q % 32 == 0 && a.P % 4 == 0 &&
-          wcfg == 0)
+      // measured slower (profiles/r04/s1)
+      if ((a.C >= 128 || a.Cout >= 128) && a.Cout % 64 == 0 && a.Q % 32 == 0 && a.P % 4 == 0)
         return launch_wgrad_ld(a, st);
       if (a.Q % 32 == 0 && a.P % 4 == 0) return launch_wgrad_halo<32, 64>(a, st);
       if (a.Q % 16 == 0 && a.P % 8 == 0) return launch_wgrad_halo<16, 64>(a, st);
     }
-    if (a.Cout == 32 && a.Q % 32 == 0 && a.P % 4 == 0) {
-      if (wcfg == 4) return launch_wgrad_halo<32, 32, true, 2>(a, st);
-      if (wcfg == 5) return launch_wgrad_halo<32, 32, true, 3>(a, st);
-      return launch_wgrad_halo<32, 32, true>(a, st);
-    }
+    if (a.Cout == 32 && a.Q % 32 == 0 && a.P % 4 == 0) return launch_wgrad_halo<32, 32, true>(a, st);
     if (a.Q % 32 == 0 && a.P % 4 == 0) return launch_wgrad_halo<32, 32>(a, st);
     if (a.Q % 16 == 0 && a.P % 8 == 0) return launch_wgrad_halo<16, 32>(a, st);
   }

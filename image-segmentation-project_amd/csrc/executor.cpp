@@ -193,10 +193,6 @@ struct unet_plan {
   // single-stream backward: a weight gradient's split-K reduction rides in the
   // next BN-backward apply launch (UNET_NO_MERGE_REDUCE=1: separate launches)
   bool merge_reduce = std::getenv("UNET_NO_MERGE_REDUCE") == nullptr;
-  // the BN-backward apply of a 3x3 / s1 conv's output BN runs inside that conv's
-  // weight gradient (wgrad_bn_fuse_ok).  Off unless UNET_WG_BN=1: measured
-  // slower than the separate apply pass
-  bool wg_bn_fuse = std::getenv("UNET_WG_BN") != nullptr;
   // 3x3 / s1 weight gradients of a gradient bucket collected and run as ONE
   // batched stream-K launch at the bucket boundary (wgrad3x3_batch_kernel):
   // no per-layer split-K slab round trip.  UNET_WG_BATCH=0: one launch per layer (A/B)
@@ -1043,9 +1039,7 @@ int wgrad_and_reduce(const Ctx& x, ConvWgradArgs& a, int mode, const std::string
 
 // ds >= 0: the block's 1x1 / stride-2 downsample weight gradient (dY = *dyds,
 // same input) folded into this 3x3 / stride-2 conv's launch (ds_fold_ok).
-// bnf: the BN-backward apply producing dy rides in this launch (bn_fused_wgrad)
-int conv_wgrad(const Ctx& x, int ci, const Act& dy, const Act& in, int ds = -1, const Act* dyds = nullptr,
-               const BnBwdArgs* bnf = nullptr) {
+int conv_wgrad(const Ctx& x, int ci, const Act& dy, const Act& in, int ds = -1, const Act* dyds = nullptr) {
   const Conv& cv = x.p->convs[ci];
   ConvWgradArgs a = {};
   a.N = x.p->cfg.N;
@@ -1066,11 +1060,6 @@ int conv_wgrad(const Ctx& x, int ci, const Act& dy, const Act& in, int ds = -1, 
   a.P = dy.H; a.Q = dy.W; a.Cout = cv.Co;
   double fl = conv_flops(x.p, cv, dy);
   std::string name = pname(x, cv.w);
-  if (bnf) {
-    a.bn = *bnf;
-    a.bn_fuse = 1;
-    name += " +bn";
-  }
   if (ds >= 0) {
     const Conv& dv = x.p->convs[ds];
     a.dy2 = x.A(*dyds); a.lddy2 = dyds->ld;
@@ -1152,23 +1141,6 @@ int flush_wgrad_batch(const Ctx& x) {
   p->wgb_names.clear();
   p->wgb_flops = 0;
   return 0;
-}
-
-// The BN-backward apply f (dY = f.dy from dZ = f.da and y) can ride in the
-// weight gradient of conv ci over input `in` (wgrad_bn_fuse_ok): fused
-// backward only (dZ stored by its producer), plain single-stream step
-bool bn_fused_wgrad(const Ctx& x, int ci, const Act& dy, const Act& in, const BnBwdArgs& f) {
-  const unet_plan* p = x.p;
-  if (!p->fuse_bwd || !p->wg_bn_fuse || x.wst != x.st) return false;
-  const Conv& cv = p->convs[ci];
-  if (cv.kind != L_CONV) return false;
-  ConvWgradArgs a = {};
-  a.N = p->cfg.N;
-  a.R = cv.R; a.S = cv.S; a.stride = cv.stride; a.pad = cv.pad;
-  a.ldx = in.ld; a.H = in.H; a.W = in.W; a.C = cv.Ci;
-  a.P = dy.H; a.Q = dy.W; a.Cout = cv.Co;
-  a.bn = f;
-  return wgrad_bn_fuse_ok(a);
 }
 
 // the downsample's weight gradient can ride in conv1's stride-2 halo wgrad
@@ -1667,19 +1639,14 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
       }
       RUN(bn_backward(x, d.bn2, c.bb, true));
     }
-    // without attention the two BN-backward applies ride in the convs' weight
-    // gradients where the shape allows (bn_fused_wgrad)
-    const BnBwdArgs fd2 = dec_bn2(l);
-    const bool wd2 = !att && bn_fused_wgrad(x, d.conv2, d.dy2, d.h, fd2);
-    if (!att && !wd2) RUN(bn_backward(x, d.bn2, fd2, fz));
+    if (!att) RUN(bn_backward(x, d.bn2, dec_bn2(l), fz));
     RUN(fork());
-    RUN(conv_wgrad(x, d.conv2, d.dy2, d.h, -1, nullptr, wd2 ? &fd2 : nullptr));
+    RUN(conv_wgrad(x, d.conv2, d.dy2, d.h));
     const BnBwdArgs f1 = dec_bn1(l);
     RUN(conv_dgrad(x, d.conv2, d.dy2, d.dh, nullptr, fz ? &f1 : nullptr));
-    const bool wd1 = bn_fused_wgrad(x, d.conv1, d.dy1, d.cat, f1);
-    if (!wd1) RUN(bn_backward(x, d.bn1, f1, fz));
+    RUN(bn_backward(x, d.bn1, f1, fz));
     RUN(fork());
-    RUN(conv_wgrad(x, d.conv1, d.dy1, d.cat, -1, nullptr, wd1 ? &f1 : nullptr));
+    RUN(conv_wgrad(x, d.conv1, d.dy1, d.cat));
     RUN(conv_dgrad(x, d.conv1, d.dy1, d.dcat, nullptr, nullptr, -1, nullptr, d.split ? &d.dcat_up : nullptr));
     // (decoder conv bias gradients: exactly 0, written by bucket 0's unpack)
     // up-conv: dU = dcat[:, skip:]; its dgrad is dA of the previous decoder's
@@ -1762,21 +1729,16 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
       }
       continue;
     }
-    // the BN-backward applies of blocks without a downsample ride in the convs'
-    // weight gradients where the shape allows (bn_fused_wgrad)
-    const BnBwdArgs f2 = blk_bn2(i);
-    const bool w2 = b.ds < 0 && bn_fused_wgrad(x, b.conv2, b.dy2, b.h, f2);
-    if (!w2) RUN(bn_backward(x, b.bn2, f2, fz));
+    RUN(bn_backward(x, b.bn2, blk_bn2(i), fz));
     RUN(fork());
-    RUN(conv_wgrad(x, b.conv2, b.dy2, b.h, -1, nullptr, w2 ? &f2 : nullptr));
+    RUN(conv_wgrad(x, b.conv2, b.dy2, b.h));
     const bool dsfold = p->ds_wgrad_fold && ds_fold_ok(x, b);
     if (b.ds >= 0 && !dsfold) RUN(conv_wgrad(x, b.ds, b.dyds, b.in));
     const BnBwdArgs f1 = blk_bn1(i);
     RUN(conv_dgrad(x, b.conv2, b.dy2, b.dh, nullptr, fz ? &f1 : nullptr));
-    const bool w1 = b.ds < 0 && bn_fused_wgrad(x, b.conv1, b.dy1, b.in, f1);
-    if (!w1) RUN(bn_backward(x, b.bn1, f1, fz));
+    RUN(bn_backward(x, b.bn1, f1, fz));
     RUN(fork());
-    RUN(conv_wgrad(x, b.conv1, b.dy1, b.in, dsfold ? b.ds : -1, &b.dyds, w1 ? &f1 : nullptr));
+    RUN(conv_wgrad(x, b.conv1, b.dy1, b.in, dsfold ? b.ds : -1, &b.dyds));
     // the last writer of d_in produces dA of the previous block's bn2
     BnBwdArgs fp = {};
     const BnBwdArgs* fprev = nullptr;

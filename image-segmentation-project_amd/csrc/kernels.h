@@ -135,8 +135,7 @@ struct ConvWgradArgs {
   // without one (single-op C ABI) the kernels add into a zeroed dW with fp32
   // atomics.
   float* slab; size_t slab_bytes;
-  // bn_fuse != 0 (stem; and 3x3 / s1 halo wgrads, wgrad_bn_fuse_ok, which
-  // also store dY to bn.dy for the dgrad): the stem does not store dY; it forms it while
+  // bn_fuse != 0 (stem only): the stem does not store dY; it forms it while
   // loading, dY = A dZ + B y + C per channel, from the stem BN's backward sums
   // (bn.sums, reduced by the fused maxpool backward), bn.da = dZ, bn.y = the raw
   // stem conv output — the expression of bn_bwd_apply_kernel, so dY is bit-
@@ -152,9 +151,6 @@ struct ConvWgradArgs {
 };
 // the stride-2 halo weight gradient covers this shape (and then folds a.dy2)
 bool wgrad_s2_fold_ok(const ConvWgradArgs& a);
-// a (non-stem) weight gradient with bn_fuse = 1 applies the BN backward of
-// a.bn (dZ = bn.da, y = bn.y, side product dY = bn.dy) in its staging
-bool wgrad_bn_fuse_ok(const ConvWgradArgs& a);
 
 hipError_t launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st);
 hipError_t launch_conv_fwd_v1(const ConvFwdArgs& a, int mode, hipStream_t st);  // register-staged

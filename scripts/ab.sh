@@ -6,6 +6,8 @@
 # in-tree libunet_hip.so); e.g.
 #   scripts/ab.sh 3 - @ab/libunet_hip_r04.so UNET_APPLY_CAP=1024
 #   BENCH_ARGS="--width 2" scripts/ab.sh 3 - UNET_NO_FL=1
+# AB_LAYERS="<regex>": per-layer instead (scripts/layer_profile.py, HIP events
+# around every launch), printing the matching launch lines of every variant
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -20,6 +22,12 @@ for r in $(seq 1 $R); do
     args=()
     [ -n "$envs" ] && IFS=',' read -ra args <<< "$envs"
     [ -n "$lib" ] && args+=("UNET_HIP_LIB=$PWD/$lib")
+    if [ -n "$AB_LAYERS" ]; then
+      echo "=== round $r [$spec]" | tee -a $out
+      env "${args[@]}" timeout -k 10 120 python3 scripts/layer_profile.py --top 400 > gpurun_out/ab_layers.log 2>&1 || exit 1
+      grep -E "$AB_LAYERS" gpurun_out/ab_layers.log | tee -a $out
+      continue
+    fi
     v=$(env "${args[@]}" timeout -k 10 120 python3 bench.py --no-cpu-baseline --no-parity --steps 30 --warmup 10 \
         $BENCH_ARGS 2>/dev/null | grep -o '"value": [0-9.]*' | grep -o '[0-9.]*$') || exit 1
     echo "round $r [$spec] $v" | tee -a $out
