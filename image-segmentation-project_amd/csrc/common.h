@@ -28,9 +28,22 @@ using unet::kTimSlots;
     if ((T) && threadIdx.x == 0 && blockIdx.x < (unsigned)kTimBlocks)                     \
       (T)[blockIdx.x * kTimSlots + (k)] = __builtin_amdgcn_s_memrealtime();               \
   } while (0)
+// the same from thread `th` (a wave other than wave 0)
+#define TSTAMP_TH(T, k, th)                                                               \
+  do {                                                                                    \
+    if ((T) && threadIdx.x == (th) && blockIdx.x < (unsigned)kTimBlocks)                  \
+      (T)[blockIdx.x * kTimSlots + (k)] = __builtin_amdgcn_s_memtime();                   \
+  } while (0)
+#define TSTAMP_RT_TH(T, k, th)                                                            \
+  do {                                                                                    \
+    if ((T) && threadIdx.x == (th) && blockIdx.x < (unsigned)kTimBlocks)                  \
+      (T)[blockIdx.x * kTimSlots + (k)] = __builtin_amdgcn_s_memrealtime();               \
+  } while (0)
 #else
 #define TSTAMP(T, k) ((void)0)
 #define TSTAMP_RT(T, k) ((void)0)
+#define TSTAMP_TH(T, k, th) ((void)0)
+#define TSTAMP_RT_TH(T, k, th) ((void)0)
 #endif
 
 // Phase ablation (debug builds only, `make abl`: -DUNET_TIMING -DUNET_ABL=n):

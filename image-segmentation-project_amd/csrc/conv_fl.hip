@@ -20,12 +20,17 @@
 //    (pixel, 8 channels): operand loads and stores are 16 B per lane, 8 lanes per
 //    128-B line.
 // One 512-thread block per CU (158 KB LDS): a 16 x 16 pixel x 64 channel output
-// tile, 8 waves x (2 rows x 4 channel fragments); per 32-channel sub-stage
-// 72 v_mfma_f32_16x16x32_bf16 per wave (2304 MFMA cycles per SIMD) against
-// ~58 KB of whole-line DMA (~1.1k cycles at 54 B/clk/CU).  The grid is
-// persistent (one block per CU): the next tile's first super-chunk and weights
-// stage under this tile's last sub-stage and epilogue; BN sums are kept per
-// thread across tiles and committed once.
+// tile per work item; 4 compute waves (4 rows x 4 channel fragments each: per
+// 32-channel sub-stage 144 v_mfma_f32_16x16x32_bf16 per wave, 2304 MFMA cycles)
+// and 4 loader waves that issue all LDS-DMA (~58 KB of whole lines per
+// sub-stage, ~1.1k cycles at 54 B/clk/CU) and own the epilogue.  The grid is
+// persistent (one block per CU, a multiple of the output-channel blocks): the
+// next item's first super-chunk and weights stage under this item's last
+// sub-stage, its epilogue runs beside the next item's first sub-stage; BN sums
+// are kept per thread across items and committed once.  Epilogue flags
+// (bias / fold / addend / fused BN backward / statistics) are a template
+// argument for the training-step combinations (EP_*), so the epilogue has no
+// per-item branches and reads its per-channel constants once.
 //
 // LDS: H0 | W0 | W1 | H1 | constants.  Sub-stage t of a tile reads panel t & 1
 // of halo H[(t >> 1) & 1] and weights W[t & 1]; C / 64 is even, so every tile
@@ -87,28 +92,35 @@ __device__ __forceinline__ void barrier_lds() {  // this wave's LDS reads/writes
 
 }  // namespace
 
+// Epilogue flags (a template argument, so the epilogue of the hot variants has
+// no per-item branches): EP_RT = read them from the arguments instead
+constexpr int EP_FOLD = 1, EP_ADD = 2, EP_FBWD = 4, EP_STATS = 8, EP_RELU = 16, EP_RT = 32;
+
+__device__ __forceinline__ void fl_ld8(const float* p, float (&d)[8]) {
+  const f32x4 x0 = *reinterpret_cast<const f32x4*>(p), x1 = *reinterpret_cast<const f32x4*>(p + 4);
+  d[0] = x0[0]; d[1] = x0[1]; d[2] = x0[2]; d[3] = x0[3]; d[4] = x1[0]; d[5] = x1[1]; d[6] = x1[2]; d[7] = x1[3];
+}
+
 // One epilogue item: 8 channels q8 .. q8 + 7 of pixel slot px (transpose
 // buffer T) / global pixel pix -- bias or eval fold, addend, ReLU mask of the
 // fused BN backward, bf16 store, BN sums (register accumulators s0 / s1 / s2)
 template <bool FLIP, bool TWO>
-__device__ __forceinline__ void fl_item(const ConvFwdArgs& a, const char* T, const float* cst, int q8, int px,
+__device__ __forceinline__ void fl_item(const ConvFwdArgs& a, const char* T, const float* cst, const float (&kb)[8],
+                                        const float (&km)[8], const float (&mu)[8], const float (&is)[8], int q8, int px,
                                         int pix, int cob, bool fold, bool want_add, bool fbwd, bool stats,
-                                        const uint4& uadd, const uint4& uact, const uint4& uy, const uint4& uy2,
-                                        float (&s0)[8], float (&s1)[8], float (&s2)[8]) {
+                                        bool relu, const uint4& uadd, const uint4& uact, const uint4& uy,
+                                        const uint4& uy2, float (&s0)[8], float (&s1)[8], float (&s2)[8]) {
   const f32x4 lo = *reinterpret_cast<const f32x4*>(T + tp_off(px, 2 * (q8 >> 3)));
   const f32x4 hi = *reinterpret_cast<const f32x4*>(T + tp_off(px, 2 * (q8 >> 3) + 1));
   float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  const f32x4 b0 = *reinterpret_cast<const f32x4*>(cst + q8), b1 = *reinterpret_cast<const f32x4*>(cst + q8 + 4);
-  const float kb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+  float kb_[8];  // TWO: per item from LDS (registers)
+  if (TWO) fl_ld8(cst + q8, kb_);
   if (fold) {
-    const f32x4 m0 = *reinterpret_cast<const f32x4*>(cst + kCOT + q8);
-    const f32x4 m1 = *reinterpret_cast<const f32x4*>(cst + kCOT + q8 + 4);
-    const float km[8] = {m0[0], m0[1], m0[2], m0[3], m1[0], m1[1], m1[2], m1[3]};
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = v[e] * km[e] + kb[e];
   } else {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] += kb[e];
+    for (int e = 0; e < 8; ++e) v[e] += TWO ? kb_[e] : kb[e];
   }
   if (want_add) {
     float ad[8];
@@ -116,7 +128,7 @@ __device__ __forceinline__ void fl_item(const ConvFwdArgs& a, const char* T, con
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] += ad[e];
   }
-  if (!FLIP && a.fold_relu) {
+  if (!FLIP && relu) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
   }
@@ -133,16 +145,15 @@ __device__ __forceinline__ void fl_item(const ConvFwdArgs& a, const char* T, con
     float dz[8], yv[8];
     unpack8(ob, dz);
     unpack8(uy, yv);
-    const f32x4 mu0 = *reinterpret_cast<const f32x4*>(cst + kCOT + q8);
-    const f32x4 mu1 = *reinterpret_cast<const f32x4*>(cst + kCOT + q8 + 4);
-    const f32x4 is0 = *reinterpret_cast<const f32x4*>(cst + 2 * kCOT + q8);
-    const f32x4 is1 = *reinterpret_cast<const f32x4*>(cst + 2 * kCOT + q8 + 4);
-    const float mu[8] = {mu0[0], mu0[1], mu0[2], mu0[3], mu1[0], mu1[1], mu1[2], mu1[3]};
-    const float is[8] = {is0[0], is0[1], is0[2], is0[3], is1[0], is1[1], is1[2], is1[3]};
+    float mu_[8], is_[8];  // TWO: per item from LDS (registers)
+    if (TWO) {
+      fl_ld8(cst + kCOT + q8, mu_);
+      fl_ld8(cst + 2 * kCOT + q8, is_);
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       s0[e] += dz[e];
-      s1[e] += dz[e] * (yv[e] - mu[e]) * is[e];
+      s1[e] += dz[e] * (yv[e] - (TWO ? mu_[e] : mu[e])) * (TWO ? is_[e] : is[e]);
     }
     if constexpr (TWO) {
       float y2[8];
@@ -172,11 +183,11 @@ __device__ __forceinline__ void fl_item(const ConvFwdArgs& a, const char* T, con
 // B_s; after F they write their accumulators to the transpose buffer T (W1 |
 // H1) and go on to the next item's B_0.  Loader waves: before B_s they wait
 // for sub-stage s's DMA and after it issue the next one; they own the whole
-// epilogue: its operands are fetched at B_{NSUB-1} (before the next item's
-// DMA, so the in-order waits stay exact), and the epilogue of item i runs right
+// epilogue: its operands are fetched at B_{NSUB-1} (after the next item's
+// DMA, which B_0 then waits for alone), and the epilogue of item i runs right
 // after the next item's B_0 -- beside that item's first sub-stage, which reads
 // only W0 / H0 -- or after Z; only then do they refill W1 / H1 (= T).
-template <bool FLIP, bool TWO>
+template <bool FLIP, bool TWO, int EP>
 __global__ void __launch_bounds__(kNW * 64) conv3x3_fl_kernel(ConvFwdArgs a, int ncb, int nitems) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* cst = reinterpret_cast<float*>(smem + kOffCst);
@@ -189,9 +200,12 @@ __global__ void __launch_bounds__(kNW * 64) conv3x3_fl_kernel(ConvFwdArgs a, int
   if (item >= nitems) return;
   const int tq = a.Q >> 4, tp = a.P / kTH;
   const int NSUB = a.C >> 5;  // 32-channel sub-stages per item (even)
-  const bool fbwd = FLIP && a.bb.sums != nullptr;
-  const bool stats = a.stats != nullptr || fbwd;
-  const bool fold = !FLIP && a.fold_on;
+  constexpr bool RT = EP & EP_RT;
+  const bool fbwd = RT ? FLIP && a.bb.sums != nullptr : (EP & EP_FBWD) != 0;
+  const bool stats = RT ? a.stats != nullptr || fbwd : (EP & EP_STATS) != 0;
+  const bool fold = RT ? !FLIP && a.fold_on : (EP & EP_FOLD) != 0;
+  const bool want_add = RT ? a.add != nullptr : (EP & EP_ADD) != 0;
+  const bool relu = RT ? a.fold_relu != 0 : (EP & EP_RELU) != 0;
   const int cob = item % ncb;  // fixed per block: gridDim % ncb == 0 (launcher)
 
   if (wave < kNC) {
@@ -306,9 +320,12 @@ __global__ void __launch_bounds__(kNW * 64) conv3x3_fl_kernel(ConvFwdArgs a, int
     for (int k = 0; k < kHPer; ++k)
       if (k < nh) glds16_asm(xr, dst + (lw + k * kNL) * 1024, hoff[k], so);
   };
+  constexpr int LT = kNC * 64;  // the loader thread that stamps (timing build)
   set_hoff(item);
+  TSTAMP_TH(a.tim, 23, LT);
   issue_w(0, 0);
   issue_h(0, 0);
+  TSTAMP_TH(a.tim, 24, LT);
   if (lt < kCOT) {  // per-channel epilogue constants of the block's output channels
     const int c = lt, co = cob * kCOT + c;
     float b = a.bias ? a.bias[co] : 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f, c4 = 0.f;
@@ -335,29 +352,81 @@ __global__ void __launch_bounds__(kNW * 64) conv3x3_fl_kernel(ConvFwdArgs a, int
     const int j = (lane >> 3) + 8 * k;
     return 16 * (j >> 2) + 4 * lw + (j & 3);
   };
-  const bool want_add = a.add != nullptr;
   float s0[8], s1[8], s2[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) s0[e] = s1[e] = s2[e] = 0.f;
   constexpr int NI = 2 * kItems;  // 8 items per loader thread
-  int pix[NI];                    // the pending epilogue's pixels (N * P * Q < 2^31: launcher)
-  uint4 opa[NI], opm[NI], opy[NI], opy2[TWO ? NI : 1];
-  // the epilogue of the item whose accumulators are in T (its operands fetched)
+  // items whose operands are prefetched at B_{NSUB-1}: all but for the
+  // dgrad without addend, where half (the rest issued by the epilogue itself)
+  // keeps the loader in registers (measured, profiles/r05/s2 conv_timing*)
+  constexpr int NP = (!RT && FLIP && !TWO && (EP & EP_FBWD) && !(EP & EP_ADD)) ? NI / 2 : NI;
+  int ep_pix0 = 0;                 // the pending epilogue's tile origin pixel (N * P * Q < 2^31: launcher)
+  auto pix_of = [&](int k) {
+    const int px = px_of(k);
+    return ep_pix0 + (px >> 4) * a.Q + (px & 15);
+  };
+  // operands of item k (k >= NP: issued by the epilogue itself, where nothing
+  // else is in flight, so the compiler's own waits are exact)
+  auto load_ops = [&](int k, uint4& oa, uint4& om, uint4& oy, uint4& oy2) {
+    const size_t pp = (size_t)pix_of(k);
+    const int co = cob * kCOT + q8;
+    oa = want_add ? *reinterpret_cast<const uint4*>(a.add + pp * a.ldadd + co) : make_uint4(0, 0, 0, 0);
+    om = fbwd ? *reinterpret_cast<const uint4*>(a.bb.act + pp * a.bb.ldact + co) : make_uint4(0, 0, 0, 0);
+    oy = fbwd ? *reinterpret_cast<const uint4*>(a.bb.y + pp * a.bb.ldy + co) : make_uint4(0, 0, 0, 0);
+    if constexpr (TWO) oy2 = fbwd ? *reinterpret_cast<const uint4*>(a.bb.y2 + pp * a.bb.ldy2 + co) : make_uint4(0, 0, 0, 0);
+  };
+  uint4 opa[NP], opm[NP], opy[NP], opy2[TWO ? NP : 1];
+  // the epilogue of the item whose accumulators are in T (items < NP: operands
+  // prefetched)
   auto epilogue = [&]() {
+    constexpr int NL = NI - NP > 0 ? NI - NP : 1;
+    uint4 la[NL], lm[NL], ly[NL], ly2[TWO ? NL : 1];
+#pragma unroll
+    for (int k = NP; k < NI; ++k) load_ops(k, la[k - NP], lm[k - NP], ly[k - NP], ly2[TWO ? k - NP : 0]);
+    // the thread's channel constants, once per epilogue
+    float kb[8], km[8], mu[8], is[8];
+    if (!TWO) fl_ld8(cst + q8, kb);
+    if (fold) fl_ld8(cst + kCOT + q8, km);
+    if (fbwd && !TWO) {
+      fl_ld8(cst + kCOT + q8, mu);
+      fl_ld8(cst + 2 * kCOT + q8, is);
+    }
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
-      fl_item<FLIP, TWO>(a, smem + kOffW1, cst, q8, px_of(k), pix[k], cob, fold, want_add, fbwd, stats,
-                         opa[k], opm[k], opy[k], opy2[TWO ? k : 0], s0, s1, s2);
+      const bool pre = k < NP;
+      const int j = pre ? k : k - NP;
+      fl_item<FLIP, TWO>(a, smem + kOffW1, cst, kb, km, mu, is, q8, px_of(k), pix_of(k), cob, fold, want_add, fbwd,
+                         stats, relu, pre ? opa[j] : la[j], pre ? opm[j] : lm[j], pre ? opy[j] : ly[j],
+                         TWO ? (pre ? opy2[j] : ly2[j]) : opy2[0], s0, s1, s2);
       asm volatile("" ::: "memory");  // one item at a time: bounded registers
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's T rows are read before its DMA refills them
   };
+  // prefetched epilogue operand loads per thread: with the half prefetch they
+  // are issued AFTER the next item's first-stage DMA, so that B_0 waits for
+  // that DMA alone (vmcnt <= NOPS); with the full prefetch (more registers,
+  // spills whose reloads wait for vmcnt(0) anyway) before it, and B_0 waits for
+  // everything (measured both ways per variant, profiles/r05/s2 conv_timing*)
+  constexpr int NOPS = (RT || NP == NI) ? -1 : NP * (((EP & EP_ADD) ? 1 : 0) + ((EP & EP_FBWD) ? (TWO ? 3 : 2) : 0));
+  auto fetch_operands = [&]() {
+#pragma unroll
+    for (int k = 0; k < NP; ++k) load_ops(k, opa[k], opm[k], opy[k], opy2[TWO ? k : 0]);
+  };
   bool pending = false;  // an epilogue waits for the next B_0 / Z
+  int nit = 0;             // items done (timing stamps of the first two)
   for (;;) {
     const int next = item + gridDim.x;
-    // s = 0 (peeled): everything landed; then the previous item's epilogue,
-    // beside this item's first sub-stage; then the refill of W1 / H1 (= T)
-    wait_vmcnt<0>();
+    // s = 0 (peeled): this sub-stage's DMA landed (the previous item's
+    // epilogue operands may still be in flight); then that epilogue, beside
+    // this item's first sub-stage; then the refill of W1 / H1 (= T)
+    if constexpr (NOPS > 0) {
+      if (pending) wait_vmcnt<(NOPS > 0 ? NOPS : 0)>();
+      else wait_vmcnt<0>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    if (nit == 0) TSTAMP_TH(a.tim, 25, LT);
+    if (nit == 1) TSTAMP_TH(a.tim, 27, LT);
     __builtin_amdgcn_s_barrier();  // B_0
     if (pending) epilogue();
     if (UNET_ABL != 2) {
@@ -383,27 +452,17 @@ __global__ void __launch_bounds__(kNW * 64) conv3x3_fl_kernel(ConvFwdArgs a, int
       const int t = item / ncb;
       const int n = t / (tp * tq), rem = t - n * (tp * tq);
       const int oh0 = (rem / tq) * kTH, ow0 = (rem % tq) << 4;
-#pragma unroll
-      for (int k = 0; k < NI; ++k) {
-        const int px = px_of(k);
-        pix[k] = (n * a.P + oh0 + (px >> 4)) * a.Q + ow0 + (px & 15);
-      }
+      ep_pix0 = (n * a.P + oh0) * a.Q + ow0;
     }
-#pragma unroll
-    for (int k = 0; k < NI; ++k) {
-      const size_t pp = (size_t)pix[k];
-      const int co = cob * kCOT + q8;
-      opa[k] = want_add ? *reinterpret_cast<const uint4*>(a.add + pp * a.ldadd + co) : make_uint4(0, 0, 0, 0);
-      opm[k] = fbwd ? *reinterpret_cast<const uint4*>(a.bb.act + pp * a.bb.ldact + co) : make_uint4(0, 0, 0, 0);
-      opy[k] = fbwd ? *reinterpret_cast<const uint4*>(a.bb.y + pp * a.bb.ldy + co) : make_uint4(0, 0, 0, 0);
-      if constexpr (TWO)
-        opy2[k] = fbwd ? *reinterpret_cast<const uint4*>(a.bb.y2 + pp * a.bb.ldy2 + co) : make_uint4(0, 0, 0, 0);
-    }
+    if constexpr (NOPS < 0) fetch_operands();
+    if (nit == 0) TSTAMP_TH(a.tim, 26, LT);
+    ++nit;
     if (next < nitems) {
       set_hoff(next);
       issue_w(0, 0);
       issue_h(0, 0);
     }
+    if constexpr (NOPS >= 0) fetch_operands();
     __builtin_amdgcn_s_barrier();  // F
     pending = true;
     item = next;
@@ -411,9 +470,13 @@ __global__ void __launch_bounds__(kNW * 64) conv3x3_fl_kernel(ConvFwdArgs a, int
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();  // Z: T holds the last item
+  TSTAMP_TH(a.tim, 28, LT);
   epilogue();
-  TSTAMP(a.tim, 21);
-  if (!stats) return;
+  TSTAMP_TH(a.tim, 21, LT);
+  if (!stats) {
+    TSTAMP_RT_TH(a.tim, 31, LT);
+    return;
+  }
   // ---- BN sums: [32 pixel slots][64 channels][3] in H0 (no DMA in flight any
   // more), summed over the slots in a fixed order (4 independent partial sums),
   // fp64 atomics into replica blockIdx % kStatRep ----
@@ -448,8 +511,8 @@ __global__ void __launch_bounds__(kNW * 64) conv3x3_fl_kernel(ConvFwdArgs a, int
       else bn_finalize(a.bn);
     }
   }
-  TSTAMP(a.tim, 22);
-  TSTAMP_RT(a.tim, 31);
+  TSTAMP_TH(a.tim, 22, LT);
+  TSTAMP_RT_TH(a.tim, 31, LT);
 }
 
 static int g_cus = 0;
@@ -493,15 +556,36 @@ hipError_t launch_conv3x3_fl(const ConvFwdArgs& a, int mode, hipStream_t st) {
   if (grid < ncb) grid = ncb;
   if (grid > nitems) grid = nitems;
   const bool two = flip && a.bb.sums && a.bb.y2;
+  const bool fbwd = flip && a.bb.sums;
+  const int ep = (!flip && a.fold_on ? EP_FOLD : 0) | (a.add ? EP_ADD : 0) | (fbwd ? EP_FBWD : 0) |
+                 (a.stats || fbwd ? EP_STATS : 0) | (!flip && a.fold_relu ? EP_RELU : 0);
+  // the training-step epilogues as their own instances, anything else reads
+  // its flags at run time
+  int sel = EP_RT;
+  if (!flip && (ep == EP_STATS || ep == 0)) sel = ep;
+  if (flip && !two && (ep == 0 || ep == EP_ADD || ep == (EP_FBWD | EP_STATS) || ep == (EP_FBWD | EP_STATS | EP_ADD)))
+    sel = ep;
+  // (two: the run-time instance -- the specialised ones spill heavily)
   char tag[96];
-  std::snprintf(tag, sizeof(tag), "conv3x3_fl_kernel<%s, %s>", flip ? "true" : "false", two ? "true" : "false");
+  std::snprintf(tag, sizeof(tag), "conv3x3_fl_kernel<%s, %s, %d>", flip ? "true" : "false", two ? "true" : "false",
+                sel);
   conv_kernel_tag(tag);
-  if (!flip)
-    hipLaunchKernelGGL((conv3x3_fl_kernel<false, false>), dim3(grid), dim3(kNW * 64), kLds, st, a, ncb, nitems);
-  else if (two)
-    hipLaunchKernelGGL((conv3x3_fl_kernel<true, true>), dim3(grid), dim3(kNW * 64), kLds, st, a, ncb, nitems);
-  else
-    hipLaunchKernelGGL((conv3x3_fl_kernel<true, false>), dim3(grid), dim3(kNW * 64), kLds, st, a, ncb, nitems);
+  const dim3 g(grid), b(kNW * 64);
+#define FL_LAUNCH(F, T, E) hipLaunchKernelGGL((conv3x3_fl_kernel<F, T, E>), g, b, kLds, st, a, ncb, nitems)
+  if (!flip) {
+    if (sel == EP_STATS) FL_LAUNCH(false, false, EP_STATS);
+    else if (sel == 0) FL_LAUNCH(false, false, 0);
+    else FL_LAUNCH(false, false, EP_RT);
+  } else if (two) {
+    FL_LAUNCH(true, true, EP_RT);
+  } else {
+    if (sel == (EP_FBWD | EP_STATS)) FL_LAUNCH(true, false, EP_FBWD | EP_STATS);
+    else if (sel == (EP_FBWD | EP_STATS | EP_ADD)) FL_LAUNCH(true, false, EP_FBWD | EP_STATS | EP_ADD);
+    else if (sel == EP_ADD) FL_LAUNCH(true, false, EP_ADD);
+    else if (sel == 0) FL_LAUNCH(true, false, 0);
+    else FL_LAUNCH(true, false, EP_RT);
+  }
+#undef FL_LAUNCH
   return hipGetLastError();
 }
 

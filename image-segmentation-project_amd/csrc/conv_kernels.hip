@@ -1783,8 +1783,13 @@ __device__ __forceinline__ int wb_block_of(const WgBatchArgs& a, long long it) {
 
 // dW of every unit spread over several blocks = the sum of its partials in
 // block order; grid (units, 36): 256 threads x one f32x4 element of the unit's
-// 9216-element (8 waves x 18 fragments x 64 lanes) SLAB_HALO partial each
+// 9216-element (8 waves x 18 fragments x 64 lanes) SLAB_HALO partial each.
+// The unit's slab slots (one per block it spans, <= grid <= 256) are located
+// once per block, one thread per spanned block, into LDS; every thread then
+// streams its element of those partials with 8 loads in flight and adds them
+// in block order (the order, hence the bits, of a serial loop)
 __global__ void __launch_bounds__(256) wgrad_batch_reduce_kernel(WgBatchArgs a) {
+  __shared__ int slots[256];
   const int u = blockIdx.x;
   int l = 0;
   while (l + 1 < a.nl && u >= a.L[l + 1].unit0) ++l;
@@ -1793,16 +1798,33 @@ __global__ void __launch_bounds__(256) wgrad_batch_reduce_kernel(WgBatchArgs a) 
   const long long S = L.item0 + (long long)combo * L.tiles;
   const int b0 = wb_block_of(a, S), b1 = wb_block_of(a, S + L.tiles - 1);
   if (b0 == b1) return;  // written directly by its block
-  const int q = blockIdx.y * 256 + threadIdx.x;
-  const f32x4* slab = reinterpret_cast<const f32x4*>(a.slab);
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int b = b0; b <= b1; ++b) {
+  const int nb = b1 - b0 + 1;
+  if ((int)threadIdx.x < nb) {
+    const int b = b0 + threadIdx.x;
     const long long ib = wb_begin(a, b);
-    if (wb_begin(a, b + 1) == ib) continue;  // an empty range (batches of fewer items than blocks)
-    WbPos p;
-    p.locate(a, ib);
-    const int slot = b * a.maxseg + (u - (a.L[p.l].unit0 + p.combo));
-    acc += slab[(size_t)slot * (kWlNW * 18 * 64) + q];
+    int slot = -1;  // -1: an empty range (batches of fewer items than blocks)
+    if (wb_begin(a, b + 1) != ib) {
+      WbPos p;
+      p.locate(a, ib);
+      slot = b * a.maxseg + (u - (a.L[p.l].unit0 + p.combo));
+    }
+    slots[threadIdx.x] = slot;
+  }
+  __syncthreads();
+  const int q = blockIdx.y * 256 + threadIdx.x;
+  const f32x4* slab = reinterpret_cast<const f32x4*>(a.slab) + q;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int j0 = 0; j0 < nb; j0 += 8) {
+    f32x4 v[8];
+    int sl[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sl[k] = j0 + k < nb ? slots[j0 + k] : -1;
+      if (sl[k] >= 0) v[k] = slab[(size_t)sl[k] * (kWlNW * 18 * 64)];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (sl[k] >= 0) acc += v[k];
   }
   const int lane = q & 63, r = q >> 6;
   const int frag = r % 18, wave = r / 18;

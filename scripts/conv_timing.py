@@ -84,6 +84,13 @@ for i in range(n):
         parts.append(f"epi {np.median(t[:, 21] - t[:, 20]):.0f}")
     if (t[:, 22] > 0).any():
         parts.append(f"stats {np.median(t[:, 22] - t[:, 21]):.0f}")
+    if (t[:, 23] > 0).mean() > 0.5:  # loader-wave stamps (conv3x3_fl_kernel)
+        ld = lambda k, j: np.median(t[:, k] - t[:, j])
+        parts.append(f"ld: issue0 {ld(24, 23):.0f} land0 {ld(25, 24):.0f}")
+        if (t[:, 27] > 0).mean() > 0.5:
+            parts.append(f"land1 {ld(27, 26):.0f}")
+        if (t[:, 28] > 0).mean() > 0.5:
+            parts.append(f"Z->epi-end {ld(21, 28):.0f}")
     start_spread = (rt0.max() - rt0.min()) / 100.0
     print(f"{nm:34s} blk {nb:4d} span {span:6.1f}us blk-dur {dur_rt:5.1f}us start-spread {start_spread:4.1f}us "
           f"clk {clk:4.2f}GHz | " + " | ".join(parts), flush=True)

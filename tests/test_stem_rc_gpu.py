@@ -75,3 +75,96 @@ def test_stem_recompute_matches_stored_path(pkg, cuda, shape):
     assert torch.equal(o2, o_rc)
     for k in g_rc:
         assert torch.equal(g2[k], g_rc[k]), k
+
+
+def _bn_train(v, g, b, stats_from=None):
+    s = v if stats_from is None else stats_from
+    mean = s.mean((0, 2, 3), keepdim=True)
+    var = s.var((0, 2, 3), unbiased=False, keepdim=True)
+    return (v - mean) / torch.sqrt(var + 1e-5) * g.view(1, -1, 1, 1) + b.view(1, -1, 1, 1)
+
+
+def _dskip(v):
+    """the decoder1 concat gradient's skip slice (the stem output x1's second consumer)"""
+    if "dec1.d.cat" in v:
+        return v["dec1.d.cat"][:, :v["x1"].shape[1]]
+    return v["dec1.d.cat.skip"][:, :v["x1"].shape[1]]
+
+
+# measured on MI355X (profiles/r05/s2/stem_tests.txt), 2 x 256^2 | 1 x 64 x 96:
+#   bf16-y0 reference: x1 1.7e-3 | 1.7e-3, p0 1.7e-3 | 1.6e-3, input_conv.weight
+#     1.0e-2 | 1.4e-2, bn1.weight 1.1e-3 | 2.1e-3, bn1.bias 2.4e-3 | 3.1e-3
+#   pure fp32 reference: x1 4.8e-3 | 3.8e-3, p0 3.8e-3 | 3.2e-3,
+#     input_conv.weight 3.8e-2 | 6.8e-2, bn1.bias 2.4e-2 | 4.3e-2 (the weight and
+#     bias gradients are small residuals of the BN backward's cancelling terms)
+#   fp64 recomputation from the stored dZ: input_conv.weight 5.8e-4
+X1_TOL, W_TOL = 3e-3, 3e-2            # bf16-y0 reference
+X1_TOL_FP32, W_TOL_FP32 = 8e-3, 1e-1  # pure fp32 reference
+W64_TOL = 2e-3
+
+
+@pytest.mark.parametrize("shape", [(2, 256, 256), (1, 64, 96)], ids=["2x256", "1x64x96"])
+def test_stem_production_path_vs_fp32(pkg, cuda, shape):
+    """The production stem (recompute, nothing but x1 / p0 stored) against a
+    torch restatement of advanced_models.py:76,81-83 on the same bf16 input and
+    weights: forward x1 = relu(bn(conv(xq))) and p0 = maxpool(x1); backward:
+    the stem parameter gradients by autograd through that chain, fed the
+    executor's own upstream gradients (d.p0 into the pool, the decoder1
+    concat's skip slice into x1).  Two references: y0 rounded to bf16 before
+    the BN, where the kernels round it (stem_rc.hip: act = bf16(relu(y sc +
+    sh)) of a bf16 y, as the stored path) -- tight bars -- and the pure fp32
+    chain of the reference model -- bars that hold the rounding's own effect."""
+    ref = oracle.ReferenceUNet()
+    sd = oracle.closed_form_state_dict(ref, seed=5)
+    xs, ms = pkg.synthetic_cells(*shape, seed=13)
+    x, y = torch.from_numpy(xs).cuda(), torch.from_numpy(ms).cuda()
+    assert os.environ.get("UNET_STEM_KEEP") is None and os.environ.get("UNET_STEM_RC") is None
+    _, v, g = _run(pkg, sd, x, y, {})
+    assert "y0" not in v, "production stem path expected (no stored y0)"
+    xq = x.cpu().to(torch.bfloat16).float()
+    for rnd, xtol, wtol in ((True, X1_TOL, W_TOL), (False, X1_TOL_FP32, W_TOL_FP32)):
+        w = sd["input_conv.weight"].to(torch.bfloat16).float().requires_grad_(True)
+        gam = sd["bn1.weight"].float().clone().requires_grad_(True)
+        bet = sd["bn1.bias"].float().clone().requires_grad_(True)
+        y0 = torch.nn.functional.conv2d(xq, w, stride=2, padding=3)
+        yq = y0
+        if rnd:  # the batch statistics from the fp32 y (the statistics pass), the
+            # normalisation applied to the bf16-rounded y (straight-through gradient)
+            yq = y0 + (y0.detach().to(torch.bfloat16).float() - y0.detach())
+        x1 = torch.relu(_bn_train(yq, gam, bet, stats_from=y0))
+        p0 = torch.nn.functional.max_pool2d(x1, 3, 2, 1)
+        ex1, ep0 = _rel(v["x1"], x1.detach()), _rel(v["p0"], p0.detach())
+        gw, gg, gb = torch.autograd.grad([p0, x1], [w, gam, bet], [v["d.p0"].float(), _dskip(v).float()])
+        rows = [("input_conv.weight", _rel(g["input_conv.weight"], gw)), ("bn1.weight", _rel(g["bn1.weight"], gg)),
+                ("bn1.bias", _rel(g["bn1.bias"], gb))]
+        print(f"{'bf16-y0' if rnd else 'fp32'} reference: x1 rel {ex1:.2e}  p0 rel {ep0:.2e}  " +
+              "  ".join(f"{k} {e:.2e}" for k, e in rows))
+        assert ex1 <= xtol and ep0 <= xtol, (rnd, ex1, ep0)
+        for k, e in rows:
+            assert e <= wtol, (rnd, k, e)
+
+
+def test_stem_weight_gradient_vs_fp64(pkg, cuda):
+    """The recompute path's stem weight gradient, formed through the
+    BN-backward identity dW = k1 (dZ^T im - m1 sum im - m2 xhat^T im), against
+    an fp64 recomputation from the same stored dZ and y0 (UNET_STEM_KEEP=1:
+    the kernel reads exactly these): dY = BN-backward(dZ) in fp64, then
+    conv2d_weight(xq, dY) in fp64."""
+    ref = oracle.ReferenceUNet()
+    sd = oracle.closed_form_state_dict(ref, seed=5)
+    xs, ms = pkg.synthetic_cells(2, 256, 256, seed=13)
+    x, y = torch.from_numpy(xs).cuda(), torch.from_numpy(ms).cuda()
+    _, v, g = _run(pkg, sd, x, y, {"UNET_STEM_KEEP": "1"})
+    y0 = v["y0"].double()
+    dz = v["d.x1"].double() * (v["x1"] > 0).double()
+    n = y0.shape[0] * y0.shape[2] * y0.shape[3]
+    mu = y0.mean((0, 2, 3), keepdim=True)
+    inv = 1.0 / torch.sqrt(y0.var((0, 2, 3), unbiased=False, keepdim=True) + 1e-5)
+    xhat = (y0 - mu) * inv
+    k1 = sd["bn1.weight"].double().view(1, -1, 1, 1) * inv
+    dy = k1 * (dz - dz.sum((0, 2, 3), keepdim=True) / n - xhat * (dz * xhat).sum((0, 2, 3), keepdim=True) / n)
+    xq = x.cpu().to(torch.bfloat16).double()
+    dw = torch.nn.grad.conv2d_weight(xq, sd["input_conv.weight"].shape, dy, stride=2, padding=3)
+    e = _rel(g["input_conv.weight"], dw)
+    print(f"input_conv.weight vs fp64 from stored dZ: rel {e:.2e}")
+    assert e <= W64_TOL
