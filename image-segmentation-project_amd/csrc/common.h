@@ -131,6 +131,22 @@ __device__ __forceinline__ void glds16_asm(const i32x4& r, char* lds_wave_base, 
       : "memory");
 }
 
+// the same with the LDS destination as a byte address (lds_addr(smem) + an
+// integer offset): no generic-pointer round trip, whose folded form
+// (readfirstlane of a flat pointer cast back to LDS) hit an instruction-selection
+// error in conv3x3_ws2_kernel
+__device__ __forceinline__ unsigned lds_addr(const char* p) { return (unsigned)(size_t)LDS_PTR(const char, p); }
+__device__ __forceinline__ void glds16_asm_at(const i32x4& r, unsigned lds_byte, unsigned voff, unsigned soff) {
+  const unsigned lds = __builtin_amdgcn_readfirstlane(lds_byte);
+  const unsigned so = __builtin_amdgcn_readfirstlane(soff);
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(r), "s"(lds), "s"(so)
+      : "memory");
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -589,4 +589,422 @@ hipError_t launch_conv3x3_fl(const ConvFwdArgs& a, int mode, hipStream_t st) {
   return hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------------------
+// Weight-stationary full-line conv for C == 64 (enc1 and decoder2.3 at Base,
+// SURVEY.md §8(a) rows a3 / a6): the same roles as conv3x3_fl_kernel, with the
+// block's 9 x 64 x 64 weights loaded ONCE (the conv3x3_ws_kernel layout: one
+// 128-B fl_off row per (tap, output channel), from the standard pack) and only
+// the 16 x 16 tiles' halos streamed, double-buffered.  The weight-stationary
+// kernel before it ran MFMA, epilogue, halo issue and barrier one after the
+// other in every wave (profiles/r05/s2 conv_timing_abl3: 4.2k MFMA cycles of a
+// 10.9k-cycle tile); here the loader waves stage the next halo and write the
+// previous tile's outputs while the compute waves run the current tile's MFMAs.
+//
+// Per tile: compute waves (4 rows x 4 channel fragments each, 288 MFMAs) add
+// the bias (forward: BN sums from the fp32 values, in registers) or the
+// addend (data gradient, loaded by the compute wave itself), round to bf16
+// and write the 256 x 64 bf16 tile T into the halo buffer they just consumed;
+// the loader waves then store T as whole lines (data gradient with fused BN
+// backward: ReLU mask and the BN-backward sums there) and refill that buffer
+// with the halo of the tile after next.  Loader wave lw reads only the T rows
+// of the 1-KB stripes its own DMA refills (stripe = px >> 3, (px >> 3) & 3 ==
+// lw), so no cross-wave hazard exists on the refill.
+// LDS: W (73,728) | H0 | H1 (41,984 each) | constants.
+constexpr int kW2Bytes = 9 * kCOT * 128;
+constexpr int k2OffH0 = kW2Bytes, k2OffH1 = k2OffH0 + kHBytes, k2OffCst = k2OffH1 + kHBytes;
+constexpr int k2OffXss = k2OffCst + 3 * kCOT * 4;  // xform: scale | shift of the 64 input channels
+constexpr int k2Lds = k2OffXss + 2 * 64 * 4;
+constexpr int EP_XF = 64;  // ws2 only: the previous BN + ReLU applied to the staged halo (ConvFwdArgs::xform)
+static_assert(k2Lds <= 163840, "LDS");
+static_assert(256 * 128 <= kHBytes, "bf16 tile fits a halo buffer");
+__device__ __forceinline__ int t2_off(int px, int c16) { return px * 128 + ((c16 ^ (px & 7)) << 4); }
+
+template <bool FLIP, int EP>
+__global__ void __launch_bounds__(kNW * 64) conv3x3_ws2_kernel(ConvFwdArgs a, int ncb, int nitems) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* cst = reinterpret_cast<float*>(smem + k2OffCst);  // bias | mean | invstd
+  TSTAMP_RT(a.tim, 30);
+  TSTAMP(a.tim, 0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int slot = xcd_remap(blockIdx.x, gridDim.x);
+  if (slot >= nitems) return;
+  const size_t rep = (size_t)(blockIdx.x % kStatRep) * 2 * a.Cout;  // BN-sum replica of the block
+  const int cob = slot % ncb;  // fixed per block: gridDim % ncb == 0 (launcher)
+  const int tq = a.Q >> 4, tp = a.P / kTH;
+  constexpr bool FBWD = FLIP && (EP & EP_FBWD), ADD = (EP & EP_ADD) != 0, STATS = (EP & EP_STATS) != 0;
+  constexpr bool XF = !FLIP && (EP & EP_XF);
+  float* xss = reinterpret_cast<float*>(smem + k2OffXss);
+  auto tile_pix0 = [&](int it) {  // global pixel of the item's tile origin
+    const int t = it / ncb;
+    const int n = t / (tp * tq), rem = t - n * (tp * tq);
+    return (n * a.P + (rem / tq) * kTH) * a.Q + ((rem % tq) << 4);
+  };
+  const char* Wl = smem;
+
+  if (wave < kNC) {
+    // ================= compute waves =================
+    const int aoff = fl_off(lane & 15, lane >> 4), g = lane >> 4;
+    int boff[kRW + 2][3];
+#pragma unroll
+    for (int h = 0; h < kRW + 2; ++h)
+#pragma unroll
+      for (int d = 0; d < 3; ++d) boff[h][d] = fl_off((wave * kRW + h) * kHW + d + (lane & 15), lane >> 4);
+    float q0[kFN][4], q1[kFN][4];
+#pragma unroll
+    for (int i = 0; i < kFN; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) q0[i][e] = q1[i][e] = 0.f;
+    if constexpr (XF) {
+      if (blockIdx.x == 0) bn_finalize(a.xbn);  // saved mean / invstd, running statistics (wave 0)
+      __builtin_amdgcn_s_barrier();             // X: the loaders' scale / shift table is in LDS
+    }
+    TSTAMP(a.tim, 1);
+    int b = 0, k = 0;
+    for (int it = slot; it < nitems; it += gridDim.x, b ^= 1, ++k) {
+      const int pix0 = tile_pix0(it);
+      __builtin_amdgcn_s_barrier();  // B: this tile's halo landed (the loaders waited)
+      asm volatile("" ::: "memory");
+      if (k < 8) TSTAMP(a.tim, 2 + 2 * k);
+      uint2 uadd[kRW][kFN];
+      if constexpr (ADD) {  // lands under the MFMAs
+#pragma unroll
+        for (int j = 0; j < kRW; ++j) {
+          const int px = (wave * kRW + j) * 16 + (lane & 15);
+          const size_t gp = (size_t)(pix0 + (px >> 4) * a.Q + (px & 15));
+#pragma unroll
+          for (int i = 0; i < kFN; ++i)
+            uadd[j][i] = *reinterpret_cast<const uint2*>(a.add + gp * a.ldadd + cob * kCOT + i * 16 + 4 * g);
+        }
+      }
+      const char* H = smem + k2OffH0 + b * kHBytes;
+      f32x4 acc[kRW][kFN];
+#pragma unroll
+      for (int j = 0; j < kRW; ++j)
+#pragma unroll
+        for (int i = 0; i < kFN; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (UNET_ABL != 1) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+          for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              bf16x8 A[kFN];
+#pragma unroll
+              for (int i = 0; i < kFN; ++i)
+                A[i] = *reinterpret_cast<const bf16x8*>(Wl + (r * 3 + c) * kCOT * 128 + i * 2048 + (aoff ^ (p << 6)));
+              const int dr = FLIP ? 2 - r : r, dc = FLIP ? 2 - c : c;
+#pragma unroll
+              for (int j = 0; j < kRW; ++j) {
+                const bf16x8 B = *reinterpret_cast<const bf16x8*>(H + (boff[j + dr][dc] ^ (p << 6)));
+#pragma unroll
+                for (int i = 0; i < kFN; ++i)
+                  acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B, acc[j][i], 0, 0, 0);
+              }
+            }
+      }
+      if (k < 8) TSTAMP(a.tim, 3 + 2 * k);
+      barrier_lds();  // F: every compute wave is done reading H (it becomes T)
+      char* T = smem + k2OffH0 + b * kHBytes;
+#pragma unroll
+      for (int i = 0; i < kFN; ++i) {
+        float kb[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) kb[e] = cst[i * 16 + 4 * g + e];
+#pragma unroll
+        for (int j = 0; j < kRW; ++j) {
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[j][i][e] + kb[e];
+          if constexpr (ADD) {
+            const float ad[4] = {__uint_as_float(uadd[j][i].x << 16), __uint_as_float(uadd[j][i].x & 0xffff0000u),
+                                 __uint_as_float(uadd[j][i].y << 16), __uint_as_float(uadd[j][i].y & 0xffff0000u)};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += ad[e];
+          }
+          if constexpr (!FLIP && STATS) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { q0[i][e] += v[e]; q1[i][e] += v[e] * v[e]; }
+          }
+          const int px = (wave * kRW + j) * 16 + (lane & 15);
+          *reinterpret_cast<uint2*>(T + t2_off(px, 2 * i + (g >> 1)) + (g & 1) * 8) =
+              make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+        }
+      }
+      barrier_lds();  // E: T written
+    }
+    TSTAMP(a.tim, 20);
+    if constexpr (!FLIP && STATS) {
+      // BN sums: per-lane partials to LDS (the halo buffer the last tile did NOT
+      // use: free), summed in a fixed order by 128 threads
+      float* red = reinterpret_cast<float*>(smem + k2OffH0 + b * kHBytes);  // b: the buffer after the last
+#pragma unroll
+      for (int i = 0; i < kFN; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          red[(wave * 64 + lane) * 32 + i * 4 + e] = q0[i][e];
+          red[(wave * 64 + lane) * 32 + 16 + i * 4 + e] = q1[i][e];
+        }
+    }
+    __builtin_amdgcn_s_barrier();  // R1
+    __builtin_amdgcn_s_barrier();  // R2
+    return;
+  }
+
+  // ================= loader waves: LDS-DMA, the tile stores, BN-backward sums =====
+  const int lw = wave - kNC, lt = tid - kNC * 64;
+  const int nh = (kHIns - lw + kNL - 1) / kNL;  // 11 or 10
+  const i32x4 xr = make_rsrc_sgpr(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
+  const i32x4 wr = make_rsrc_sgpr(a.w, (unsigned)((size_t)a.Cout * 9 * a.C * 2));
+  constexpr int LT = kNC * 64;
+  unsigned hoff[kHPer];
+  auto set_hoff = [&](int it) {
+    const int t = it / ncb;
+    const int n = t / (tp * tq), rem = t - n * (tp * tq);
+    const int oh0 = (rem / tq) * kTH, ow0 = (rem % tq) << 4;
+#pragma unroll
+    for (int k = 0; k < kHPer; ++k) {
+      const int hp = (lw + k * kNL) * 8 + (lane >> 3);
+      const int hr = hp / kHW, hc = hp - hr * kHW;
+      const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
+      const int q = (lane & 7) ^ (hp & 6);
+      hoff[k] = kOOB;
+      if (hp < kHPix && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+        hoff[k] = (unsigned)((((n * a.H + ih) * a.W + iw) * a.ldx + q * 8) * 2);
+    }
+  };
+  const unsigned l0 = lds_addr(smem);
+  auto issue_h = [&](int bb) {
+    const unsigned dst = l0 + k2OffH0 + bb * kHBytes;
+#pragma unroll
+    for (int k = 0; k < kHPer; ++k)
+      if (k < nh) glds16_asm_at(xr, dst + (lw + k * kNL) * 1024, hoff[k], 0u);
+  };
+  if constexpr (XF) {  // the previous BN's scale / shift, before any DMA is in flight
+    if (lt < 64) {
+      float m, iv, var;
+      bn_scale_shift(a.xbn, lt, xss[lt], xss[64 + lt], m, iv, var);
+    }
+  }
+  // the weights, once: 72 instructions of 8 (tap, channel) rows x 128 B
+  TSTAMP_TH(a.tim, 23, LT);
+  for (int ins = lw; ins < 9 * kCOT / 8; ins += kNL) {
+    const int row = ins * 8 + (lane >> 3);
+    const int co = row % kCOT, tap = row / kCOT;
+    const int q = (lane & 7) ^ (row & 6);
+    const unsigned off = (unsigned)((((cob * kCOT + co) * 9 + tap) * a.C + q * 8) * 2);
+    glds16_asm_at(wr, l0 + ins * 1024, off, 0u);
+  }
+  int item = slot;
+  set_hoff(item);
+  issue_h(0);
+  TSTAMP_TH(a.tim, 24, LT);
+  if (lt < kCOT) {
+    const int co = cob * kCOT + lt;
+    cst[lt] = a.bias ? a.bias[co] : 0.f;
+    cst[kCOT + lt] = FBWD ? a.bb.mean[co] : 0.f;
+    cst[2 * kCOT + lt] = FBWD ? a.bb.invstd[co] : 0.f;
+  }
+  if constexpr (XF) __builtin_amdgcn_s_barrier();  // X: xss (computed first thing) visible
+  // xform: relu(x * scale + shift) of the halo chunks this lane's own DMA
+  // staged (its wait covers exactly those), in place; conv padding (kOOB, zero
+  // filled) stays 0; the tile interior is the activation h, stored by the
+  // blocks of output-channel block 0 (bn_apply's expression: bit-identical)
+  auto xform_halo = [&](int bb, int it) {
+    char* Hb = smem + k2OffH0 + bb * kHBytes;
+    const int t = it / ncb;
+    const int n = t / (tp * tq), rem = t - n * (tp * tq);
+    const int oh0 = (rem / tq) * kTH, ow0 = (rem % tq) << 4;
+#pragma unroll
+    for (int k = 0; k < kHPer; ++k) {
+      if (k >= nh || hoff[k] == kOOB) continue;
+      const int hp = (lw + k * kNL) * 8 + (lane >> 3);
+      const int c0 = ((lane & 7) ^ (hp & 6)) * 8;
+      uint4* q = reinterpret_cast<uint4*>(Hb + (lw + k * kNL) * 1024 + lane * 16);
+      float v[8];
+      unpack8(*q, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = v[e] * xss[c0 + e] + xss[64 + c0 + e];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+      const uint4 o = pack8(v);
+      *q = o;
+      const int hr = hp / kHW, hc = hp - hr * kHW;
+      if (cob == 0 && hr >= 1 && hr <= kTH && hc >= 1 && hc <= 16 && UNET_ABL != 4)
+        *reinterpret_cast<uint4*>(a.xh + ((size_t)(n * a.H + oh0 - 1 + hr) * a.W + ow0 - 1 + hc) * a.ldxh + c0) = o;
+    }
+  };
+  const int c8 = (lane & 7) * 8;  // this lane's 8 channels of every epilogue item
+  float s0[8], s1[8], mu[8], is[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s0[e] = s1[e] = 0.f;
+  bool have_cst = false;
+  // the epilogue of the tile whose bf16 outputs are in T (buffer tb): item q =
+  // stripe lw + 4 q, pixel 8 stripe + (lane >> 3)
+  // (the fused-backward operands are loaded by the epilogue itself: a
+  // prefetch a tile ahead made hipcc wait for vmcnt(0) -- the next halo's DMA
+  // -- before reusing the store-data registers; measured slower)
+  auto epilogue = [&](int tb, int pix0) {
+    const char* T = smem + k2OffH0 + tb * kHBytes;
+    if (FBWD && !have_cst) {
+      fl_ld8(cst + kCOT + c8, mu);
+      fl_ld8(cst + 2 * kCOT + c8, is);
+      have_cst = true;
+    }
+    uint4 om[8], oy[8];
+    if constexpr (FBWD) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int px = (lw + 4 * q) * 8 + (lane >> 3);
+        const size_t gp = (size_t)(pix0 + (px >> 4) * a.Q + (px & 15));
+        om[q] = *reinterpret_cast<const uint4*>(a.bb.act + gp * a.bb.ldact + cob * kCOT + c8);
+        oy[q] = *reinterpret_cast<const uint4*>(a.bb.y + gp * a.bb.ldy + cob * kCOT + c8);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int px = (lw + 4 * q) * 8 + (lane >> 3);
+      const size_t gp = (size_t)(pix0 + (px >> 4) * a.Q + (px & 15));
+      uint4 o = *reinterpret_cast<const uint4*>(T + t2_off(px, lane & 7));
+      if constexpr (FBWD) {
+        float v[8], m[8], yv[8];
+        unpack8(o, v);
+        unpack8(om[q], m);
+        unpack8(oy[q], yv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          if (!(m[e] > 0.f)) v[e] = 0.f;
+          s0[e] += v[e];
+          s1[e] += v[e] * (yv[e] - mu[e]) * is[e];
+        }
+        o = pack8(v);
+      }
+      if (UNET_ABL != 4) *reinterpret_cast<uint4*>(a.y + gp * a.ldy + cob * kCOT + c8) = o;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own T rows read before the refill
+  };
+  int k = 0, b = 0, prev_pix0 = 0;
+  for (; item < nitems; item += gridDim.x, b ^= 1, ++k) {
+    const int next = item + gridDim.x;
+    // this tile's halo (first time also the weights and constants); XF: after
+    // the first tile it was waited for and transformed in the previous
+    // iteration, under the MFMAs
+    if (!XF || k == 0) wait_vmcnt<0>();
+    if (XF && k == 0) xform_halo(b, item);
+    if (k == 0) TSTAMP_TH(a.tim, 25, LT);
+    if (k == 1) TSTAMP_TH(a.tim, 27, LT);
+    __builtin_amdgcn_s_barrier();  // B
+    if (k > 0) epilogue(b ^ 1, prev_pix0);  // the previous tile, in the other buffer
+    if (k == 0) TSTAMP_TH(a.tim, 26, LT);
+    if (next < nitems) {  // its halo into the buffer just emptied
+      set_hoff(next);
+      issue_h(b ^ 1);
+    }
+    prev_pix0 = tile_pix0(item);
+    if (XF && next < nitems) {  // the next halo: landed and transformed before F
+      wait_vmcnt<0>();
+      xform_halo(b ^ 1, next);
+    }
+    __builtin_amdgcn_s_barrier();  // F
+    __builtin_amdgcn_s_barrier();  // E
+  }
+  // the last tile (buffer b ^ 1 after the loop's final flip)
+  epilogue(b ^ 1, prev_pix0);
+  TSTAMP_TH(a.tim, 21, LT);
+  // BN-backward sums: [32 slots][64 channels][2] in the other buffer (free),
+  // then 128 threads sum the slots in a fixed order
+  float* red = reinterpret_cast<float*>(smem + k2OffH0 + b * kHBytes);
+  if constexpr (FBWD) {
+    const int sl = lt >> 3;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(sl * kCOT + c8 + e) * 2 + 0] = s0[e];
+      red[(sl * kCOT + c8 + e) * 2 + 1] = s1[e];
+    }
+  }
+  __builtin_amdgcn_s_barrier();  // R1
+  if constexpr (!FLIP && STATS) {  // the compute waves' forward BN partials: [wave][lane][2][16]
+    if (lt < 2 * kCOT) {
+      const int co = lt % kCOT, which = lt / kCOT;
+      const int i = co >> 4, gg = (co >> 2) & 3, e = co & 3;
+      float p[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int w = 0; w < kNC; ++w)
+#pragma unroll
+        for (int l = 0; l < 16; ++l) p[l & 3] += red[(w * 64 + gg * 16 + l) * 32 + which * 16 + i * 4 + e];
+      const float tsum = (p[0] + p[1]) + (p[2] + p[3]);
+      atomicAdd(a.stats + rep + which * a.Cout + cob * kCOT + co, (double)tsum);
+    }
+  }
+  if constexpr (FBWD) {
+    if (lt < 2 * kCOT) {
+      const int c = lt % kCOT, which = lt / kCOT;
+      float p[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sl = 0; sl < 32; ++sl) p[sl & 3] += red[(sl * kCOT + c) * 2 + which];
+      const float tsum = (p[0] + p[1]) + (p[2] + p[3]);
+      atomicAdd(a.bb.sums + rep + which * a.Cout + cob * kCOT + c, (double)tsum);
+    }
+  }
+  __builtin_amdgcn_s_barrier();  // R2
+  TSTAMP_TH(a.tim, 22, LT);
+  TSTAMP_RT_TH(a.tim, 31, LT);
+}
+
+// the shapes and epilogues conv3x3_ws2_kernel covers (training step: forward
+// with bias and / or BN sums, data gradient with or without addend and fused
+// BN backward); everything else stays on conv3x3_ws_kernel
+bool conv3x3_ws2_ok(const ConvFwdArgs& a, bool flip) {
+  // A/B: the previous kernel (read per launch: tests set it); "f" / "b" / "x":
+  // only the forward / the data gradient / the xform forward
+  const char* ev = std::getenv("UNET_NO_WS2");
+  const bool off = ev && (ev[0] == '1' || (ev[0] == 'f' && !flip) || (ev[0] == 'b' && flip) ||
+                          (ev[0] == 'x' && !flip && a.xform));
+  // (the last-block BN finalisation, UNET_BN_TICKET, is not built in)
+  if (a.bn.ticket || a.bb.ticket) return false;
+  if (off || a.C != 64 || a.Cout % kCOT || a.P % kTH || a.Q % 16 || a.H != a.P || a.W != a.Q) return false;
+  if (a.R != 3 || a.S != 3 || a.stride != 1 || a.pad != 1 || a.x2 || a.ysplit || a.fold_on) return false;
+  if (a.xform && (flip || !a.xh || a.ldxh % 8)) return false;
+  if (a.ldx % 8 || a.ldy % 8 || (a.add && a.ldadd % 4)) return false;
+  if (!flip && (a.add || a.bb.sums)) return false;
+  if (flip && (a.stats || (a.bb.sums && (a.bb.y2 || a.bb.ldact % 8 || a.bb.ldy % 8)))) return false;
+  if ((size_t)a.N * a.H * a.W * a.ldx * 2 >= 0x80000000ull || (size_t)a.N * a.P * a.Q >= 0x80000000ull) return false;
+  return true;
+}
+
+hipError_t launch_conv3x3_ws2(const ConvFwdArgs& a, int mode, hipStream_t st) {
+  const bool flip = mode == 1;
+  if (!conv3x3_ws2_ok(a, flip)) return hipErrorInvalidValue;
+  const int ncb = a.Cout / kCOT;
+  const int nitems = a.N * (a.P / kTH) * (a.Q / 16) * ncb;
+  int grid = cu_count() / ncb * ncb;
+  if (grid < ncb) grid = ncb;
+  if (grid > nitems) grid = nitems;
+  const bool fbwd = flip && a.bb.sums;
+  const int ep = (a.add ? EP_ADD : 0) | (fbwd ? EP_FBWD : 0) | (a.stats || fbwd ? EP_STATS : 0) |
+                 (!flip && a.xform ? EP_XF : 0);
+  char tag[96];
+  std::snprintf(tag, sizeof(tag), "conv3x3_ws2_kernel<%s, %d>", flip ? "true" : "false", ep);
+  conv_kernel_tag(tag);
+  const dim3 g(grid), bl(kNW * 64);
+#define WS2_LAUNCH(F, E) hipLaunchKernelGGL((conv3x3_ws2_kernel<F, E>), g, bl, k2Lds, st, a, ncb, nitems)
+  if (!flip) {
+    if (ep == (EP_STATS | EP_XF)) WS2_LAUNCH(false, EP_STATS | EP_XF);
+    else if (ep == EP_XF) WS2_LAUNCH(false, EP_XF);
+    else if (ep == EP_STATS) WS2_LAUNCH(false, EP_STATS);
+    else WS2_LAUNCH(false, 0);
+  } else {
+    switch (ep) {
+      case EP_FBWD | EP_STATS: WS2_LAUNCH(true, EP_FBWD | EP_STATS); break;
+      case EP_FBWD | EP_STATS | EP_ADD: WS2_LAUNCH(true, EP_FBWD | EP_STATS | EP_ADD); break;
+      case EP_ADD: WS2_LAUNCH(true, EP_ADD); break;
+      default: WS2_LAUNCH(true, 0); break;
+    }
+  }
+#undef WS2_LAUNCH
+  return hipGetLastError();
+}
+
 }  // namespace unet

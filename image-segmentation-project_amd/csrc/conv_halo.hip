@@ -1110,6 +1110,7 @@ static hipError_t launch_halo_shape(const ConvFwdArgs& a, hipStream_t st) {
     return hipErrorNotSupported;
   }
   // weight-stationary: every tap of the block's channels fits in LDS
+  if (C == 64 && conv3x3_ws2_ok(a, FLIP)) return launch_conv3x3_ws2(a, FLIP ? 1 : 0, st);
   if (C == 64 && Co % 64 == 0 && a.P % 16 == 0) return launch_ws<2, 4, 16, 8, FLIP>(a, st);
   // decoder1 shapes (256^2, 96 / 32 channels), round-3 sweep on the Base
   // config: 8-row tiles on 8 waves (one row each, two waves per SIMD hide each

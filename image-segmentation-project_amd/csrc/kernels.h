@@ -166,6 +166,10 @@ bool conv3x3_ws_xform_ok(const ConvFwdArgs& a);
 // those convs chunk-major exactly when conv3x3_fl_shape holds (UNET_NO_FL=1: never)
 bool conv3x3_fl_shape(int N, int C, int Cout, int P, int Q);
 hipError_t launch_conv3x3_fl(const ConvFwdArgs& a, int mode, hipStream_t st);
+// weight-stationary full-line conv for C == 64 (conv_fl.hip), standard weight
+// pack; launch_conv3x3_ws uses it where conv3x3_ws2_ok holds (UNET_NO_WS2=1: never)
+bool conv3x3_ws2_ok(const ConvFwdArgs& a, bool flip);
+hipError_t launch_conv3x3_ws2(const ConvFwdArgs& a, int mode, hipStream_t st);
 // 3x3 / stride-2 / pad-1 data gradient by parity class on a shared dY halo
 // (conv_halo.hip), with the optional folded downsample (x2 / w2) range
 hipError_t launch_conv3x3s2_dgrad(const ConvFwdArgs& a, hipStream_t st);

@@ -1,11 +1,12 @@
-// Standalone check of conv3x3_fl_kernel (conv_fl.hip) against a CPU
-// reference: every buffer sits inside a guard region filled with a sentinel,
+// Standalone check of conv3x3_fl_kernel (conv_fl.hip; -DWS2: conv3x3_ws2_kernel,
+// C = 64, standard weight pack) against a CPU reference: every buffer sits inside a guard region filled with a sentinel,
 // so an out-of-range access lands in mapped memory and shows up as a changed
 // guard instead of a GPU fault.  Forward (bias + BN sums) and data gradient
 // (addend + fused BN-backward epilogue), C = Cout = 128, 16 x 32 x 64 pixels
 // (256 work items: the smallest shape the launcher takes on 256 CUs).
 // build: hipcc -O3 --offload-arch=gfx950 -I../../image-segmentation-project_amd/csrc \
 //          -o fl_check fl_check.hip ../../image-segmentation-project_amd/csrc/conv_fl.hip
+//        (the same with -DWS2 -o ws2_check)
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdio>
@@ -64,7 +65,11 @@ static float frand() {
 }
 
 int main(int argc, char** argv) {
+#ifdef WS2
+  const int N = 4, H = 32, W = 64, C = 64, Co = 64;
+#else
   const int N = 16, H = 32, W = 64, C = 128, Co = 128;
+#endif
   const int npix = N * H * W;
   // weights W[co][ci][3][3] (fp32 reference), input x[n][h][w][ci]
   std::vector<float> w((size_t)Co * C * 9), x((size_t)npix * C), bias(Co);
@@ -81,8 +86,13 @@ int main(int argc, char** argv) {
       for (int ci = 0; ci < C; ++ci)
         for (int t = 0; t < 9; ++t) {
           const float v = w[((size_t)co * C + ci) * 9 + t];
+#ifdef WS2  // standard pack [out][9][K]
+          if (mode == 0) wch[((size_t)co * 9 + t) * C + ci] = f2b(v);
+          else wch[((size_t)ci * 9 + t) * Co + co] = f2b(v);
+#else
           if (mode == 0) wch[((size_t)((ci >> 5) * 9 + t) * M + co) * 32 + (ci & 31)] = f2b(v);
           else wch[((size_t)((co >> 5) * 9 + t) * C + ci) * 32 + (co & 31)] = f2b(v);  // K = Co
+#endif
         }
     std::vector<uint16_t> xb((size_t)npix * K), addb((size_t)npix * M), actb((size_t)npix * M), yb((size_t)npix * M);
     for (size_t i = 0; i < xb.size(); ++i) xb[i] = f2b(x[i]);
@@ -143,7 +153,11 @@ int main(int argc, char** argv) {
     hipMemset(dsums.p(), 0, (size_t)kStatRep * 2 * M * 8);
     ConvFwdArgs a = {};
     a.x = (const bf16_t*)dx.p(); a.ldx = K;
+#ifdef WS2
+    a.w = (const bf16_t*)dw.p();
+#else
     a.wch = (const bf16_t*)dw.p();
+#endif
     a.y = (bf16_t*)dy.p(); a.ldy = M;
     a.N = N; a.H = H; a.W = W; a.C = K; a.P = H; a.Q = W; a.Cout = M;
     a.R = 3; a.S = 3; a.stride = 1; a.pad = 1;
@@ -158,7 +172,11 @@ int main(int argc, char** argv) {
       a.bb.mean = (const float*)dmean.p(); a.bb.invstd = (const float*)dinv.p();
       a.bb.C = M;
     }
+#ifdef WS2
+    hipError_t e = launch_conv3x3_ws2(a, mode, 0);
+#else
     hipError_t e = launch_conv3x3_fl(a, mode, 0);
+#endif
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) { printf("mode %d: launch/sync error %s\n", mode, hipGetErrorString(e)); return 1; }
     std::vector<uint16_t> out((size_t)npix * M);
