@@ -620,6 +620,49 @@ static_assert(k2Lds <= 163840, "LDS");
 static_assert(256 * 128 <= kHBytes, "bf16 tile fits a halo buffer");
 __device__ __forceinline__ int t2_off(int px, int c16) { return px * 128 + ((c16 ^ (px & 7)) << 4); }
 
+// items q0 .. q1 - 1 of one wave's share of a bf16 tile T: item q = stripe
+// sw + 4 q (8 pixels x 128 B), lane = (pixel (lane >> 3), 8 channels
+// c8 = 8 (lane & 7)); stores whole lines; FBWD: ReLU mask of the BN whose
+// backward is fused and its sums (s0, s1) from the stored bf16 dZ
+// (TV: the T values were read before -- tv[q - Q0] -- so that the buffer could
+// be refilled in between)
+template <bool FBWD, int Q0, int Q1, bool TV = false>
+__device__ __forceinline__ void ws2_items(const ConvFwdArgs& a, const char* T, int cob, int pix0, int sw, int lane,
+                                          const float (&mu)[8], const float (&is)[8], float (&s0)[8],
+                                          float (&s1)[8], const uint4* tv = nullptr) {
+  const int c8 = (lane & 7) * 8;
+  uint4 om[Q1 - Q0], oy[Q1 - Q0];
+  if constexpr (FBWD) {
+#pragma unroll
+    for (int q = Q0; q < Q1; ++q) {
+      const int px = (sw + 4 * q) * 8 + (lane >> 3);
+      const size_t gp = (size_t)(pix0 + (px >> 4) * a.Q + (px & 15));
+      om[q - Q0] = *reinterpret_cast<const uint4*>(a.bb.act + gp * a.bb.ldact + cob * kCOT + c8);
+      oy[q - Q0] = *reinterpret_cast<const uint4*>(a.bb.y + gp * a.bb.ldy + cob * kCOT + c8);
+    }
+  }
+#pragma unroll
+  for (int q = Q0; q < Q1; ++q) {
+    const int px = (sw + 4 * q) * 8 + (lane >> 3);
+    const size_t gp = (size_t)(pix0 + (px >> 4) * a.Q + (px & 15));
+    uint4 o = TV ? tv[q - Q0] : *reinterpret_cast<const uint4*>(T + t2_off(px, lane & 7));
+    if constexpr (FBWD) {
+      float v[8], m[8], yv[8];
+      unpack8(o, v);
+      unpack8(om[q - Q0], m);
+      unpack8(oy[q - Q0], yv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if (!(m[e] > 0.f)) v[e] = 0.f;
+        s0[e] += v[e];
+        s1[e] += v[e] * (yv[e] - mu[e]) * is[e];
+      }
+      o = pack8(v);
+    }
+    if (UNET_ABL != 4) *reinterpret_cast<uint4*>(a.y + gp * a.ldy + cob * kCOT + c8) = o;
+  }
+}
+
 template <bool FLIP, int EP>
 __global__ void __launch_bounds__(kNW * 64) conv3x3_ws2_kernel(ConvFwdArgs a, int ncb, int nitems) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -677,6 +720,7 @@ __global__ void __launch_bounds__(kNW * 64) conv3x3_ws2_kernel(ConvFwdArgs a, in
           for (int i = 0; i < kFN; ++i)
             uadd[j][i] = *reinterpret_cast<const uint2*>(a.add + gp * a.ldadd + cob * kCOT + i * 16 + 4 * g);
         }
+        asm volatile("" ::: "memory");  // issued here, not sunk next to their use after the MFMAs
       }
       const char* H = smem + k2OffH0 + b * kHBytes;
       f32x4 acc[kRW][kFN];
@@ -736,6 +780,29 @@ __global__ void __launch_bounds__(kNW * 64) conv3x3_ws2_kernel(ConvFwdArgs a, in
       barrier_lds();  // E: T written
     }
     TSTAMP(a.tim, 20);
+    float es0[8], es1[8], emu[8], eis[8];  // the compute waves' share of the last tile's epilogue
+#pragma unroll
+    for (int e = 0; e < 8; ++e) es0[e] = es1[e] = 0.f;
+    {
+      const int ce8 = (lane & 7) * 8;
+      if constexpr (FBWD) {
+        fl_ld8(cst + kCOT + ce8, emu);
+        fl_ld8(cst + 2 * kCOT + ce8, eis);
+      }
+      int lit = slot;  // the block's last item
+      while (lit + (int)gridDim.x < nitems) lit += gridDim.x;
+      ws2_items<FBWD, 4, 8>(a, smem + k2OffH0 + (b ^ 1) * kHBytes, cob, tile_pix0(lit), wave, lane, emu, eis, es0,
+                            es1);
+    }
+    if constexpr (FBWD) {  // partials into slots 32 .. 63 of the loaders' sum table
+      float* red = reinterpret_cast<float*>(smem + k2OffH0 + b * kHBytes);
+      const int sl = 32 + (tid >> 3), ce8 = (lane & 7) * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(sl * kCOT + ce8 + e) * 2 + 0] = es0[e];
+        red[(sl * kCOT + ce8 + e) * 2 + 1] = es1[e];
+      }
+    }
     if constexpr (!FLIP && STATS) {
       // BN sums: per-lane partials to LDS (the halo buffer the last tile did NOT
       // use: free), summed in a fixed order by 128 threads
@@ -846,44 +913,24 @@ __global__ void __launch_bounds__(kNW * 64) conv3x3_ws2_kernel(ConvFwdArgs a, in
   // (the fused-backward operands are loaded by the epilogue itself: a
   // prefetch a tile ahead made hipcc wait for vmcnt(0) -- the next halo's DMA
   // -- before reusing the store-data registers; measured slower)
-  auto epilogue = [&](int tb, int pix0) {
+  // the previous tile's epilogue in two halves around the refill of its
+  // buffer: this wave's T rows into registers, then (the caller) the next
+  // halo's DMA, then the operand loads, mask / sums and stores -- the DMA is
+  // older than the operand loads, so hipcc's waits for those cover it exactly
+  uint4 tv[8];
+  auto epi_read = [&](int tb) {
     const char* T = smem + k2OffH0 + tb * kHBytes;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) tv[q] = *reinterpret_cast<const uint4*>(T + t2_off((lw + 4 * q) * 8 + (lane >> 3), lane & 7));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own T rows read before the refill
+  };
+  auto epilogue = [&](int tb, int pix0) {
     if (FBWD && !have_cst) {
       fl_ld8(cst + kCOT + c8, mu);
       fl_ld8(cst + 2 * kCOT + c8, is);
       have_cst = true;
     }
-    uint4 om[8], oy[8];
-    if constexpr (FBWD) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int px = (lw + 4 * q) * 8 + (lane >> 3);
-        const size_t gp = (size_t)(pix0 + (px >> 4) * a.Q + (px & 15));
-        om[q] = *reinterpret_cast<const uint4*>(a.bb.act + gp * a.bb.ldact + cob * kCOT + c8);
-        oy[q] = *reinterpret_cast<const uint4*>(a.bb.y + gp * a.bb.ldy + cob * kCOT + c8);
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int px = (lw + 4 * q) * 8 + (lane >> 3);
-      const size_t gp = (size_t)(pix0 + (px >> 4) * a.Q + (px & 15));
-      uint4 o = *reinterpret_cast<const uint4*>(T + t2_off(px, lane & 7));
-      if constexpr (FBWD) {
-        float v[8], m[8], yv[8];
-        unpack8(o, v);
-        unpack8(om[q], m);
-        unpack8(oy[q], yv);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          if (!(m[e] > 0.f)) v[e] = 0.f;
-          s0[e] += v[e];
-          s1[e] += v[e] * (yv[e] - mu[e]) * is[e];
-        }
-        o = pack8(v);
-      }
-      if (UNET_ABL != 4) *reinterpret_cast<uint4*>(a.y + gp * a.ldy + cob * kCOT + c8) = o;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own T rows read before the refill
+    ws2_items<FBWD, 0, 8, true>(a, nullptr, cob, pix0, lw, lane, mu, is, s0, s1, tv);
   };
   int k = 0, b = 0, prev_pix0 = 0;
   for (; item < nitems; item += gridDim.x, b ^= 1, ++k) {
@@ -896,12 +943,13 @@ __global__ void __launch_bounds__(kNW * 64) conv3x3_ws2_kernel(ConvFwdArgs a, in
     if (k == 0) TSTAMP_TH(a.tim, 25, LT);
     if (k == 1) TSTAMP_TH(a.tim, 27, LT);
     __builtin_amdgcn_s_barrier();  // B
-    if (k > 0) epilogue(b ^ 1, prev_pix0);  // the previous tile, in the other buffer
+    if (k > 0) epi_read(b ^ 1);  // the previous tile's T, in the other buffer
     if (k == 0) TSTAMP_TH(a.tim, 26, LT);
     if (next < nitems) {  // its halo into the buffer just emptied
       set_hoff(next);
       issue_h(b ^ 1);
     }
+    if (k > 0) epilogue(b ^ 1, prev_pix0);
     prev_pix0 = tile_pix0(item);
     if (XF && next < nitems) {  // the next halo: landed and transformed before F
       wait_vmcnt<0>();
@@ -910,10 +958,17 @@ __global__ void __launch_bounds__(kNW * 64) conv3x3_ws2_kernel(ConvFwdArgs a, in
     __builtin_amdgcn_s_barrier();  // F
     __builtin_amdgcn_s_barrier();  // E
   }
-  // the last tile (buffer b ^ 1 after the loop's final flip)
-  epilogue(b ^ 1, prev_pix0);
+  // the last tile (buffer b ^ 1 after the loop's final flip): items 0 .. 3 of
+  // every stripe set here, 4 .. 7 by the compute waves (nothing else to do)
+  {
+    if (FBWD && !have_cst) {
+      fl_ld8(cst + kCOT + c8, mu);
+      fl_ld8(cst + 2 * kCOT + c8, is);
+    }
+    ws2_items<FBWD, 0, 4>(a, smem + k2OffH0 + (b ^ 1) * kHBytes, cob, prev_pix0, lw, lane, mu, is, s0, s1);
+  }
   TSTAMP_TH(a.tim, 21, LT);
-  // BN-backward sums: [32 slots][64 channels][2] in the other buffer (free),
+  // BN-backward sums: [64 slots (32 loader, 32 compute)][64 channels][2] in the other buffer (free),
   // then 128 threads sum the slots in a fixed order
   float* red = reinterpret_cast<float*>(smem + k2OffH0 + b * kHBytes);
   if constexpr (FBWD) {
@@ -943,7 +998,7 @@ __global__ void __launch_bounds__(kNW * 64) conv3x3_ws2_kernel(ConvFwdArgs a, in
       const int c = lt % kCOT, which = lt / kCOT;
       float p[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int sl = 0; sl < 32; ++sl) p[sl & 3] += red[(sl * kCOT + c) * 2 + which];
+      for (int sl = 0; sl < 64; ++sl) p[sl & 3] += red[(sl * kCOT + c) * 2 + which];
       const float tsum = (p[0] + p[1]) + (p[2] + p[3]);
       atomicAdd(a.bb.sums + rep + which * a.Cout + cob * kCOT + c, (double)tsum);
     }

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Interleaved A/B of whole-step throughput (bench.py graph replay, no CPU
-# baseline, no parity leg): R rounds over the given variants, one bench process
-# per variant per round, medians at the end.
+# baseline, no parity leg, STEPS timed steps, default 150): R rounds over the
+# given variants, one bench process per variant per round, every other round in
+# reverse order (ABBA), medians at the end.
 # A variant is  [VAR=val[,VAR=val...]][@lib.so]  ("-" or "" = defaults, the
 # in-tree libunet_hip.so); e.g.
 #   scripts/ab.sh 3 - @ab/libunet_hip_r04.so UNET_APPLY_CAP=1024
@@ -14,8 +15,13 @@ mkdir -p gpurun_out
 R=$1; shift
 out=gpurun_out/ab.txt
 : > $out
+STEPS=${STEPS:-150}
+specs=("$@")
 for r in $(seq 1 $R); do
-  for spec in "$@"; do
+  # ABBA: every other round in reverse order (clock / thermal drift cancels)
+  order=("${specs[@]}")
+  if [ $((r % 2)) -eq 0 ]; then order=(); for ((i=${#specs[@]}-1; i>=0; i--)); do order+=("${specs[$i]}"); done; fi
+  for spec in "${order[@]}"; do
     envs=${spec%%@*}; lib=""
     [[ "$spec" == *@* ]] && lib=${spec#*@}
     [ "$envs" = "-" ] && envs=""
@@ -28,7 +34,7 @@ for r in $(seq 1 $R); do
       grep -E "$AB_LAYERS" gpurun_out/ab_layers.log | tee -a $out
       continue
     fi
-    v=$(env "${args[@]}" timeout -k 10 120 python3 bench.py --no-cpu-baseline --no-parity --steps 30 --warmup 10 \
+    v=$(env "${args[@]}" timeout -k 10 120 python3 bench.py --no-cpu-baseline --no-parity --steps $STEPS --warmup 20 \
         $BENCH_ARGS 2>/dev/null | grep -o '"value": [0-9.]*' | grep -o '[0-9.]*$') || exit 1
     echo "round $r [$spec] $v" | tee -a $out
   done
