@@ -14,6 +14,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # UNET_HIP_LIB: an alternative in-tree build for A/B measurements (scripts/)
 LIB_PATH = os.environ.get("UNET_HIP_LIB") or os.path.join(_HERE, "libunet_hip.so")
+LOSS_SUMS_LEN = 8 + 8 * 256  # UNET_LOSS_SUMS_LEN (include/unet_hip.h): 8 sums + per-block partials
 
 _lib = None
 

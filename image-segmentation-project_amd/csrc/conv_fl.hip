@@ -320,7 +320,7 @@ __global__ void __launch_bounds__(kNW * 64) conv3x3_fl_kernel(ConvFwdArgs a, int
     for (int k = 0; k < kHPer; ++k)
       if (k < nh) glds16_asm(xr, dst + (lw + k * kNL) * 1024, hoff[k], so);
   };
-  constexpr int LT = kNC * 64;  // the loader thread that stamps (timing build)
+  [[maybe_unused]] constexpr int LT = kNC * 64;  // the loader thread that stamps (timing build)
   set_hoff(item);
   TSTAMP_TH(a.tim, 23, LT);
   issue_w(0, 0);
@@ -825,7 +825,7 @@ __global__ void __launch_bounds__(kNW * 64) conv3x3_ws2_kernel(ConvFwdArgs a, in
   const int nh = (kHIns - lw + kNL - 1) / kNL;  // 11 or 10
   const i32x4 xr = make_rsrc_sgpr(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
   const i32x4 wr = make_rsrc_sgpr(a.w, (unsigned)((size_t)a.Cout * 9 * a.C * 2));
-  constexpr int LT = kNC * 64;
+  [[maybe_unused]] constexpr int LT = kNC * 64;
   unsigned hoff[kHPer];
   auto set_hoff = [&](int it) {
     const int t = it / ncb;

@@ -947,7 +947,8 @@ hipError_t launch_head_grads(const HeadArgs& a, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------
-// per-channel sums (ConvTranspose bias gradients)
+// per-channel sums (ConvTranspose bias gradients; the replicas are summed into
+// the fp32 gradient by bucket 0's unpack launch, UP_D2F)
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) channel_sum_kernel(const bf16_t* x, int ldx, int64_t npix, int C,
                                                          double* acc) {
@@ -1146,6 +1147,15 @@ hipError_t launch_pack(const PackTable& t, hipStream_t st) {
 constexpr int kUpK = 512, kUpT = 9;
 __global__ void __launch_bounds__(256) unpack_kernel(UnpackTable t) {
   const UnpackEntry e = t.e[blockIdx.y];
+  if (e.kind == UP_D2F) {  // dst[i] = sum of the kStatRep fp64 replicas acc[r][i] (as d2f_kernel)
+    const double* s = reinterpret_cast<const double*>(e.acc);
+    for (int i = (int)blockIdx.x * blockDim.x + threadIdx.x; i < e.Co; i += (int)gridDim.x * blockDim.x) {
+      double v = 0.0;
+      for (int r = 0; r < kStatRep; ++r) v += s[(size_t)r * e.Co + i];
+      e.dst[i] = (float)v;
+    }
+    return;
+  }
   if (e.kind == UP_ZERO || e.kind == UP_STEM) {
     const int total = e.kind == UP_ZERO ? e.Co : e.Co * 49;
     for (int i = (int)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int)gridDim.x * blockDim.x) {
@@ -1232,17 +1242,27 @@ hipError_t launch_unpack(const UnpackTable& t, hipStream_t st) {
 // pixel-wise loss and mask metrics (losses.py:13-37,161-171; utils.py:120-151)
 // ---------------------------------------------------------------------------
 // One pass over the pixels: 8 per-thread fp32 sums, folded per block in fp64
-// and added with fp64 atomics.  One block per CU (256 blocks): a 1024-block
-// grid put 1024 fp64 atomics on each of the 8 addresses, which serialised at
-// L2 (62 us per Base step for 4 M pixels; 256 per address now).  float4 loads
-// (4 in flight per thread) when both operands are 16-B aligned.
+// into the block's partial slot (loss_reduce_kernel adds the slots in order).
+// One block per CU (256 blocks); float4 loads (4 in flight per thread) when both
+// operands are 16-B aligned.  The pass is VALU-bound, not HBM-bound: libm
+// expf + log1pf + expf + an IEEE divide per pixel compiled to ~175 VALU
+// instructions (26.7 us for 4 M pixels, 1.2 TB/s), so the terms share one
+// exponential e = exp(-|v|) and one reciprocal of 1 + e on the hardware
+// v_exp_f32 / v_log_f32 / v_rcp_f32 (~1 ulp each):
+//   log1p(e) = log(u) * e / (u - 1), u = 1 + e  (exact-rounding correction; e when u == 1)
+//   sigma(v) = (v >= 0 ? 1 : e) / u
 __device__ __forceinline__ void loss_accum(float v, float y, int from_prob, float (&s)[8]) {
   float pred;
   if (!from_prob) {
     // torch: (1 - y) * x - log_sigmoid(x),  log_sigmoid(x) = min(x,0) - log1p(exp(-|x|))
-    const float ls = fminf(v, 0.f) - log1pf(expf(-fabsf(v)));
+    const float e = __expf(-fabsf(v));
+    const float u = 1.f + e;
+    const float ru = __builtin_amdgcn_rcpf(u);
+    const float um1 = u - 1.f;
+    const float l1p = um1 == 0.f ? e : __logf(u) * (e * __builtin_amdgcn_rcpf(um1));
+    const float ls = fminf(v, 0.f) - l1p;
     s[0] += (1.f - y) * v - ls;
-    const float sg = 1.f / (1.f + expf(-v));
+    const float sg = (v >= 0.f ? 1.f : e) * ru;
     s[1] += sg * y;
     s[2] += sg;
     s[3] += y;
@@ -1299,34 +1319,51 @@ __global__ void __launch_bounds__(kLossNT) loss_sums_kernel(const float* x, cons
     if (lane == 0) red[wave][k] = v;
   }
   __syncthreads();
+  // this block's partial sums (fixed wave order) go to its own slot: the 8
+  // totals are summed in block order by loss_reduce_kernel.  One fp64 atomic
+  // per block and value on a single 64-B line serialised ~256 device-scope
+  // atomics per address (the kernel measured 37 us for 32 MB, r04 profiles)
+  // and made the sums depend on block arrival order.
   if (threadIdx.x < 8) {
     const int k = threadIdx.x;
     double v = 0.0;
     for (int w = 0; w < kLossNT / 64; ++w) v += red[w][k];
-    atomicAdd(sums + k, v);
+    sums[8 + blockIdx.x * 8 + k] = v;
   }
 }
 
-hipError_t launch_loss_sums(const float* logits, const float* target, int64_t n, double* sums, int from_prob,
-                            hipStream_t st) {
-  hipLaunchKernelGGL(loss_sums_kernel, dim3(grid_for(n, kLossNT * 16, 256)), dim3(kLossNT), 0, st, logits, target, n,
-                     sums, from_prob);
-  return hipGetLastError();
+// sums[k] = sum over blocks b (in order, 64 lanes then a fixed butterfly) of
+// the partial sums[8 + 8 b + k]; wave k owns value k.  Thread 0 then writes the
+// loss value when `out` is given.
+__global__ void __launch_bounds__(512) loss_reduce_kernel(double* s, int nblk, int64_t n, int kind, float alpha,
+                                                          float smooth, float* out) {
+  __shared__ double tot[8];
+  const int k = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  double v = 0.0;
+  for (int b = lane; b < nblk; b += 64) v += s[8 + b * 8 + k];
+  v = wave_sum_d(v);
+  if (lane == 0) {
+    s[k] = v;
+    tot[k] = v;
+  }
+  __syncthreads();
+  if (out == nullptr || threadIdx.x != 0) return;
+  const double bce = tot[0] / (double)n;
+  const double dice = 1.0 - (2.0 * tot[1] + smooth) / (tot[2] + tot[3] + smooth);
+  double r;
+  if (kind == LOSS_BCE) r = bce;
+  else if (kind == LOSS_DICE) r = dice;
+  else r = alpha * bce + (1.0 - alpha) * dice;
+  *out = (float)r;
 }
 
-__global__ void loss_value_kernel(const double* s, int64_t n, int kind, float alpha, float smooth, float* out) {
-  if (threadIdx.x != 0) return;
-  const double bce = s[0] / (double)n;
-  const double dice = 1.0 - (2.0 * s[1] + smooth) / (s[2] + s[3] + smooth);
-  double v;
-  if (kind == LOSS_BCE) v = bce;
-  else if (kind == LOSS_DICE) v = dice;
-  else v = alpha * bce + (1.0 - alpha) * dice;
-  *out = (float)v;
-}
-hipError_t launch_loss_value(const double* sums, int64_t n, int kind, float alpha, float smooth, float* out,
-                             hipStream_t st) {
-  hipLaunchKernelGGL(loss_value_kernel, dim3(1), dim3(64), 0, st, sums, n, kind, alpha, smooth, out);
+hipError_t launch_loss_sums(const float* logits, const float* target, int64_t n, double* sums, int from_prob,
+                            int kind, float alpha, float smooth, float* out, hipStream_t st) {
+  const int nblk = grid_for(n, kLossNT * 16, kLossBlocks);
+  hipLaunchKernelGGL(loss_sums_kernel, dim3(nblk), dim3(kLossNT), 0, st, logits, target, n, sums, from_prob);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(512), 0, st, sums, nblk, n, kind, alpha, smooth, out);
   return hipGetLastError();
 }
 

@@ -148,6 +148,9 @@ struct unet_plan {
   size_t ws_bytes = 0;
   size_t zero_fwd_off = 0, zero_fwd_bytes = 0;
   size_t zero_bwd_off = 0, zero_bwd_bytes = 0;
+  // a training forward zeroes the backward's region too (it follows the
+  // forward's, one fill instead of two); the next backward then skips its fill
+  bool bwd_zeroed = false;
   size_t head_usum = 0;
   size_t wslab = 0, wslab_bytes = 0;  // split-K partials of the halo weight-gradient kernel
   int64_t grad_numel = 0;
@@ -205,7 +208,7 @@ struct unet_plan {
   // too (tests of the intermediates)
   bool stem_rc = !(std::getenv("UNET_STEM_RC") && std::atoi(std::getenv("UNET_STEM_RC")) == 0);
   bool stem_keep = std::getenv("UNET_STEM_KEEP") && std::atoi(std::getenv("UNET_STEM_KEEP")) != 0;
-  size_t stem_part = 0, stem_tot = 0;
+  size_t stem_part = 0, stem_tot = 0, stem_tkt = 0;
   std::vector<ConvWgradArgs> wgb;  // collected weight gradients of the current bucket
   std::vector<std::string> wgb_names;
   double wgb_flops = 0;
@@ -483,13 +486,14 @@ static int build_plan(unet_plan* p) {
   for (auto& cv : p->convs)
     if (cv.kind == L_CONVT) cv.bias_acc = A.take((size_t)kStatRep * cv.Co * sizeof(double));
   p->head_usum = A.take((size_t)(up0_in * 4 + 1) * sizeof(double));
+  p->stem_tkt = A.take(kStemTickets * sizeof(unsigned));
   for (auto& t : p->atts) {
     t.pbs = A.take(2 * sizeof(double));
     t.cda = A.take((size_t)N * t.C * sizeof(double));
     t.gpsi = A.take((size_t)kStatRep * t.Fi * sizeof(double));
     t.gfc = A.take((size_t)kStatRep * 2 * t.C * t.Cr * sizeof(double));
   }
-  p->zero_bwd_bytes = A.top - p->zero_bwd_off;
+  p->zero_bwd_bytes = A.top - p->zero_bwd_off;  // starts where the forward's region ends: one fill spans both
   // weight-gradient accumulators: every element is WRITTEN by its wgrad launch
   // (deterministic split-K slab reduction, kernels.h SlabLayout), so they are
   // not zeroed
@@ -1262,6 +1266,14 @@ int unpack_bucket(const Ctx& x, int bk, float* grads) {
       RUN(zero(x.p->convs[a.wx].b));
       RUN(zero(a.psi_b));
     }
+    // up-conv (ConvTranspose) bias gradients: the channel sums' fp64 replicas
+    for (const Dec& d : x.p->decs) {
+      if (d.up < 0) continue;
+      const Conv& up = x.p->convs[d.up];
+      t.e[t.n++] = UnpackEntry{reinterpret_cast<const float*>(x.W<double>(up.bias_acc)),
+                               grads + x.p->params[up.b].flat, UP_D2F, up.Co, 1, 1, 1};
+      if (t.n == kMaxPack) { CK(launch_unpack(t, x.wst)); t.n = 0; }
+    }
   }
   for (int ci : x.p->bucket_convs[bk]) {
     const Conv& cv = x.p->convs[ci];
@@ -1379,7 +1391,12 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
                        float* logits, int training, hipStream_t st) {
   Ctx x{p, ws, prm, buf, st, training};
   const int N = p->cfg.N;
-  CK(hipMemsetAsync(ws + p->zero_fwd_off, 0, p->zero_fwd_bytes, st));
+  if (training) {
+    CK(hipMemsetAsync(ws + p->zero_fwd_off, 0, p->zero_fwd_bytes + p->zero_bwd_bytes, st));
+    p->bwd_zeroed = true;
+  } else {
+    CK(hipMemsetAsync(ws + p->zero_fwd_off, 0, p->zero_fwd_bytes, st));
+  }
   if (p->f8n) {  // fp8 scale states: calibrate on the plan's first forward, else roll
     // (training only: an eval forward quantizes with the scales in use and
     // commits no amax, so validation never moves the training scales)
@@ -1576,7 +1593,8 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
   p->syncused = 0;
   // fork: the weight stream starts after the zeroing of the accumulators
   auto fork = [&]() { return stream_edge(p, st, x.wst); };
-  CK(hipMemsetAsync(ws + p->zero_bwd_off, 0, p->zero_bwd_bytes, st));
+  if (!p->bwd_zeroed) CK(hipMemsetAsync(ws + p->zero_bwd_off, 0, p->zero_bwd_bytes, st));
+  p->bwd_zeroed = false;
   const bool att = !p->atts.empty();
   // head (upconv0 + conv_final)
   {
@@ -1678,8 +1696,8 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     RUN(conv_wgrad(x, d.up, du, d.up_in));
     {
       ProfScope ps(p, x.wst, "bias_sum", 0);
+      // the replicas become the fp32 gradient in bucket 0's unpack launch (UP_D2F)
       CK(launch_channel_sum(x.A(du), du.ld, (int64_t)N * du.H * du.W, up.Co, x.W<double>(up.bias_acc), x.wst));
-      CK(launch_d2f(x.W<double>(up.bias_acc), grads + p->params[up.b].flat, up.Co, x.wst));
     }
     const BnBwdArgs fu = l > 0 ? dec_bn2(l - 1) : blk_bn2(nb - 1);
     // with attention the up-conv input of levels 3..1 is the channel-gated
@@ -1773,6 +1791,7 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     s.part = x.W<float>(p->stem_part);
     s.l2 = reinterpret_cast<double*>(s.part + stem_rc_l2_offset(N, p->y0.H, p->y0.W, p->x1.C) / sizeof(float));
     s.tot = x.W<double>(p->stem_tot);
+    s.tkt = x.W<unsigned>(p->stem_tkt);
     s.imsum = reinterpret_cast<float*>(reinterpret_cast<char*>(s.tot) + stem_rc_imsum_offset(p->x1.C));
     s.dw = x.W<float>(p->convs[p->stem_conv].wacc);
     s.dgamma = sb.dgamma; s.dbeta = sb.dbeta;
@@ -1991,11 +2010,11 @@ int unet_bucket_wait(unet_plan* p, int bucket, hipStream_t waiter) {
   return 0;
 }
 
+static_assert(UNET_LOSS_SUMS_LEN == 8 + 8 * kLossBlocks, "loss partial slots");
+
 int unet_loss_forward(const float* logits, const float* target, int64_t n, int kind, float alpha, float smooth,
                       double* sums8, float* loss_out, hipStream_t stream) {
-  CK(hipMemsetAsync(sums8, 0, 8 * sizeof(double), stream));
-  CK(launch_loss_sums(logits, target, n, sums8, 0, stream));
-  CK(launch_loss_value(sums8, n, kind, alpha, smooth, loss_out, stream));
+  CK(launch_loss_sums(logits, target, n, sums8, 0, kind, alpha, smooth, loss_out, stream));
   return 0;
 }
 
@@ -2007,8 +2026,7 @@ int unet_loss_backward(const float* logits, const float* target, int64_t n, int 
 
 int unet_mask_metrics(const float* values, const float* target, int64_t n, int values_are_prob, double* sums8,
                       hipStream_t stream) {
-  CK(hipMemsetAsync(sums8, 0, 8 * sizeof(double), stream));
-  CK(launch_loss_sums(values, target, n, sums8, values_are_prob, stream));
+  CK(launch_loss_sums(values, target, n, sums8, values_are_prob, 0, 0.f, 0.f, nullptr, stream));
   return 0;
 }
 

@@ -301,6 +301,7 @@ struct StemRcArgs {
   const float* mean; const float* invstd;   // saved batch statistics
   bf16_t* dz; int lddz;
   float* part; double* l2; double* tot;   // partials, fp64 level-1 sums, fp64 totals
+  unsigned* tkt;                     // reduce tickets (stem_rc_tickets(Cout) words, zeroed)
   float* imsum;                      // [256] fixed-order block sums of img (backward centring)
   float* dw; float* dgamma; float* dbeta;
   int64_t npix;
@@ -308,8 +309,10 @@ struct StemRcArgs {
 };
 bool stem_rc_ok(int Cout, int P, int Q);
 hipError_t launch_stem_rc_fwd(const StemRcArgs& a, int mode, hipStream_t st);
-// stage 0: the fused backward pass; stage 1: the fixed-order reduce + finalise
+// stage 0: the fused backward pass; stage 1: the fixed-order reduce + finalise (one launch)
 hipError_t launch_stem_rc_bwd(const StemRcArgs& a, int stage, hipStream_t st);
+int stem_rc_tickets(int Cout);
+constexpr int kStemTickets = 1024;  // ticket words the executor reserves
 size_t stem_rc_part_bytes(int N, int P, int Q, int Cout);  // a.part followed by a.l2
 size_t stem_rc_tot_bytes(int Cout);                        // a.tot followed by a.imsum
 size_t stem_rc_imsum_offset(int Cout);                     // bytes from a.tot to a.imsum
@@ -337,8 +340,8 @@ hipError_t launch_head_bwd(const HeadArgs& a, hipStream_t st);
 hipError_t launch_head_grads(const HeadArgs& a, hipStream_t st);
 
 // per-channel sum over pixels (ConvTranspose bias grads): acc[r][c] += partial
-// sums of x[px][c] (acc: fp64 [kStatRep][C], zeroed); launch_d2f then writes
-// dst[c] = sum_r acc[r][c]
+// sums of x[px][c] (acc: fp64 [kStatRep][C], zeroed); an UP_D2F unpack entry
+// (or launch_d2f) then writes dst[c] = sum_r acc[r][c]
 hipError_t launch_channel_sum(const bf16_t* x, int ldx, int64_t npix, int C, double* acc,
                               hipStream_t st);
 hipError_t launch_d2f(const double* src, float* dst, int n, hipStream_t st);
@@ -351,7 +354,8 @@ hipError_t launch_d2f_strided(const double* src, float* dst, int n, int stride, 
 enum { PK_CONV_FWD = 0, PK_CONV_DGRAD = 1, PK_CONVT_FWD = 2, PK_CONVT_DGRAD = 3, PK_STEM = 4, PK_CONV_FWD_CH = 5,
        PK_CONV_DGRAD_CH = 6 };
 struct PackEntry { const float* src; bf16_t* dst; int kind, Co, Ci, R, S; };
-enum { UP_CONV = 0, UP_CONVT = 1, UP_STEM = 2, UP_ZERO = 3 };  // UP_ZERO: dst[0 .. Co) = 0
+// UP_ZERO: dst[0 .. Co) = 0; UP_D2F: dst[i] = sum_r acc[r][i], acc fp64 [kStatRep][Co]
+enum { UP_CONV = 0, UP_CONVT = 1, UP_STEM = 2, UP_ZERO = 3, UP_D2F = 4 };
 struct UnpackEntry { const float* acc; float* dst; int kind, Co, Ci, R, S; };
 constexpr int kMaxPack = 48;
 struct PackTable { int n; PackEntry e[kMaxPack]; };
@@ -361,11 +365,11 @@ hipError_t launch_unpack(const UnpackTable& t, hipStream_t st);
 
 // loss + metrics
 enum { LOSS_BCE = 0, LOSS_DICE = 1, LOSS_COMBO = 2 };
-// sums[0..8): sum bce, sum sig*y, sum sig, sum y, tp, fp, fn, tn
+// sums[0..8): sum bce, sum sig*y, sum sig, sum y, tp, fp, fn, tn; sums[8..8+8*kLossBlocks):
+// per-block partials (UNET_LOSS_SUMS_LEN doubles in all).  out != nullptr: also the loss value.
+constexpr int kLossBlocks = 256;
 hipError_t launch_loss_sums(const float* logits, const float* target, int64_t n, double* sums,
-                            int from_prob, hipStream_t st);
-hipError_t launch_loss_value(const double* sums, int64_t n, int kind, float alpha, float smooth,
-                             float* out, hipStream_t st);
+                            int from_prob, int kind, float alpha, float smooth, float* out, hipStream_t st);
 hipError_t launch_loss_grad(const float* logits, const float* target, int64_t n, const double* sums,
                             int kind, float alpha, float smooth, const float* gscale, float* dl,
                             hipStream_t st);

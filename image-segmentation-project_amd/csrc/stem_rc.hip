@@ -792,64 +792,35 @@ __global__ void __launch_bounds__(kRbNT, 2) stem_rc_bwd_kernel(StemRcArgs a, int
 // fixed-order sums of the blocks' partials, in fp64: level 1 block (chunk,
 // seg, group) sums partials [16 seg, 16 seg + 16) of f32x4 units [64 chunk,
 // 64 chunk + 64) (4 split lanes of 4 partials, added in lane order); level 2
-// sums the segments the same way.  The finalise forms dW from the totals.
+// sums the segments the same way, and the last of a group's level-2 blocks to
+// arrive (ticket) forms dW from the totals (formerly a third launch; same
+// orders, bit-identical).  Level 1 takes no ticket: its ~1.2 k blocks would
+// each need an agent-scope release (an L2 write-back) and a returning atomic on
+// one word — that single-launch form measured 39.5 us against 14 us for the
+// three launches.
 constexpr int kRbSeg = 16;
-__global__ void __launch_bounds__(256) stem_rc_sum1_kernel(StemRcArgs a, int nblk, int nseg) {
-  __shared__ double sp[4][64][4];
-  const int tid = threadIdx.x, lane = tid & 63, sl = tid >> 6;
-  const int seg = blockIdx.y, grp = blockIdx.z;
-  const f32x4* part = reinterpret_cast<const f32x4*>(a.part) + (size_t)grp * nblk * kRbPartF4;
-  const int u = blockIdx.x * 64 + lane;
-  double d[4] = {0.0, 0.0, 0.0, 0.0};
-  if (u < kRbPartF4) {
-    const int b0 = seg * kRbSeg + sl * (kRbSeg / 4);
-    f32x4 v[kRbSeg / 4];
-#pragma unroll
-    for (int q = 0; q < kRbSeg / 4; ++q)
-      v[q] = b0 + q < nblk ? part[(size_t)(b0 + q) * kRbPartF4 + u] : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int q = 0; q < kRbSeg / 4; ++q)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) d[e] += (double)v[q][e];
-  }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) sp[sl][lane][e] = d[e];
-  __syncthreads();
-  if (sl == 0 && u < kRbPartF4) {
-    double* o = a.l2 + (((size_t)grp * nseg + seg) * kRbPartF4 + u) * 4;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = ((sp[0][lane][e] + sp[1][lane][e]) + sp[2][lane][e]) + sp[3][lane][e];
-  }
-}
+constexpr int kRbChunks = (kRbPartF4 + 63) / 64;
 
-__global__ void __launch_bounds__(256) stem_rc_sum2_kernel(StemRcArgs a, int nseg) {
-  __shared__ double sp[4][64][4];
-  const int tid = threadIdx.x, lane = tid & 63, sl = tid >> 6;
-  const int grp = blockIdx.y;
-  const int u = blockIdx.x * 64 + lane;
-  double d[4] = {0.0, 0.0, 0.0, 0.0};
-  if (u < kRbPartF4) {
-    for (int s = sl; s < nseg; s += 4) {
-      const double* o = a.l2 + (((size_t)grp * nseg + s) * kRbPartF4 + u) * 4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) d[e] += o[e];
-    }
-  }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) sp[sl][lane][e] = d[e];
+// every wave drains its stores, one lane releases them at agent scope (L2
+// write-back: the reader may sit on another XCD) and takes a ticket
+__device__ __forceinline__ bool rb_arrive(unsigned* ticket, unsigned total, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (sl == 0 && u < kRbPartF4) {
-    double* o = a.tot + ((size_t)grp * kRbPartF4 + u) * 4;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = ((sp[0][lane][e] + sp[1][lane][e]) + sp[2][lane][e]) + sp[3][lane][e];
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = prev == total - 1 ? 1 : 0;
+    if (*flag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
+  __syncthreads();
+  return *flag != 0;
 }
 
 // dW[co][k] = k1 (A - m1 B - m2 X), dgamma = sum dZ xhat, dbeta = sum dZ
 // (one block per 64-channel group; totals [unit][4] fp64)
-__global__ void __launch_bounds__(256) stem_rc_finalize_kernel(StemRcArgs a) {
+__device__ void stem_rc_finalize(const StemRcArgs& a, int grp) {
   __shared__ double cA[64], cM1[64], cM2[64], bsum[64];
-  const int tid = threadIdx.x, grp = blockIdx.x, cg = grp * 64;
+  const int tid = threadIdx.x, cg = grp * 64;
   const double* tot = a.tot + (size_t)grp * kRbPartF4 * 4;
   if (tid < 64) {
     // channel sums: floats [0, 64) sum dZ, [64, 128) sum dZ xhat after the 2304 fragment units
@@ -881,6 +852,60 @@ __global__ void __launch_bounds__(256) stem_rc_finalize_kernel(StemRcArgs a) {
       a.dw[(size_t)(cg + co) * 64 + k] = (float)(cA[co] * (A[e] - cM1[co] * bsum[k] - cM2[co] * X[e]));
     }
   }
+}
+
+__global__ void __launch_bounds__(256) stem_rc_sum1_kernel(StemRcArgs a, int nblk, int nseg) {
+  __shared__ double sp[4][64][4];
+  const int tid = threadIdx.x, lane = tid & 63, sl = tid >> 6;
+  const int seg = blockIdx.y, grp = blockIdx.z;
+  const f32x4* part = reinterpret_cast<const f32x4*>(a.part) + (size_t)grp * nblk * kRbPartF4;
+  const int u = blockIdx.x * 64 + lane;
+  double d[4] = {0.0, 0.0, 0.0, 0.0};
+  if (u < kRbPartF4) {
+    const int b0 = seg * kRbSeg + sl * (kRbSeg / 4);
+    f32x4 v[kRbSeg / 4];
+#pragma unroll
+    for (int q = 0; q < kRbSeg / 4; ++q)
+      v[q] = b0 + q < nblk ? part[(size_t)(b0 + q) * kRbPartF4 + u] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < kRbSeg / 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) d[e] += (double)v[q][e];
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) sp[sl][lane][e] = d[e];
+  __syncthreads();
+  if (sl == 0 && u < kRbPartF4) {
+    double* o = a.l2 + (((size_t)grp * nseg + seg) * kRbPartF4 + u) * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = ((sp[0][lane][e] + sp[1][lane][e]) + sp[2][lane][e]) + sp[3][lane][e];
+  }
+}
+
+__global__ void __launch_bounds__(256) stem_rc_sum2_kernel(StemRcArgs a, int nseg) {
+  __shared__ double sp[4][64][4];
+  __shared__ int flag;
+  const int tid = threadIdx.x, lane = tid & 63, sl = tid >> 6;
+  const int grp = blockIdx.y;
+  const int u = blockIdx.x * 64 + lane;
+  double d[4] = {0.0, 0.0, 0.0, 0.0};
+  if (u < kRbPartF4) {
+    for (int s = sl; s < nseg; s += 4) {
+      const double* o = a.l2 + (((size_t)grp * nseg + s) * kRbPartF4 + u) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) d[e] += o[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) sp[sl][lane][e] = d[e];
+  __syncthreads();
+  if (sl == 0 && u < kRbPartF4) {
+    double* o = a.tot + ((size_t)grp * kRbPartF4 + u) * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = ((sp[0][lane][e] + sp[1][lane][e]) + sp[2][lane][e]) + sp[3][lane][e];
+  }
+  if (!rb_arrive(a.tkt + grp, gridDim.x, &flag)) return;
+  stem_rc_finalize(a, grp);
 }
 
 // ---------------------------------------------------------------------------
@@ -932,6 +957,7 @@ int stem_rc_bwd_blocks(int N, int P, int Q, int Cout) {
   const int per = std::max(1, (total + want - 1) / want);
   return (total + per - 1) / per;
 }
+int stem_rc_tickets(int Cout) { return Cout / 64; }
 static int rc_nseg(int nblk) { return (nblk + kRbSeg - 1) / kRbSeg; }
 size_t stem_rc_part_bytes(int N, int P, int Q, int Cout) {
   const int nblk = stem_rc_bwd_blocks(N, P, Q, Cout), groups = Cout / 64;
@@ -946,7 +972,7 @@ size_t stem_rc_l2_offset(int N, int P, int Q, int Cout) {
 hipError_t launch_stem_rc_bwd(const StemRcArgs& a, int stage, hipStream_t st) {
   if (!stem_rc_ok(a.Cout, a.P, a.Q) || a.Pp * 2 != a.P || a.Qp * 2 != a.Q || a.H != 2 * a.P || a.W != 2 * a.Q ||
       !a.part || !a.l2 || !a.tot || !a.imsum || !a.dw || !a.bn.training || !a.bn.stats || a.lddpool % 8 || a.ldadd % 8 ||
-      !a.add || !a.dpool || !a.idx)
+      !a.add || !a.dpool || !a.idx || !a.tkt || stem_rc_tickets(a.Cout) > kStemTickets)
     return hipErrorInvalidValue;
   // 32-bit buffer offsets of the LDS-DMA (kOOB = 2^31 must lie past every range)
   if ((size_t)a.N * a.P * a.Q * a.ldadd * 2 >= kOOB || (size_t)a.N * a.Pp * a.Qp * a.lddpool * 2 >= kOOB ||
@@ -958,16 +984,15 @@ hipError_t launch_stem_rc_bwd(const StemRcArgs& a, int stage, hipStream_t st) {
   const int blocks = stem_rc_bwd_blocks(a.N, a.P, a.Q, a.Cout);
   const int per = (total + blocks - 1) / blocks;
   const int nseg = rc_nseg(blocks);
-  const int chunks = (kRbPartF4 + 63) / 64;
+  const int chunks = kRbChunks;
   if (stage == 0) {
     conv_kernel_tag("stem_rc_bwd_kernel");
     hipLaunchKernelGGL(stem_rc_imsum_kernel, dim3(kRcImBlocks), dim3(kRcImNT), 0, st, a);
     hipLaunchKernelGGL(stem_rc_bwd_kernel, dim3(blocks, groups), dim3(kRbNT), kRbLds, st, a, per);
   } else {
-    conv_kernel_tag("stem_rc_sum1/sum2/finalize");
+    conv_kernel_tag("stem_rc_sum1/sum2");
     hipLaunchKernelGGL(stem_rc_sum1_kernel, dim3(chunks, nseg, groups), dim3(256), 0, st, a, blocks, nseg);
     hipLaunchKernelGGL(stem_rc_sum2_kernel, dim3(chunks, groups), dim3(256), 0, st, a, nseg);
-    hipLaunchKernelGGL(stem_rc_finalize_kernel, dim3(groups), dim3(256), 0, st, a);
   }
   return hipGetLastError();
 }

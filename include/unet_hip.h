@@ -98,6 +98,11 @@ int unet_profile_enable(unet_plan* p, int on);
 int unet_profile_report(unet_plan* p, char* buf, int64_t buflen);
 
 /* ---- loss + metrics (kind: 0 bce, 1 dice, 2 combo) ---- */
+/* sums8 holds UNET_LOSS_SUMS_LEN doubles: [0..8) the sums (bce, sigma*y, sigma,
+ * y, tp, fp, fn, tn), the rest per-block partials that the library reduces in a
+ * fixed order (no atomics: the sums are bit-reproducible).  Nothing needs to be
+ * zeroed beforehand. */
+#define UNET_LOSS_SUMS_LEN (8 + 8 * 256)
 int unet_loss_forward(const float* logits, const float* target, int64_t n, int kind, float alpha,
                       float smooth, double* sums8, float* loss_out, hipStream_t stream);
 int unet_loss_backward(const float* logits, const float* target, int64_t n, int kind, float alpha,
