@@ -335,10 +335,7 @@ class UNetWithBackbone(nn.Module):
         plan.generation += 1
         rc = plan.lib.unet_forward(plan.handle, x.data_ptr(), pa, ba, plan.workspace.data_ptr(), logits.data_ptr(),
                                    1 if training else 0, _lib.stream_handle(x.device))
-        _lib.check(rc, "unet_forward")
-        if training:
-            nbt = [b for k, b in self.named_buffers() if k.endswith("num_batches_tracked")]
-            torch._foreach_add_(nbt, 1)
+        _lib.check(rc, "unet_forward")  # training: it also adds 1 to every num_batches_tracked
         return logits
 
     def _run_backward(self, plan, x, grad_logits):

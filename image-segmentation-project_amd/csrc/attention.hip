@@ -133,6 +133,7 @@ __global__ void __launch_bounds__(256) att_gate_fwd_kernel(AttGateArgs a) {
     const float unb = (float)((double)var * (n / (n > 1.0 ? n - 1.0 : 1.0)));
     a.run_mean[0] = (1.f - a.momentum) * a.run_mean[0] + a.momentum * mean;
     a.run_var[0] = (1.f - a.momentum) * a.run_var[0] + a.momentum * unb;
+    if (a.nbt) *a.nbt += 1;
   }
 }
 

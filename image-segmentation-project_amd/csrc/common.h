@@ -250,6 +250,7 @@ __device__ __forceinline__ void bn_finalize(const unet::BnLaunch& p) {
       const float unb = (float)((double)var * (n / (n > 1.0 ? n - 1.0 : 1.0)));
       p.run_mean[c] = (1.f - p.momentum) * p.run_mean[c] + p.momentum * m;
       p.run_var[c] = (1.f - p.momentum) * p.run_var[c] + p.momentum * unb;
+      if (c == 0 && p.nbt) *p.nbt += 1;  // exactly once per training forward, like the running stats
     }
   }
 }

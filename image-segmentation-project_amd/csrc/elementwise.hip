@@ -48,6 +48,7 @@ __device__ void bn_finalize_block0(const BnLaunch& p, int tid, int nthreads, int
       const float unb = (float)((double)var * (n / (n > 1.0 ? n - 1.0 : 1.0)));
       p.run_mean[c] = (1.f - p.momentum) * p.run_mean[c] + p.momentum * m;
       p.run_var[c] = (1.f - p.momentum) * p.run_var[c] + p.momentum * unb;
+      if (c == 0 && p.nbt) *p.nbt += 1;  // exactly once per training forward, like the running stats
     }
   }
 }
@@ -1124,6 +1125,19 @@ __global__ void __launch_bounds__(256) pack_kernel(PackTable t) {
         for (int j = sub; j < run; j += 4) dst[(size_t)j * A] = f2bf(lds[j * LD + lane]);
       }
     }
+    if (e.dst2) {  // forward layout from the same tile: element (a0+al, b0+bl, t) = lds[(bl*T + t)*LD + al]
+      const int nb = min(kPkTB, B - b0), na = min(kPkTA, A - a0);
+      const bool ch2 = e.kind2 == PK_CONV_FWD_CH;
+      const int bl = threadIdx.x % kPkTB, b = b0 + bl;  // 16 lanes write 16 consecutive b (32 B)
+      if (bl < nb)
+        for (int al = threadIdx.x / kPkTB; al < na; al += blockDim.x / kPkTB) {
+          const int a = a0 + al;
+          // fwd dst[b/32][t][a][b%32] (chunk-major) or dst[a][t][b]
+          bf16_t* d = ch2 ? e.dst2 + ((size_t)(b >> 5) * T * A + a) * 32 + (b & 31) : e.dst2 + (size_t)a * T * B + b;
+          const size_t dt = ch2 ? (size_t)A * 32 : (size_t)B;
+          for (int t = 0; t < T; ++t) d[t * dt] = f2bf(lds[(bl * T + t) * LD + al]);
+        }
+    }
     __syncthreads();
   }
 }
@@ -1133,6 +1147,9 @@ hipError_t launch_pack(const PackTable& t, hipStream_t st) {
   for (int i = 0; i < t.n; ++i) {
     const PackEntry& e = t.e[i];
     if (e.kind != PK_STEM && e.R * e.S > kPkTmax) return hipErrorInvalidValue;
+    if (e.dst2 && (!(e.kind == PK_CONV_DGRAD || e.kind == PK_CONV_DGRAD_CH) ||
+                   !(e.kind2 == PK_CONV_FWD || e.kind2 == PK_CONV_FWD_CH)))
+      return hipErrorInvalidValue;
   }
   hipLaunchKernelGGL(pack_kernel, dim3(256, t.n), dim3(256), 0, st, t);
   return hipGetLastError();

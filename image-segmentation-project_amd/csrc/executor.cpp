@@ -158,6 +158,9 @@ struct unet_plan {
   std::vector<std::vector<int>> bucket_convs;        // convs to unpack per bucket
   hipEvent_t events[8] = {};
   int nevents = 0;
+  // without bucket events (no DDP overlap) the buckets' unpack entries are
+  // collected here and launched together at the end of the backward
+  UnpackTable pend{};
   // The whole backward runs on the caller's stream.  Weight gradients on a
   // second stream and split-K reduces on a third were both measured slower on
   // MI355X (8.39 vs 7.86 ms/step; 2019 vs 2201 img/s: the LDS-heavy wgrad and
@@ -875,6 +878,8 @@ BnLaunch bn_launch(const Ctx& x, int bi, int64_t npix) {
   l.training = x.training;
   l.ss = x.p->bn_ticket ? x.W<float>(b.ss) : nullptr;
   l.ticket = x.p->bn_ticket ? x.W<unsigned>(b.tfwd) : nullptr;
+  // buffers are (running_mean, running_var, num_batches_tracked) per BN
+  l.nbt = x.buf && x.training ? reinterpret_cast<long long*>(x.buf[3 * b.idx + 2]) : nullptr;
   return l;
 }
 
@@ -1245,8 +1250,12 @@ int unpack_bucket(const Ctx& x, int bk, float* grads) {
   RUN(flush_reduce(x));
   if (x.rst != x.wst) RUN(stream_edge(x.p, x.rst, x.wst));  // every reduction so far is in dW
   ProfScope ps(x.p, x.wst, "unpack", 0);
-  UnpackTable t;
-  t.n = 0;
+  UnpackTable local;
+  local.n = 0;
+  // no bucket events: nothing waits for this bucket before the backward ends,
+  // so its entries join the pending table (fewer, fuller launches)
+  const bool defer = x.p->nevents == 0;
+  UnpackTable& t = defer ? x.p->pend : local;
   if (bk == 0) {
     // decoder (and attention W_g / W_x / psi) conv biases feed a training-mode
     // BN: their exact gradient is sum(dY) = 0 (BN removes the mean); written
@@ -1286,7 +1295,10 @@ int unpack_bucket(const Ctx& x, int bk, float* grads) {
     else { e.kind = UP_STEM; e.Co = cv.Co; e.Ci = 1; e.R = 7; e.S = 7; }
     if (t.n == kMaxPack) { CK(launch_unpack(t, x.wst)); t.n = 0; }
   }
-  CK(launch_unpack(t, x.wst));
+  if (!defer || bk == 3) {  // bucket 3 (the stem's) is the backward's last
+    CK(launch_unpack(t, x.wst));
+    t.n = 0;
+  }
   return 0;
 }
 
@@ -1307,6 +1319,7 @@ AttGateArgs gate_args(const Ctx& x, int l, float* grads) {
   a.gamma = x.prm[b.gamma]; a.beta = x.prm[b.beta];
   a.run_mean = x.buf ? x.buf[3 * b.idx + 0] : nullptr;
   a.run_var = x.buf ? x.buf[3 * b.idx + 1] : nullptr;
+  a.nbt = x.buf && x.training ? reinterpret_cast<long long*>(x.buf[3 * b.idx + 2]) : nullptr;
   a.npix = (int64_t)p->cfg.N * d.cat.H * d.cat.W;
   a.count = (double)a.npix; a.eps = p->cfg.bn_eps; a.momentum = p->cfg.bn_momentum; a.training = x.training;
   a.x = x.A(t.x); a.ldx = t.x.ld;
@@ -1424,13 +1437,16 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
       if (cv.kind == L_STEM) {
         t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_fwd), PK_STEM, cv.Co, 1, 7, 7};
       } else if (cv.kind == L_CONV) {
-        if (!cv.f8)
-          t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_fwd), cv.fl_fwd ? PK_CONV_FWD_CH : PK_CONV_FWD, cv.Co,
-                                 cv.Ci, cv.R, cv.S};
-        if (t.n == kMaxPack) RUN(flush());
-        if (training)
-          t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_dgrad), cv.fl_dgrad ? PK_CONV_DGRAD_CH : PK_CONV_DGRAD,
-                                 cv.Co, cv.Ci, cv.R, cv.S};
+        const int fk = cv.fl_fwd ? PK_CONV_FWD_CH : PK_CONV_FWD;
+        const int dk = cv.fl_dgrad ? PK_CONV_DGRAD_CH : PK_CONV_DGRAD;
+        if (training && !cv.f8) {  // both layouts from one read of the fp32 weight
+          t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_dgrad), dk, cv.Co, cv.Ci, cv.R, cv.S,
+                                 x.W<bf16_t>(cv.pk_fwd), fk};
+        } else {
+          if (!cv.f8) t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_fwd), fk, cv.Co, cv.Ci, cv.R, cv.S};
+          if (t.n == kMaxPack) RUN(flush());
+          if (training) t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_dgrad), dk, cv.Co, cv.Ci, cv.R, cv.S};
+        }
       } else {
         t.e[t.n++] = PackEntry{prm[cv.w], x.W<bf16_t>(cv.pk_fwd), PK_CONVT_FWD, cv.Co, cv.Ci, cv.R, cv.S};
         if (t.n == kMaxPack) RUN(flush());
@@ -1584,6 +1600,7 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
   Ctx x{p, ws, prm, nullptr, st, 1};
   const int N = p->cfg.N;
   wgrad_reset();  // nothing queued by an earlier backward that failed midway
+  p->pend.n = 0;
   p->wgb.clear();
   p->wgb_names.clear();
   p->wgb_flops = 0;

@@ -37,6 +37,7 @@ struct BnLaunch {
   double count; int C; float eps, momentum; int training;
   float* ss;          // [2][C] scale | shift (written by the finaliser)
   unsigned* ticket;   // zeroed per step; last arriving block finalises
+  long long* nbt;     // num_batches_tracked (int64), += 1 with channel 0's running stats; null: untouched
 };
 
 // backward: dZ = dA * (A > 0); sums over pixels of dZ and dZ*xhat (and for bn2)
@@ -353,13 +354,17 @@ hipError_t launch_d2f_strided(const double* src, float* dst, int n, int stride, 
 // (forward: K = Ci, Cout' = Co; data gradient: K = Co, Cout' = Ci)
 enum { PK_CONV_FWD = 0, PK_CONV_DGRAD = 1, PK_CONVT_FWD = 2, PK_CONVT_DGRAD = 3, PK_STEM = 4, PK_CONV_FWD_CH = 5,
        PK_CONV_DGRAD_CH = 6 };
-struct PackEntry { const float* src; bf16_t* dst; int kind, Co, Ci, R, S; };
+// dst2 / kind2 (optional, conv data-gradient kinds only): the same tile pass also
+// writes the forward layout kind2 (PK_CONV_FWD / PK_CONV_FWD_CH) to dst2, so a
+// training step reads each fp32 weight once for both packs
+struct PackEntry { const float* src; bf16_t* dst; int kind, Co, Ci, R, S; bf16_t* dst2; int kind2; };
 // UP_ZERO: dst[0 .. Co) = 0; UP_D2F: dst[i] = sum_r acc[r][i], acc fp64 [kStatRep][Co]
 enum { UP_CONV = 0, UP_CONVT = 1, UP_STEM = 2, UP_ZERO = 3, UP_D2F = 4 };
 struct UnpackEntry { const float* acc; float* dst; int kind, Co, Ci, R, S; };
-constexpr int kMaxPack = 48;
+constexpr int kMaxPack = 56;  // PackTable 3.1 KB of kernel arguments (< 4 KB)
 struct PackTable { int n; PackEntry e[kMaxPack]; };
 struct UnpackTable { int n; UnpackEntry e[kMaxPack]; };
+static_assert(sizeof(PackTable) <= 4096 && sizeof(UnpackTable) <= 4096, "tables travel as kernel arguments");
 hipError_t launch_pack(const PackTable& t, hipStream_t st);
 hipError_t launch_unpack(const UnpackTable& t, hipStream_t st);
 
@@ -401,6 +406,7 @@ struct AttGateArgs {
   double* pst; double* pbs;            // BN(1) fwd sums (sum, sumsq) / bwd sums (sum dZ, sum dZ phat)
   float* save;                         // mean, invstd
   const float* gamma; const float* beta; float* run_mean; float* run_var;
+  long long* nbt;     // num_batches_tracked of the psi BN (+= 1 with the running stats), or null
   double count; float eps, momentum; int training;
   const bf16_t* x; int ldx;            // skip activation (F_l channels)
   bf16_t* xatt; int ldxatt;            // x * psi (concat slice)

@@ -202,6 +202,7 @@ __global__ void __launch_bounds__(kRcNT) stem_rc_fwd_kernel(StemRcArgs a, int pe
         const float unb = (float)((double)var * (cnt / (cnt > 1.0 ? cnt - 1.0 : 1.0)));
         a.bn.run_mean[c] = (1.f - a.bn.momentum) * a.bn.run_mean[c] + a.bn.momentum * m;
         a.bn.run_var[c] = (1.f - a.bn.momentum) * a.bn.run_var[c] + a.bn.momentum * unb;
+        if (c == 0 && a.bn.nbt) *a.bn.nbt += 1;
       }
     }
   }

@@ -97,6 +97,9 @@ class GraphedTrainStep:
         self.model, self.criterion, self.optimizer = model, criterion, optimizer
         self.x = images.clone()
         self.y = masks.clone()
+        # the backward seed dL/dL = 1, made once in the warmup: loss.backward()
+        # would fill a fresh ones tensor inside every replay (one more kernel)
+        self._seed = None
         # the captured kernels write this plan's workspace, events and side
         # stream: keep it alive (and un-evictable) for the graph's lifetime
         self._plan = model._plan_for(self.x)
@@ -121,7 +124,9 @@ class GraphedTrainStep:
         out = self.model(self.x)
         loss = self.criterion(out, self.y)
         self.optimizer.zero_grad(set_to_none=True)
-        loss.backward()
+        if self._seed is None or self._seed.shape != loss.shape or self._seed.dtype != loss.dtype:
+            self._seed = torch.ones_like(loss)
+        loss.backward(self._seed)
         self.optimizer.step()
         return out, loss
 

@@ -73,8 +73,10 @@ int unet_plan_num_tensors(const unet_plan* p);
 int unet_plan_tensor_info(const unet_plan* p, int i, char* name, int namelen, int64_t info[5]);
 
 /* params[i]: fp32 tensors in unet_plan_param_name order (== reference
- * state_dict parameter order); buffers[3*k+0/1]: running_mean/var of BN k in
- * named_buffers order (num_batches_tracked slots are ignored). */
+ * state_dict parameter order); buffers[3*k+0/1/2]: running_mean/var (fp32) and
+ * num_batches_tracked (int64) of BN k in named_buffers order.  A training
+ * forward updates the running statistics and adds 1 to num_batches_tracked,
+ * as torch.nn.BatchNorm2d.train() does. */
 int unet_forward(unet_plan* p, const float* image, const float* const* params, float* const* buffers,
                  void* workspace, float* logits, int training, hipStream_t stream);
 /* grads: flat fp32 [unet_plan_grad_numel], param i at unet_plan_param_offset(i). */
