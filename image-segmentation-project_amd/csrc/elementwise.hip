@@ -1034,6 +1034,12 @@ __global__ void __launch_bounds__(256) pack_kernel(PackTable t) {
   // one LDS buffer for either path: [kPkTB*T][kPkTA+1] tile or a [B*T] row
   __shared__ float lds[kPkTB * kPkTmax * (kPkTA + 1)];
   static_assert(512 * kPkTmax <= kPkTB * kPkTmax * (kPkTA + 1), "row fits");
+  if (e.kind == PK_ZERO) {
+    uint4* d = reinterpret_cast<uint4*>(e.dst);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < e.Co; i += gridDim.x * blockDim.x)
+      d[i] = make_uint4(0, 0, 0, 0);
+    return;
+  }
   if (e.kind == PK_STEM) {  // dst[co][k], k = kr*8 + ks -> W[co][0][kr][ks] (kr, ks < 7; else 0)
     const int total = e.Co * 64;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {

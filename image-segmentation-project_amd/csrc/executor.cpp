@@ -1404,12 +1404,12 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
                        float* logits, int training, hipStream_t st) {
   Ctx x{p, ws, prm, buf, st, training};
   const int N = p->cfg.N;
-  if (training) {
-    CK(hipMemsetAsync(ws + p->zero_fwd_off, 0, p->zero_fwd_bytes + p->zero_bwd_bytes, st));
-    p->bwd_zeroed = true;
-  } else {
-    CK(hipMemsetAsync(ws + p->zero_fwd_off, 0, p->zero_fwd_bytes, st));
-  }
+  // the zeroed region: one PK_ZERO entry of the weight-pack launch below (the
+  // first kernel of the step) unless the fp8 kernels run before that launch
+  const size_t zbytes = p->zero_fwd_bytes + (training ? p->zero_bwd_bytes : 0);
+  const bool zero_in_pack = !p->f8n && zbytes % 16 == 0 && zbytes / 16 < (size_t)INT32_MAX;
+  if (!zero_in_pack) CK(hipMemsetAsync(ws + p->zero_fwd_off, 0, zbytes, st));
+  if (training) p->bwd_zeroed = true;
   if (p->f8n) {  // fp8 scale states: calibrate on the plan's first forward, else roll
     // (training only: an eval forward quantizes with the scales in use and
     // commits no amax, so validation never moves the training scales)
@@ -1427,6 +1427,8 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
   {
     PackTable t;
     t.n = 0;
+    if (zero_in_pack)
+      t.e[t.n++] = PackEntry{nullptr, reinterpret_cast<bf16_t*>(ws + p->zero_fwd_off), PK_ZERO, (int)(zbytes / 16), 0, 0, 0};
     auto flush = [&]() -> int {
       ProfScope ps(p, st, "pack", 0);
       CK(launch_pack(t, st));

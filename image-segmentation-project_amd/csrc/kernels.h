@@ -352,8 +352,9 @@ hipError_t launch_d2f_strided(const double* src, float* dst, int n, int stride, 
 // weight (un)packing between torch fp32 layouts and kernel bf16 layouts
 // PK_CONV_*_CH: 3x3 convs of conv3x3_fl_kernel, chunk-major [K/32][9][Cout'][32]
 // (forward: K = Ci, Cout' = Co; data gradient: K = Co, Cout' = Ci)
+// PK_ZERO: 16-B units dst[0 .. Co) = 0 (the step's zeroed workspace region, no fill launch)
 enum { PK_CONV_FWD = 0, PK_CONV_DGRAD = 1, PK_CONVT_FWD = 2, PK_CONVT_DGRAD = 3, PK_STEM = 4, PK_CONV_FWD_CH = 5,
-       PK_CONV_DGRAD_CH = 6 };
+       PK_CONV_DGRAD_CH = 6, PK_ZERO = 7 };
 // dst2 / kind2 (optional, conv data-gradient kinds only): the same tile pass also
 // writes the forward layout kind2 (PK_CONV_FWD / PK_CONV_FWD_CH) to dst2, so a
 // training step reads each fp32 weight once for both packs
