@@ -1784,12 +1784,17 @@ __device__ __forceinline__ int wb_block_of(const WgBatchArgs& a, long long it) {
 // dW of every unit spread over several blocks = the sum of its partials in
 // block order; grid (units, 36): 256 threads x one f32x4 element of the unit's
 // 9216-element (8 waves x 18 fragments x 64 lanes) SLAB_HALO partial each.
+// Block y takes fragment y % 18 of the four compute waves wn of half wm = y / 18:
+// one tap's 16 output channels x all 64 input channels, so after a transpose
+// through LDS every thread stores 4 consecutive input channels and 16 lanes
+// write one 256-B dW row segment (the fragment-order stores wrote 64-B pieces).
 // The unit's slab slots (one per block it spans, <= grid <= 256) are located
 // once per block, one thread per spanned block, into LDS; every thread then
 // streams its element of those partials with 8 loads in flight and adds them
 // in block order (the order, hence the bits, of a serial loop)
 __global__ void __launch_bounds__(256) wgrad_batch_reduce_kernel(WgBatchArgs a) {
   __shared__ int slots[256];
+  __shared__ float tile[16][65];
   const int u = blockIdx.x;
   int l = 0;
   while (l + 1 < a.nl && u >= a.L[l + 1].unit0) ++l;
@@ -1811,7 +1816,8 @@ __global__ void __launch_bounds__(256) wgrad_batch_reduce_kernel(WgBatchArgs a) 
     slots[threadIdx.x] = slot;
   }
   __syncthreads();
-  const int q = blockIdx.y * 256 + threadIdx.x;
+  const int wm = blockIdx.y / 18, frag = blockIdx.y % 18, wn = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int q = ((wm + 2 * wn) * 18 + frag) * 64 + lane;
   const f32x4* slab = reinterpret_cast<const f32x4*>(a.slab) + q;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   for (int j0 = 0; j0 < nb; j0 += 8) {
@@ -1826,15 +1832,16 @@ __global__ void __launch_bounds__(256) wgrad_batch_reduce_kernel(WgBatchArgs a) 
     for (int k = 0; k < 8; ++k)
       if (sl[k] >= 0) acc += v[k];
   }
-  const int lane = q & 63, r = q >> 6;
-  const int frag = r % 18, wave = r / 18;
-  const int t = frag >> 1, i = frag & 1, wm = wave & 1, wn = wave >> 1;
+  const int t = frag >> 1, i = frag & 1;
   const int g = lane >> 4, li = lane & 15;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) tile[4 * g + e][wn * 16 + li] = acc[e];
+  __syncthreads();
   const int co0 = (combo % L.co_blocks) * 64, c0 = (combo / L.co_blocks) * 64;
   const int Krow = 9 * L.C;
-  const int c = c0 + wn * 16 + li;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) L.dw[(size_t)(co0 + wm * 32 + i * 16 + 4 * g + e) * Krow + t * L.C + c] = acc[e];
+  const int col = threadIdx.x >> 4, c4 = (threadIdx.x & 15) * 4;  // output channel, 4 input channels
+  const float4 o = make_float4(tile[col][c4], tile[col][c4 + 1], tile[col][c4 + 2], tile[col][c4 + 3]);
+  *reinterpret_cast<float4*>(L.dw + (size_t)(co0 + wm * 32 + i * 16 + col) * Krow + t * L.C + c0 + c4) = o;
 }
 
 // dW = sum over the splits of the slab (slab_reduce_block, common.h)
