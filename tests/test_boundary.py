@@ -175,3 +175,13 @@ def test_importable_alias_and_reference_layout_modules(pkg):
         sys.path.remove(os.path.join(REPO, "dropin"))
         for name in ("advanced_models", "losses", "train", "utils"):
             sys.modules.pop(name, None)
+
+
+def test_loss_sums_buffer_length_matches_header(pkg):
+    """losses.py / utils.py size the loss-sums buffer from _lib.LOSS_SUMS_LEN;
+    the library writes UNET_LOSS_SUMS_LEN doubles (8 sums + per-block partials)."""
+    lib_mod = importlib.import_module("image-segmentation-project_amd._lib")
+    src = open(os.path.join(REPO, "include", "unet_hip.h")).read()
+    m = re.search(r"#define\s+UNET_LOSS_SUMS_LEN\s+\(8 \+ 8 \* (\d+)\)", src)
+    assert m, "UNET_LOSS_SUMS_LEN not found in include/unet_hip.h"
+    assert lib_mod.LOSS_SUMS_LEN == 8 + 8 * int(m.group(1))
