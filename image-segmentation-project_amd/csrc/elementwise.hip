@@ -61,7 +61,10 @@ __device__ void bn_finalize_block0(const BnLaunch& p, int tid, int nthreads, int
 // registers).  kBnPPT pixels per thread per pass; the first pass's loads are
 // issued BEFORE the coefficient prologue so the two latencies overlap.
 constexpr int kBnCG = 64;
-constexpr int kBnPPT = 4;
+#ifndef UNET_BN_PPT
+#define UNET_BN_PPT 2
+#endif
+constexpr int kBnPPT = UNET_BN_PPT;  // (variant builds: make variant VDEF=-DUNET_BN_PPT=n)
 __host__ __device__ __forceinline__ int bn_group(int C) { return C % kBnCG == 0 ? kBnCG : C; }
 
 template <int RES, bool RELU>
