@@ -14,7 +14,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # UNET_HIP_LIB: an alternative in-tree build for A/B measurements (scripts/)
 LIB_PATH = os.environ.get("UNET_HIP_LIB") or os.path.join(_HERE, "libunet_hip.so")
-LOSS_SUMS_LEN = 8 + 8 * 256  # UNET_LOSS_SUMS_LEN (include/unet_hip.h): 8 sums + per-block partials
+LOSS_SCRATCH_LEN = 8 * 256  # UNET_LOSS_SCRATCH_LEN (include/unet_hip.h): per-block partials of the loss sums
 
 _lib = None
 
@@ -55,10 +55,10 @@ SIGNATURES = {
     "unet_timing_read": (c_int64, [c_void_p, c_void_p, c_int64, ctypes.c_char_p, c_int64]),
     "unet_profile_report": (c_int, [c_void_p, ctypes.c_char_p, c_int64]),
     "unet_loss_forward": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_float, c_float, c_void_p, c_void_p,
-                                  c_void_p]),
+                                  c_int64, c_void_p, c_void_p]),
     "unet_loss_backward": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_float, c_float, c_void_p, c_void_p,
                                    c_void_p, c_void_p]),
-    "unet_mask_metrics": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
+    "unet_mask_metrics": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_int64, c_void_p]),
     "unet_adam_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float,
                                c_float, c_float, c_int, c_void_p]),
     "unet_grad_to_bf16": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
@@ -66,6 +66,9 @@ SIGNATURES = {
     "unet_conv_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]
                       + [c_int] * 12 + [c_void_p]),
     "unet_conv_wgrad": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p] + [c_int] * 12 + [c_void_p]),
+    "unet_conv3x3_fl": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                                c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                c_void_p, c_void_p, c_void_p] + [c_int] * 8 + [c_void_p]),
     "unet_f8_quantize": (c_int, [c_void_p, c_int, c_int, c_int64, c_void_p, c_void_p, c_int, c_void_p]),
     "unet_f8_pack_weight": (c_int, [c_void_p] + [c_int] * 4 + [c_void_p, c_void_p, c_int, c_void_p]),
     "unet_f8_roll": (c_int, [c_void_p, c_int, c_void_p]),
@@ -129,6 +132,13 @@ def require_gpu(*tensors):
 
 def stream_handle(device=None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
+
+
+def loss_buffers(device):
+    """(sums [8], scratch [LOSS_SCRATCH_LEN]) fp64 device buffers of one
+    unet_loss_forward / unet_mask_metrics call (one allocation)."""
+    buf = torch.empty(8 + LOSS_SCRATCH_LEN, dtype=torch.float64, device=device)
+    return buf[:8], buf[8:]
 
 
 def ptr(t) -> int:

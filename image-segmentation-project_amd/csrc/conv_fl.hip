@@ -515,22 +515,17 @@ __global__ void __launch_bounds__(kNW * 64) conv3x3_fl_kernel(ConvFwdArgs a, int
   TSTAMP_RT_TH(a.tim, 31, LT);
 }
 
-static int g_cus = 0;
-static int cu_count() {
-  if (!g_cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                 hipSuccess || g_cus <= 0)
-      g_cus = 256;
-  }
-  return g_cus;
-}
+static int cu_count() { return device_cu_count(); }
 
 // shapes the kernel covers AND fills: at least one 16 x 16 x 64 work item per
 // CU (enc4 at 512^2 has 128: it stays on the 32-channel halo-streamed kernel)
+bool conv3x3_fl_geom(int C, int Cout, int P, int Q) {
+  return C > 0 && Cout > 0 && P > 0 && Q > 0 && C % 128 == 0 && Cout % kCOT == 0 && P % kTH == 0 && Q % 16 == 0;
+}
+
 bool conv3x3_fl_shape(int N, int C, int Cout, int P, int Q) {
   static const bool off = std::getenv("UNET_NO_FL") != nullptr;  // A/B: the halo-streamed kernel
-  if (off || C % 128 || Cout % kCOT || P % kTH || Q % 16) return false;
+  if (off || !conv3x3_fl_geom(C, Cout, P, Q)) return false;
   return (long long)N * (P / kTH) * (Q / 16) * (Cout / kCOT) >= cu_count();
 }
 
@@ -539,7 +534,7 @@ hipError_t launch_conv3x3_fl(const ConvFwdArgs& a, int mode, hipStream_t st) {
   const bool flip = mode == 1;
   if (!a.wch || a.R != 3 || a.S != 3 || a.stride != 1 || a.pad != 1 || a.x2 || a.ysplit || a.xform)
     return hipErrorInvalidValue;
-  if (a.H != a.P || a.W != a.Q || !conv3x3_fl_shape(a.N, a.C, a.Cout, a.P, a.Q)) return hipErrorInvalidValue;
+  if (a.N <= 0 || a.H != a.P || a.W != a.Q || !conv3x3_fl_geom(a.C, a.Cout, a.P, a.Q)) return hipErrorInvalidValue;
   if (a.ldx % 8 || a.ldy % 8 || (a.add && a.ldadd % 8)) return hipErrorInvalidValue;
   if (flip && (a.fold_on || a.stats || (a.bb.sums && (a.bb.ldact % 8 || a.bb.ldy % 8 ||
                                                      (a.bb.y2 && a.bb.ldy2 % 8)))))
@@ -553,6 +548,7 @@ hipError_t launch_conv3x3_fl(const ConvFwdArgs& a, int mode, hipStream_t st) {
   // persistent grid: one block per CU, a multiple of ncb so that every block
   // keeps one output-channel block
   int grid = cu_count() / ncb * ncb;
+  if (a.grid_cap > 0 && a.grid_cap < grid) grid = a.grid_cap / ncb * ncb;
   if (grid < ncb) grid = ncb;
   if (grid > nitems) grid = nitems;
   const bool two = flip && a.bb.sums && a.bb.y2;
@@ -1035,6 +1031,7 @@ hipError_t launch_conv3x3_ws2(const ConvFwdArgs& a, int mode, hipStream_t st) {
   const int ncb = a.Cout / kCOT;
   const int nitems = a.N * (a.P / kTH) * (a.Q / 16) * ncb;
   int grid = cu_count() / ncb * ncb;
+  if (a.grid_cap > 0 && a.grid_cap < grid) grid = a.grid_cap / ncb * ncb;
   if (grid < ncb) grid = ncb;
   if (grid > nitems) grid = nitems;
   const bool fbwd = flip && a.bb.sums;

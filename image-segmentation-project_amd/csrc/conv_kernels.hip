@@ -1793,7 +1793,7 @@ __device__ __forceinline__ int wb_block_of(const WgBatchArgs& a, long long it) {
 // streams its element of those partials with 8 loads in flight and adds them
 // in block order (the order, hence the bits, of a serial loop)
 __global__ void __launch_bounds__(256) wgrad_batch_reduce_kernel(WgBatchArgs a) {
-  __shared__ int slots[256];
+  __shared__ int slots[kWbMaxGrid];
   __shared__ float tile[16][65];
   const int u = blockIdx.x;
   int l = 0;
@@ -2623,15 +2623,25 @@ bool wgrad_batch_ok(const ConvWgradArgs& a) {
          (size_t)a.N * a.P * a.Q * a.lddy * 2 < 0x80000000ull;
 }
 
-int wgrad_batch_grid() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                 hipSuccess || cus <= 0)
-      cus = 256;
+// CU count of the CURRENT device, cached per device id (the persistent grids
+// are sized from it; a plan is bound to the device current at its creation)
+int device_cu_count() {
+  static int cus[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (!cus[dev]) {
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+    cus[dev] = c;
   }
-  return cus;
+  return cus[dev];
+}
+
+// one block per CU, at most kWbMaxGrid: the reduce collects a split unit's
+// slot list in a kWbMaxGrid-entry LDS table
+int wgrad_batch_grid() {
+  const int c = device_cu_count();
+  return c < kWbMaxGrid ? c : kWbMaxGrid;
 }
 
 // largest number of units any block of the batch touches (its slab slots)
@@ -2658,6 +2668,7 @@ static void launch_wgrad_batch_tw(const WgBatchArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_wgrad_batch(const WgBatchArgs& a, hipStream_t st) {
+  if (a.grid <= 0 || a.grid > kWbMaxGrid) return hipErrorInvalidValue;  // slots[] of the reduce
   if (a.tw == 32) launch_wgrad_batch_tw<32>(a, st);
   else if (a.tw == 16) launch_wgrad_batch_tw<16>(a, st);
   else return hipErrorInvalidValue;

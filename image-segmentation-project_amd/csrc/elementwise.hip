@@ -1307,7 +1307,7 @@ __device__ __forceinline__ void loss_accum(float v, float y, int from_prob, floa
 // stays at <= 256 (same-address fp64 atomics are serialised)
 constexpr int kLossNT = 1024;
 __global__ void __launch_bounds__(kLossNT) loss_sums_kernel(const float* x, const float* t, int64_t n,
-                                                            double* sums, int from_prob) {
+                                                            double* part, int from_prob) {
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1354,19 +1354,19 @@ __global__ void __launch_bounds__(kLossNT) loss_sums_kernel(const float* x, cons
     const int k = threadIdx.x;
     double v = 0.0;
     for (int w = 0; w < kLossNT / 64; ++w) v += red[w][k];
-    sums[8 + blockIdx.x * 8 + k] = v;
+    part[blockIdx.x * 8 + k] = v;
   }
 }
 
-// sums[k] = sum over blocks b (in order, 64 lanes then a fixed butterfly) of
-// the partial sums[8 + 8 b + k]; wave k owns value k.  Thread 0 then writes the
+// s[k] = sum over blocks b (in order, 64 lanes then a fixed butterfly) of
+// the partial part[8 b + k]; wave k owns value k.  Thread 0 then writes the
 // loss value when `out` is given.
-__global__ void __launch_bounds__(512) loss_reduce_kernel(double* s, int nblk, int64_t n, int kind, float alpha,
-                                                          float smooth, float* out) {
+__global__ void __launch_bounds__(512) loss_reduce_kernel(double* s, const double* part, int nblk, int64_t n,
+                                                          int kind, float alpha, float smooth, float* out) {
   __shared__ double tot[8];
   const int k = threadIdx.x >> 6, lane = threadIdx.x & 63;
   double v = 0.0;
-  for (int b = lane; b < nblk; b += 64) v += s[8 + b * 8 + k];
+  for (int b = lane; b < nblk; b += 64) v += part[b * 8 + k];
   v = wave_sum_d(v);
   if (lane == 0) {
     s[k] = v;
@@ -1383,13 +1383,14 @@ __global__ void __launch_bounds__(512) loss_reduce_kernel(double* s, int nblk, i
   *out = (float)r;
 }
 
-hipError_t launch_loss_sums(const float* logits, const float* target, int64_t n, double* sums, int from_prob,
-                            int kind, float alpha, float smooth, float* out, hipStream_t st) {
+hipError_t launch_loss_sums(const float* logits, const float* target, int64_t n, double* sums, double* part,
+                            int from_prob, int kind, float alpha, float smooth, float* out, hipStream_t st) {
   const int nblk = grid_for(n, kLossNT * 16, kLossBlocks);
-  hipLaunchKernelGGL(loss_sums_kernel, dim3(nblk), dim3(kLossNT), 0, st, logits, target, n, sums, from_prob);
+  if (nblk > kLossBlocks) return hipErrorInvalidValue;  // part holds kLossBlocks slots
+  hipLaunchKernelGGL(loss_sums_kernel, dim3(nblk), dim3(kLossNT), 0, st, logits, target, n, part, from_prob);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(512), 0, st, sums, nblk, n, kind, alpha, smooth, out);
+  hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(512), 0, st, sums, part, nblk, n, kind, alpha, smooth, out);
   return hipGetLastError();
 }
 

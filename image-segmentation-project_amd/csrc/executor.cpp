@@ -150,7 +150,8 @@ struct unet_plan {
   size_t zero_bwd_off = 0, zero_bwd_bytes = 0;
   // a training forward zeroes the backward's region too (it follows the
   // forward's, one fill instead of two); the next backward then skips its fill
-  bool bwd_zeroed = false;
+  bool bwd_zeroed = false;          // the last training forward zeroed the backward accumulators ...
+  const char* bwd_zeroed_ws = nullptr;  // ... of this workspace
   size_t head_usum = 0;
   size_t wslab = 0, wslab_bytes = 0;  // split-K partials of the halo weight-gradient kernel
   int64_t grad_numel = 0;
@@ -827,7 +828,11 @@ static int build_plan(unet_plan* p) {
   p->flops_fwd = fw;
   p->flops_train = 3 * fw - stem;
 
-  return 0;  // bucket events are created lazily (plan creation needs no GPU)
+  // bucket events are created lazily; plan creation does query the current
+  // device's CU count (device_cu_count: the full-line conv routing and the
+  // chunk-major packs depend on it), so it initialises the HIP runtime and the
+  // plan is bound to the device current at creation
+  return 0;
 }
 
 static int ensure_events(unet_plan* p) {
@@ -1409,7 +1414,10 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
   const size_t zbytes = p->zero_fwd_bytes + (training ? p->zero_bwd_bytes : 0);
   const bool zero_in_pack = !p->f8n && zbytes % 16 == 0 && zbytes / 16 < (size_t)INT32_MAX;
   if (!zero_in_pack) CK(hipMemsetAsync(ws + p->zero_fwd_off, 0, zbytes, st));
-  if (training) p->bwd_zeroed = true;
+  // the backward accumulators were zeroed for THIS workspace (an eval forward or
+  // another workspace makes the next unet_backward zero them itself)
+  p->bwd_zeroed = training != 0;
+  p->bwd_zeroed_ws = training ? ws : nullptr;
   if (p->f8n) {  // fp8 scale states: calibrate on the plan's first forward, else roll
     // (training only: an eval forward quantizes with the scales in use and
     // commits no amax, so validation never moves the training scales)
@@ -1612,8 +1620,9 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
   p->syncused = 0;
   // fork: the weight stream starts after the zeroing of the accumulators
   auto fork = [&]() { return stream_edge(p, st, x.wst); };
-  if (!p->bwd_zeroed) CK(hipMemsetAsync(ws + p->zero_bwd_off, 0, p->zero_bwd_bytes, st));
+  if (!p->bwd_zeroed || p->bwd_zeroed_ws != ws) CK(hipMemsetAsync(ws + p->zero_bwd_off, 0, p->zero_bwd_bytes, st));
   p->bwd_zeroed = false;
+  p->bwd_zeroed_ws = nullptr;
   const bool att = !p->atts.empty();
   // head (upconv0 + conv_final)
   {
@@ -2029,11 +2038,23 @@ int unet_bucket_wait(unet_plan* p, int bucket, hipStream_t waiter) {
   return 0;
 }
 
-static_assert(UNET_LOSS_SUMS_LEN == 8 + 8 * kLossBlocks, "loss partial slots");
+static_assert(UNET_LOSS_SCRATCH_LEN == 8 * kLossBlocks, "loss partial slots");
+
+static bool loss_bufs_ok(const char* fn, const double* sums8, const double* scratch, int64_t scratch_len) {
+  if (!sums8 || !scratch || scratch_len < UNET_LOSS_SCRATCH_LEN) {
+    char m[160];
+    std::snprintf(m, sizeof(m), "%s: sums8 / scratch null or scratch_len %lld < UNET_LOSS_SCRATCH_LEN (%d)", fn,
+                  (long long)scratch_len, UNET_LOSS_SCRATCH_LEN);
+    set_err(m);
+    return false;
+  }
+  return true;
+}
 
 int unet_loss_forward(const float* logits, const float* target, int64_t n, int kind, float alpha, float smooth,
-                      double* sums8, float* loss_out, hipStream_t stream) {
-  CK(launch_loss_sums(logits, target, n, sums8, 0, kind, alpha, smooth, loss_out, stream));
+                      double* sums8, double* scratch, int64_t scratch_len, float* loss_out, hipStream_t stream) {
+  if (!loss_bufs_ok("unet_loss_forward", sums8, scratch, scratch_len)) return 1;
+  CK(launch_loss_sums(logits, target, n, sums8, scratch, 0, kind, alpha, smooth, loss_out, stream));
   return 0;
 }
 
@@ -2044,8 +2065,9 @@ int unet_loss_backward(const float* logits, const float* target, int64_t n, int 
 }
 
 int unet_mask_metrics(const float* values, const float* target, int64_t n, int values_are_prob, double* sums8,
-                      hipStream_t stream) {
-  CK(launch_loss_sums(values, target, n, sums8, values_are_prob, 0, 0.f, 0.f, nullptr, stream));
+                      double* scratch, int64_t scratch_len, hipStream_t stream) {
+  if (!loss_bufs_ok("unet_mask_metrics", sums8, scratch, scratch_len)) return 1;
+  CK(launch_loss_sums(values, target, n, sums8, scratch, values_are_prob, 0, 0.f, 0.f, nullptr, stream));
   return 0;
 }
 
@@ -2088,6 +2110,40 @@ int unet_conv_fwd(const void* x, int ldx, const void* w, void* y, int ldy, const
   a.R = R; a.S = S; a.stride = stride; a.pad = pad;
   if (mode < 0 || mode > 2) { set_err("bad mode"); return 1; }
   CK(launch_conv_fwd(a, mode, stream));
+  return 0;
+}
+
+int unet_conv3x3_fl(const void* x, int ldx, const void* wch, void* y, int ldy, const float* bias, const void* addend,
+                    int ldadd, double* stats, const void* act, int ldact, const void* yraw, int ldyraw,
+                    const float* mean, const float* invstd, const void* yraw2, int ldyraw2, const float* mean2,
+                    const float* invstd2, double* bsums, double* bsums2, int N, int H, int W, int C, int Cout,
+                    int mode, int grid, hipStream_t stream) {
+  if (mode != 0 && mode != 1) { set_err("unet_conv3x3_fl: mode must be 0 (conv) or 1 (data gradient)"); return 1; }
+  if (!conv3x3_fl_geom(C, Cout, H, W) || N <= 0) {
+    set_err("unet_conv3x3_fl: needs C % 128 == 0, Cout % 64 == 0, H % 16 == 0, W % 16 == 0, N > 0");
+    return 1;
+  }
+  if (mode == 0 && bsums) { set_err("unet_conv3x3_fl: the fused BN backward is a data-gradient epilogue"); return 1; }
+  if (bsums && (!act || !yraw || !mean || !invstd || (yraw2 && (!mean2 || !invstd2 || !bsums2)))) {
+    set_err("unet_conv3x3_fl: fused BN backward needs act, yraw, mean, invstd (and mean2, invstd2, bsums2 with yraw2)");
+    return 1;
+  }
+  ConvFwdArgs a = {};
+  a.x = (const bf16_t*)x; a.ldx = ldx; a.wch = (const bf16_t*)wch; a.y = (bf16_t*)y; a.ldy = ldy;
+  a.bias = bias; a.add = (const bf16_t*)addend; a.ldadd = ldadd; a.stats = mode == 0 ? stats : nullptr;
+  a.N = N; a.H = H; a.W = W; a.C = C; a.P = H; a.Q = W; a.Cout = Cout;
+  a.R = 3; a.S = 3; a.stride = 1; a.pad = 1;
+  a.grid_cap = grid;
+  if (bsums) {
+    a.bb.act = (const bf16_t*)act; a.bb.ldact = ldact; a.bb.y = (const bf16_t*)yraw; a.bb.ldy = ldyraw;
+    a.bb.mean = mean; a.bb.invstd = invstd; a.bb.sums = bsums;
+    a.bb.npix = (int64_t)N * H * W; a.bb.C = Cout; a.bb.relu = 1;
+    if (yraw2) {
+      a.bb.y2 = (const bf16_t*)yraw2; a.bb.ldy2 = ldyraw2; a.bb.mean2 = mean2; a.bb.invstd2 = invstd2;
+      a.bb.sums2 = bsums2;
+    }
+  }
+  CK(launch_conv3x3_fl(a, mode, stream));
   return 0;
 }
 
@@ -2159,6 +2215,12 @@ int unet_convt_wgrad_slab(const void* dy, int lddy, const void* x, int ldx, floa
 }
 
 int unet_pack_weight(const float* src, void* dst, int kind, int Co, int Ci, int R, int S, hipStream_t stream) {
+  if (kind < PK_CONV_FWD || kind > PK_CONV_DGRAD_CH) { set_err("unet_pack_weight: kind must be 0..6"); return 1; }
+  if ((kind == PK_CONV_FWD_CH || kind == PK_CONV_DGRAD_CH) &&
+      (R != 3 || S != 3 || Co % 32 || Ci % 32)) {
+    set_err("unet_pack_weight: chunk-major packs are 3x3 with Co, Ci multiples of 32");
+    return 1;
+  }
   PackTable t;
   t.n = 1;
   t.e[0] = PackEntry{src, (bf16_t*)dst, kind, Co, Ci, R, S};

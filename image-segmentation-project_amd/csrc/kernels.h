@@ -7,6 +7,10 @@ namespace unet {
 
 typedef unsigned short bf16_t;
 
+// CU count of the current device (cached per device id; queried on first use,
+// which initialises the HIP runtime: unet_plan_create calls it)
+int device_cu_count();
+
 // in-kernel phase timing buffer geometry (common.h TSTAMP, debug build only)
 constexpr int kTimBlocks = 1024, kTimSlots = 32, kTimLaunches = 320;
 
@@ -105,6 +109,9 @@ struct ConvFwdArgs {
   int P, Q, Cout;                // output geometry
   int R, S, stride, pad;
   int mblocks, nblocks, Pc, Qc;  // filled by the launcher
+  // persistent kernels (conv3x3_fl_kernel): 0 = one block per CU; > 0 caps the
+  // grid (single-op tests: several work items per block)
+  int grid_cap;
   // in-kernel phase stamps (debug build -DUNET_TIMING only, null otherwise):
   // [block < kTimBlocks][kTimSlots] s_memtime values (scripts/conv_timing.py)
   unsigned long long* tim;
@@ -166,6 +173,9 @@ bool conv3x3_ws_xform_ok(const ConvFwdArgs& a);
 // (PK_CONV_FWD_CH / PK_CONV_DGRAD_CH); mode 0 conv, 1 dgrad.  The plan packs
 // those convs chunk-major exactly when conv3x3_fl_shape holds (UNET_NO_FL=1: never)
 bool conv3x3_fl_shape(int N, int C, int Cout, int P, int Q);
+// the geometry alone (what launch_conv3x3_fl accepts; the single-op C ABI may
+// launch shapes that do not fill the chip)
+bool conv3x3_fl_geom(int C, int Cout, int P, int Q);
 hipError_t launch_conv3x3_fl(const ConvFwdArgs& a, int mode, hipStream_t st);
 // weight-stationary full-line conv for C == 64 (conv_fl.hip), standard weight
 // pack; launch_conv3x3_ws uses it where conv3x3_ws2_ok holds (UNET_NO_WS2=1: never)
@@ -240,7 +250,8 @@ struct WgBatchArgs {
 bool wgrad_batch_ok(const ConvWgradArgs& a);
 int wgrad_batch_tw(const ConvWgradArgs& a);  // the batch tile width of a layer (0: not batchable)
 constexpr size_t kWbPartBytes = 8 * 18 * 64 * 16;  // one block's 64 x 64 x 9 fp32 partial (SLAB_HALO layout)
-// the grid of a batch (one block per CU) and the largest slab slot count it needs
+// the grid of a batch (one block per CU, at most kWbMaxGrid) and the largest slab slot count it needs
+constexpr int kWbMaxGrid = 256;
 int wgrad_batch_grid();
 int wgrad_batch_maxseg(const WgBatchArgs& a);
 hipError_t launch_wgrad_batch(const WgBatchArgs& a, hipStream_t st);
@@ -371,10 +382,10 @@ hipError_t launch_unpack(const UnpackTable& t, hipStream_t st);
 
 // loss + metrics
 enum { LOSS_BCE = 0, LOSS_DICE = 1, LOSS_COMBO = 2 };
-// sums[0..8): sum bce, sum sig*y, sum sig, sum y, tp, fp, fn, tn; sums[8..8+8*kLossBlocks):
-// per-block partials (UNET_LOSS_SUMS_LEN doubles in all).  out != nullptr: also the loss value.
+// sums[0..8): sum bce, sum sig*y, sum sig, sum y, tp, fp, fn, tn; part[0..8*kLossBlocks):
+// per-block partials (UNET_LOSS_SCRATCH_LEN doubles).  out != nullptr: also the loss value.
 constexpr int kLossBlocks = 256;
-hipError_t launch_loss_sums(const float* logits, const float* target, int64_t n, double* sums,
+hipError_t launch_loss_sums(const float* logits, const float* target, int64_t n, double* sums, double* part,
                             int from_prob, int kind, float alpha, float smooth, float* out, hipStream_t st);
 hipError_t launch_loss_grad(const float* logits, const float* target, int64_t n, const double* sums,
                             int kind, float alpha, float smooth, const float* gscale, float* dl,

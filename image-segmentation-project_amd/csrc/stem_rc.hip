@@ -7,14 +7,15 @@
 //
 //   stats pass   conv -> BN batch sums (fp64 replica atomics, last block
 //                finalises scale/shift/save/running stats as stem_fwd did)
-//   apply pass   conv -> bf16 y -> relu(y * scale + shift) = act (the
+//   apply pass   conv -> fp32 y -> relu(y * scale + shift) = act (the
 //                decoder1 skip, stored once) -> MaxPool(3,2,1) of act in LDS
 //                -> pooled + argmax index.  A block walks pooled rows, keeping
 //                the last three act rows in an LDS ring; its first pooled row
 //                recomputes the act row above it (owned by the previous block).
-//   backward     conv -> y, xhat; dZ = [act > 0] (maxpool scatter of dpool +
-//                the skip gradient) -- maxpool_bwd's expression, bit-identical
-//                dZ -- and, in the same pass, the stem weight gradient through
+//   backward     conv -> fp32 y -> ReLU mask bit and xhat; dZ = [act > 0]
+//                (maxpool scatter of dpool + the skip gradient) --
+//                maxpool_bwd's expression -- and, in the same pass, the stem
+//                weight gradient through
 //                the BN-backward identity
 //                  dY = k1 dZ - k1 m1 - k1 m2 xhat       (k1 = gamma invstd,
 //                  m1 = mean dZ, m2 = mean dZ xhat), so
@@ -149,7 +150,10 @@ __device__ __forceinline__ void lds_sync() {
   asm volatile("" ::: "memory");
 }
 
-// act = bf16(relu(y * sc + sh)) of a bf16-rounded y (bn_relu_maxpool_fwd's expression)
+// act = bf16(relu(y * sc + sh)) of the fp32 conv output y (round 6: the
+// stored-y0 path, bn_relu_maxpool_fwd, necessarily normalises a bf16 y; the
+// recompute passes hold y in fp32 and normalise it as the reference's fp32
+// BatchNorm does, advanced_models.py:81-83)
 __device__ __forceinline__ float stem_act(float y, float sc, float sh) {
   const float z = y * sc + sh;
   return bf2f(f2bf(z > 0.f ? z : 0.f));
@@ -265,7 +269,7 @@ __global__ void __launch_bounds__(kRcNT) stem_rc_fwd_kernel(StemRcArgs a, int pe
           } else {
             float v[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = stem_act(bf2f(f2bf(acc[i][j2][e])), coef[co + e], coef[64 + co + e]);
+            for (int e = 0; e < 4; ++e) v[e] = stem_act(acc[i][j2][e], coef[co + e], coef[64 + co + e]);
             uint2 o;
             o.x = pack_bf2(v[0], v[1]);
             o.y = pack_bf2(v[2], v[3]);
@@ -445,6 +449,7 @@ constexpr int kRbPdRow = kRbPQ * 8, kRbPiRow = kRbPQ * 4;  // 16-B pieces per ro
 constexpr int kRbPdIns = (kRbPdRow + 63) / 64, kRbPiIns = (kRbPiRow + 63) / 64;
 constexpr int kRbPd = 2 * kRbPdRow * 16, kRbPi = 2 * kRbPiRow * 16;
 constexpr int kRbLds = kRbPatchB + 3 * kRbTile + 5 * 64 * 4 + kRbPd + kRbPi;
+static_assert(kRbPatchB >= kRbNPX * 8, "the ReLU mask bits ([128 px][64 bits]) reuse the patch area");
 // per-block partial: [4 waves][9 tiles][64 lanes] f32x4 | [2][64] sum dZ, sum dZ xhat
 constexpr int kRbPartF4 = 4 * 9 * 64 + 32;
 
@@ -615,19 +620,35 @@ __global__ void __launch_bounds__(kRbNT, 2) stem_rc_bwd_kernel(StemRcArgs a, int
     }
     lds_sync();
     if (kt < 2) TSTAMP(a.tim, 6 + 9 * kt);
-    {  // recompute y (bf16, as the forward rounded it) -> Ys
+    {  // recompute y in fp32 -> xhat = (y - mean) invstd (bf16: the third GEMM's
+      // operand) -> Ys, and the forward's ReLU mask [y sc + sh > 0] of the same
+      // fp32 y -> one bit per (pixel, channel) in the patch area (free until the
+      // next unit's patch store): pixel px's 64-bit word holds channel
+      // c = 16 i + 4 g + e at bit 16 g + 4 i + e, so lane group g writes one
+      // 16-bit half word per pixel
       f32x4 acc[4][2];
       conv32(Xs, wave * 32, wf, acc);
+      unsigned short* mbits = reinterpret_cast<unsigned short*>(patch);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int px = wave * 32 + j * 16 + li;
+        unsigned mk = 0u;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
+          const int co = i * 16 + 4 * g;
+          float xh[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float yv = acc[i][j][e];
+            xh[e] = (yv - cf[128 + co + e]) * cf[192 + co + e];
+            mk |= (stem_act(yv, cf[co + e], cf[64 + co + e]) > 0.f ? 1u : 0u) << (4 * i + e);
+          }
           uint2 o;
-          o.x = pack_bf2(acc[i][j][0], acc[i][j][1]);
-          o.y = pack_bf2(acc[i][j][2], acc[i][j][3]);
-          *reinterpret_cast<uint2*>(Ys + tt_off(px, i * 16 + 4 * g)) = o;
+          o.x = pack_bf2(xh[0], xh[1]);
+          o.y = pack_bf2(xh[2], xh[3]);
+          *reinterpret_cast<uint2*>(Ys + tt_off(px, co)) = o;
         }
+        mbits[px * 4 + g] = (unsigned short)mk;
       }
     }
     if (kt < 2) TSTAMP(a.tim, 7 + 9 * kt);
@@ -659,7 +680,8 @@ __global__ void __launch_bounds__(kRbNT, 2) stem_rc_bwd_kernel(StemRcArgs a, int
       const int w = q0 + px;
       const bool valid = px < Qs;
       const bool hodd = h & 1, wodd = it & 1;
-      const uint4 yv = *reinterpret_cast<const uint4*>(Ys + tt_off(px, c8));
+      const uint4 xhv = *reinterpret_cast<const uint4*>(Ys + tt_off(px, c8));
+      const unsigned long long mword = reinterpret_cast<const unsigned long long*>(patch)[px];
       const uint4 av = addv[it];
       const uint4 xv = *reinterpret_cast<const uint4*>(Xs + tt_off(px, c8));
       // the pooled cells that may have this pixel as their argmax, in
@@ -705,24 +727,26 @@ __global__ void __launch_bounds__(kRbNT, 2) stem_rc_bwd_kernel(StemRcArgs a, int
 #pragma unroll
         for (int k = 0; k < 8; ++k) acc[k] += r[k];
       }
-      float y[8];
-      unpack8(yv, y);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] = (valid & (stem_act(y[k], cf[c8 + k], cf[64 + c8 + k]) > 0.f)) ? acc[k] : 0.f;
+      for (int k = 0; k < 8; ++k) {
+        const int c = c8 + k;  // bit 16 g + 4 i + e of c = 16 i + 4 g + e
+        const int bit = ((c >> 2) & 3) * 16 + (c >> 4) * 4 + (c & 3);
+        acc[k] = (valid & (((mword >> bit) & 1ull) != 0ull)) ? acc[k] : 0.f;
+      }
       const uint4 o = pack8(acc);
       *reinterpret_cast<uint4*>(Ds + tt_off(px, c8)) = o;
       if (a.dz && valid) *reinterpret_cast<uint4*>(a.dz + (rowpix + w) * a.lddz + cg + c8) = o;
       float dz[8], xh[8];
       unpack8(o, dz);
+      unpack8(xhv, xh);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        xh[k] = (y[k] - cf[128 + c8 + k]) * cf[192 + c8 + k];
         s1[k] += dz[k];
         s2[k] += dz[k] * xh[k];
       }
-      // the xhat operand of the third GEMM (zero rows past the row end: their
+      // the xhat operand of the third GEMM: zero rows past the row end (their
       // im2col rows are zero too)
-      *reinterpret_cast<uint4*>(Ys + tt_off(px, c8)) = valid ? pack8(xh) : make_uint4(0, 0, 0, 0);
+      if (!valid) *reinterpret_cast<uint4*>(Ys + tt_off(px, c8)) = make_uint4(0, 0, 0, 0);
       if (valid) {  // im2col row chunk of this pixel, centred (the conv has read it)
         float im[8];
         unpack8(xv, im);
@@ -912,15 +936,7 @@ __global__ void __launch_bounds__(256) stem_rc_sum2_kernel(StemRcArgs a, int nse
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-static int rc_cus() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  }
-  return cus;
-}
+static int rc_cus() { return device_cu_count(); }
 
 bool stem_rc_ok(int Cout, int P, int Q) {
   return Cout % 64 == 0 && Q <= kRcNPX && Q % 2 == 0 && P % 2 == 0 && Q >= 2;

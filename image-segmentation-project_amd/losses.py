@@ -28,10 +28,11 @@ class _FusedLoss(torch.autograd.Function):
         t = target.to(device=x.device, dtype=torch.float32).contiguous()
         if x.numel() != t.numel():
             raise ValueError(f"logits {tuple(x.shape)} and target {tuple(t.shape)} differ in size")
-        sums = torch.empty(_lib.LOSS_SUMS_LEN, dtype=torch.float64, device=x.device)
+        sums, scratch = _lib.loss_buffers(x.device)
         out = torch.empty((), dtype=torch.float32, device=x.device)
         _lib.check(lib.unet_loss_forward(x.data_ptr(), t.data_ptr(), x.numel(), kind, float(alpha), float(smooth),
-                                         sums.data_ptr(), out.data_ptr(), _lib.stream_handle(x.device)),
+                                         sums.data_ptr(), scratch.data_ptr(), scratch.numel(), out.data_ptr(),
+                                         _lib.stream_handle(x.device)),
                    "unet_loss_forward")
         ctx.save_for_backward(x, t, sums)
         ctx.cfg = (kind, float(alpha), float(smooth))

@@ -31,10 +31,11 @@ def mask_counts(values, target, from_logits: bool):
     _lib.require_gpu(values, target)
     v = values.contiguous().float()
     t = target.to(device=v.device, dtype=torch.float32).contiguous()
-    sums = torch.empty(_lib.LOSS_SUMS_LEN, dtype=torch.float64, device=v.device)
+    sums, scratch = _lib.loss_buffers(v.device)
     _lib.check(_lib.load().unet_mask_metrics(v.data_ptr(), t.data_ptr(), v.numel(), 0 if from_logits else 1,
-                                             sums.data_ptr(), _lib.stream_handle(v.device)), "unet_mask_metrics")
-    return sums[:8]
+                                             sums.data_ptr(), scratch.data_ptr(), scratch.numel(),
+                                             _lib.stream_handle(v.device)), "unet_mask_metrics")
+    return sums
 
 
 def calculate_metrics(pred, target) -> dict:

@@ -79,7 +79,16 @@ int unet_plan_tensor_info(const unet_plan* p, int i, char* name, int namelen, in
  * as torch.nn.BatchNorm2d.train() does. */
 int unet_forward(unet_plan* p, const float* image, const float* const* params, float* const* buffers,
                  void* workspace, float* logits, int training, hipStream_t stream);
-/* grads: flat fp32 [unet_plan_grad_numel], param i at unet_plan_param_offset(i). */
+/* grads: flat fp32 [unet_plan_grad_numel], param i at unet_plan_param_offset(i).
+ * Ordering contract: unet_backward differentiates the LAST training
+ * unet_forward of the same plan and workspace (its saved activations and BN
+ * statistics).  A training forward also zeroes the backward's accumulators
+ * inside its first launch; if the workspace differs, or an eval forward came in
+ * between, unet_backward zeroes them itself (one memset), so a mismatched call
+ * order is never silently wrong about the accumulators -- but the gradients
+ * are only meaningful for the pairing above.
+ * unet_plan_create queries the current device's CU count (HIP runtime init);
+ * use the plan on that device. */
 int unet_backward(unet_plan* p, const float* image, const float* dlogits, const float* const* params,
                   void* workspace, float* grads, hipStream_t stream);
 /* record one hipEvent per gradient bucket in every unet_backward (DDP overlap) */
@@ -100,20 +109,25 @@ int unet_profile_enable(unet_plan* p, int on);
 int unet_profile_report(unet_plan* p, char* buf, int64_t buflen);
 
 /* ---- loss + metrics (kind: 0 bce, 1 dice, 2 combo) ---- */
-/* sums8 holds UNET_LOSS_SUMS_LEN doubles: [0..8) the sums (bce, sigma*y, sigma,
- * y, tp, fp, fn, tn), the rest per-block partials that the library reduces in a
- * fixed order (no atomics: the sums are bit-reproducible).  Nothing needs to be
- * zeroed beforehand. */
-#define UNET_LOSS_SUMS_LEN (8 + 8 * 256)
+/* sums8: exactly 8 doubles out, the sums (bce, sigma*y, sigma, y, tp, fp, fn, tn).
+ * scratch: caller-owned device scratch of scratch_len >= UNET_LOSS_SCRATCH_LEN
+ * doubles for the per-block partials, which the library reduces in a fixed
+ * order (no atomics: the sums are bit-reproducible); a shorter or null scratch
+ * is rejected with an error before anything is launched.  Nothing needs to be
+ * zeroed beforehand.  (Round 5 wrote the partials behind sums8; the separate,
+ * length-checked scratch makes an 8-double sums8 buffer safe again.) */
+#define UNET_LOSS_SCRATCH_LEN (8 * 256)
 int unet_loss_forward(const float* logits, const float* target, int64_t n, int kind, float alpha,
-                      float smooth, double* sums8, float* loss_out, hipStream_t stream);
+                      float smooth, double* sums8, double* scratch, int64_t scratch_len, float* loss_out,
+                      hipStream_t stream);
 int unet_loss_backward(const float* logits, const float* target, int64_t n, int kind, float alpha,
                        float smooth, const double* sums8, const float* grad_scale, float* dlogits,
                        hipStream_t stream);
 /* sums8[4..8) = tp, fp, fn, tn.  values_are_prob=0: logits (mask = sigmoid>0.5
- * evaluated bit-exactly as logit >= 0x33C00001); 1: probabilities (p > 0.5). */
+ * evaluated bit-exactly as logit >= 0x33C00001); 1: probabilities (p > 0.5).
+ * scratch / scratch_len as for unet_loss_forward. */
 int unet_mask_metrics(const float* values, const float* target, int64_t n, int values_are_prob,
-                      double* sums8, hipStream_t stream);
+                      double* sums8, double* scratch, int64_t scratch_len, hipStream_t stream);
 
 /* ---- optimizer ---- */
 /* One Adam step (coupled L2 weight decay, torch.optim.Adam semantics) over n
@@ -156,6 +170,27 @@ int unet_conv_wgrad_slab(const void* dy, int lddy, const void* x, int ldx, float
                          int S, int stride, int pad, int stem, hipStream_t stream);
 int unet_convt_wgrad_slab(const void* dy, int lddy, const void* x, int ldx, float* dw, void* slab,
                           int64_t slab_bytes, int N, int H, int W, int Ci, int Co, hipStream_t stream);
+/* The full-line halo conv (conv3x3_fl_kernel: every 3x3 / stride-1 conv with
+ * C >= 128 that fills the chip, i.e. the enc2 / enc3 BasicBlocks and decoder4 /
+ * decoder3 of the reference, advanced_models.py:84-87,197-205) as a single op.
+ * C % 128 == 0, Cout % 64 == 0, H % 16 == 0, W % 16 == 0 (here C = the op's
+ * input channels, Cout its output channels).  wch: the chunk-major pack of
+ * unet_pack_weight kind 5 (mode 0, forward weight [Cout][C][3][3]) or kind 6
+ * (mode 1, data gradient of a forward conv whose weight is [C][Cout][3][3]).
+ * mode 0: y = conv3x3(x) (+bias)(+addend); stats != null: BN sums of y into
+ *   stats[16][2][Cout] (fp64 atomics, caller zeroes).
+ * mode 1: y = conv3x3_transpose(x) (+addend); bsums != null: the fused BN(+ReLU)
+ *   backward epilogue: y := dZ = dA * (act > 0) and bsums[16][2][Cout] +=
+ *   (sum dZ, sum dZ * (yraw - mean) * invstd); yraw2 != null (downsample blocks,
+ *   two BNs): bsums2[16][1][Cout] (the second half of each replica) +=
+ *   sum dZ * (yraw2 - mean2) * invstd2.
+ * grid: 0 = the production persistent grid (one block per CU); > 0 caps it
+ * (rounded down to a multiple of Cout / 64) so blocks run several work items. */
+int unet_conv3x3_fl(const void* x, int ldx, const void* wch, void* y, int ldy, const float* bias,
+                    const void* addend, int ldadd, double* stats, const void* act, int ldact, const void* yraw,
+                    int ldyraw, const float* mean, const float* invstd, const void* yraw2, int ldyraw2,
+                    const float* mean2, const float* invstd2, double* bsums, double* bsums2, int N, int H,
+                    int W, int C, int Cout, int mode, int grid, hipStream_t stream);
 /* ---- fp8 e4m3 forward conv (BASELINE.json configs[4]; no reference counterpart:
  * the reference's convs are fp32 torch.nn.Conv2d, advanced_models.py:72-100) ----
  * state: 16-B scale state {amax prev (float bits), amax this step, e8m0 code,
@@ -180,7 +215,9 @@ int unet_conv_fwd_f8(const void* xq, int ldx, const void* wq, const void* state_
 /* tile configuration of the implicit-GEMM conv kernels: 0 automatic (default),
  * >0 a fixed configuration from the tuning table (scripts/tune_conv.py) */
 int unet_set_conv_config(int cfg);
-/* kind: 0 conv fwd, 1 conv dgrad, 2 convT fwd, 3 convT dgrad, 4 stem */
+/* kind: 0 conv fwd, 1 conv dgrad, 2 convT fwd, 3 convT dgrad, 4 stem,
+ * 5 conv fwd chunk-major [Ci/32][3*3][Co][32], 6 conv dgrad chunk-major
+ * [Co/32][3*3][Ci][32] (3x3 only; unet_conv3x3_fl) */
 int unet_pack_weight(const float* src, void* dst, int kind, int Co, int Ci, int R, int S,
                      hipStream_t stream);
 /* kind: 0 conv [Co][R][S][Ci] -> [Co][Ci][R][S], 1 convT, 2 stem */

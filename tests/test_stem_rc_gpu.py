@@ -3,18 +3,19 @@ to 256 pixels) against the stored-y0 stem path (UNET_STEM_RC=0: stem_fwd +
 bn_relu_maxpool_fwd + maxpool_bwd + BN-fused stem_wgrad) on the same inputs
 and weights (resnet34 stem, advanced_models.py:76-83).
 
-The two paths compute y with the same MFMA sequence, but the BN batch sums
-are accumulated in another order (fp32 partials -> fp64), so scale/shift may
-differ in the last bit and a few bf16 activations round the other way; and
-the recompute path forms the stem weight gradient through the BN-backward
-identity dW = k1 (dZ^T im - m1 sum im - m2 xhat^T im) instead of rounding
-dY = k1 (dZ - m1 - m2 xhat) to bf16 first.  Bars: forward activations (x1,
-pooled p0) relative L2 <= 1e-3 with >= 99 % of elements bit-equal and the
-argmax index equal wherever the inputs are; every parameter gradient relative
-L2 <= 1e-2 (input_conv.weight, the one computed differently: <= 2e-2); the
-recompute path's backward is bit-reproducible.  The teacher-forced rows of
-test_wiring_gpu.py (UNET_STEM_KEEP=1) pin the recompute path's dZ, bn1 and
-input_conv gradients against fp32 recomputations at 2e-2.
+The two paths compute y with the same MFMA sequence, but since round 6 the
+recompute path normalises the fp32 y (as the reference's fp32 BatchNorm does)
+while the stored path can only normalise the bf16 y0 it stored; the recompute
+path also forms the stem weight gradient through the BN-backward identity
+dW = k1 (dZ^T im - m1 sum im - m2 xhat^T im) instead of rounding
+dY = k1 (dZ - m1 - m2 xhat) to bf16 first.  So the two differ by one bf16
+rounding of y before the BN: each is pinned against ITS reference in
+test_stem_production_path_vs_fp32 (recompute: the pure fp32 chain; stored:
+the chain with y0 rounded to bf16), and here they are only checked to agree
+within that rounding's own effect.  The recompute path's backward is
+bit-reproducible.  The teacher-forced rows of test_wiring_gpu.py
+(UNET_STEM_KEEP=1) pin the recompute path's dZ, bn1 and input_conv gradients
+against fp32 recomputations at 2e-2.
 """
 import os
 
@@ -63,13 +64,16 @@ def test_stem_recompute_matches_stored_path(pkg, cuda, shape):
     for k in ("x1", "p0"):
         e, same = _rel(v_rc[k], v_st[k]), (v_rc[k] == v_st[k]).float().mean().item()
         print(f"{k}: rel {e:.2e}, bit-equal fraction {same:.5f}")
-        assert e <= 1e-3 and same >= 0.99, (k, e, same)
+        assert e <= X1_TOL_FP32, (k, e, same)
     print("logits rel", _rel(o_rc, o_st))
-    assert _rel(o_rc, o_st) <= 1e-2
+    assert _rel(o_rc, o_st) <= 5e-2
     worst = sorted(((_rel(g_rc[k], g_st[k]), k) for k in g_st if g_st[k].norm() > 0), reverse=True)[:6]
     print("largest gradient differences:", [(k, f"{e:.2e}") for e, k in worst])
+    stem = ("input_conv.weight", "bn1.weight", "bn1.bias")
     for e, k in worst:
-        assert e <= (2e-2 if k == "input_conv.weight" else 1e-2), (k, e)
+        # the stem's own gradients carry the bf16-y rounding difference (the BN
+        # backward's cancelling terms amplify it); the rest only its echo
+        assert e <= (STEM_PATHS_TOL if k in stem else 5e-2), (k, e)
     # bit-reproducible: the same step again on the recompute path
     o2, v2, g2 = _run(pkg, sd, x, y, {"UNET_STEM_RC": "1"})
     assert torch.equal(o2, o_rc)
@@ -98,31 +102,35 @@ def _dskip(v):
 #     input_conv.weight 3.8e-2 | 6.8e-2, bn1.bias 2.4e-2 | 4.3e-2 (the weight and
 #     bias gradients are small residuals of the BN backward's cancelling terms)
 #   fp64 recomputation from the stored dZ: input_conv.weight 5.8e-4
-X1_TOL, W_TOL = 3e-3, 3e-2            # bf16-y0 reference
-X1_TOL_FP32, W_TOL_FP32 = 8e-3, 1e-1  # pure fp32 reference
+X1_TOL, W_TOL = 3e-3, 3e-2   # each path against its own reference (<= 3e-2)
+X1_TOL_FP32 = 8e-3            # recompute vs stored path: one bf16 rounding of y apart
+STEM_PATHS_TOL = 1.5e-1       # their stem gradients (the rounding's amplified effect, measured above)
 W64_TOL = 2e-3
 
 
+@pytest.mark.parametrize("path", ["recompute", "stored"])
 @pytest.mark.parametrize("shape", [(2, 256, 256), (1, 64, 96)], ids=["2x256", "1x64x96"])
-def test_stem_production_path_vs_fp32(pkg, cuda, shape):
+def test_stem_production_path_vs_fp32(pkg, cuda, shape, path):
     """The production stem (recompute, nothing but x1 / p0 stored) against a
     torch restatement of advanced_models.py:76,81-83 on the same bf16 input and
     weights: forward x1 = relu(bn(conv(xq))) and p0 = maxpool(x1); backward:
     the stem parameter gradients by autograd through that chain, fed the
     executor's own upstream gradients (d.p0 into the pool, the decoder1
-    concat's skip slice into x1).  Two references: y0 rounded to bf16 before
-    the BN, where the kernels round it (stem_rc.hip: act = bf16(relu(y sc +
-    sh)) of a bf16 y, as the stored path) -- tight bars -- and the pure fp32
-    chain of the reference model -- bars that hold the rounding's own effect."""
+    concat's skip slice into x1).  The recompute path normalises the fp32 conv
+    output, so its reference is the pure fp32 chain of the reference model; the
+    stored-y0 path (UNET_STEM_RC=0: HiRes rows wider than 256) stores y0 in
+    bf16, so its reference rounds y0 to bf16 before the BN.  Both at the same
+    bars: x1 / p0 <= 3e-3, every stem gradient <= 3e-2."""
     ref = oracle.ReferenceUNet()
     sd = oracle.closed_form_state_dict(ref, seed=5)
     xs, ms = pkg.synthetic_cells(*shape, seed=13)
     x, y = torch.from_numpy(xs).cuda(), torch.from_numpy(ms).cuda()
     assert os.environ.get("UNET_STEM_KEEP") is None and os.environ.get("UNET_STEM_RC") is None
-    _, v, g = _run(pkg, sd, x, y, {})
-    assert "y0" not in v, "production stem path expected (no stored y0)"
+    _, v, g = _run(pkg, sd, x, y, {} if path == "recompute" else {"UNET_STEM_RC": "0"})
+    if path == "recompute":
+        assert "y0" not in v, "production stem path expected (no stored y0)"
     xq = x.cpu().to(torch.bfloat16).float()
-    for rnd, xtol, wtol in ((True, X1_TOL, W_TOL), (False, X1_TOL_FP32, W_TOL_FP32)):
+    for rnd, xtol, wtol in ((path == "stored", X1_TOL, W_TOL),):
         w = sd["input_conv.weight"].to(torch.bfloat16).float().requires_grad_(True)
         gam = sd["bn1.weight"].float().clone().requires_grad_(True)
         bet = sd["bn1.bias"].float().clone().requires_grad_(True)
@@ -137,7 +145,7 @@ def test_stem_production_path_vs_fp32(pkg, cuda, shape):
         gw, gg, gb = torch.autograd.grad([p0, x1], [w, gam, bet], [v["d.p0"].float(), _dskip(v).float()])
         rows = [("input_conv.weight", _rel(g["input_conv.weight"], gw)), ("bn1.weight", _rel(g["bn1.weight"], gg)),
                 ("bn1.bias", _rel(g["bn1.bias"], gb))]
-        print(f"{'bf16-y0' if rnd else 'fp32'} reference: x1 rel {ex1:.2e}  p0 rel {ep0:.2e}  " +
+        print(f"{path} path vs {'bf16-y0' if rnd else 'fp32'} reference: x1 rel {ex1:.2e}  p0 rel {ep0:.2e}  " +
               "  ".join(f"{k} {e:.2e}" for k, e in rows))
         assert ex1 <= xtol and ep0 <= xtol, (rnd, ex1, ep0)
         for k, e in rows:
@@ -147,15 +155,17 @@ def test_stem_production_path_vs_fp32(pkg, cuda, shape):
 def test_stem_weight_gradient_vs_fp64(pkg, cuda):
     """The recompute path's stem weight gradient, formed through the
     BN-backward identity dW = k1 (dZ^T im - m1 sum im - m2 xhat^T im), against
-    an fp64 recomputation from the same stored dZ and y0 (UNET_STEM_KEEP=1:
-    the kernel reads exactly these): dY = BN-backward(dZ) in fp64, then
-    conv2d_weight(xq, dY) in fp64."""
+    an fp64 recomputation from the same stored dZ (UNET_STEM_KEEP=1) and the
+    conv output y0 recomputed in fp64 from the same bf16 image and weights (the
+    kernel normalises its fp32 y, not the bf16 y0 it stores for tests):
+    dY = BN-backward(dZ) in fp64, then conv2d_weight(xq, dY) in fp64."""
     ref = oracle.ReferenceUNet()
     sd = oracle.closed_form_state_dict(ref, seed=5)
     xs, ms = pkg.synthetic_cells(2, 256, 256, seed=13)
     x, y = torch.from_numpy(xs).cuda(), torch.from_numpy(ms).cuda()
     _, v, g = _run(pkg, sd, x, y, {"UNET_STEM_KEEP": "1"})
-    y0 = v["y0"].double()
+    wq = sd["input_conv.weight"].to(torch.bfloat16).double()
+    y0 = torch.nn.functional.conv2d(x.cpu().to(torch.bfloat16).double(), wq, stride=2, padding=3)
     dz = v["d.x1"].double() * (v["x1"] > 0).double()
     n = y0.shape[0] * y0.shape[2] * y0.shape[3]
     mu = y0.mean((0, 2, 3), keepdim=True)
