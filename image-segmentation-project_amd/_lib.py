@@ -61,6 +61,11 @@ SIGNATURES = {
     "unet_mask_metrics": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_int64, c_void_p]),
     "unet_adam_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float,
                                c_float, c_float, c_int, c_void_p]),
+    "unet_allreduce_unique_id": (c_int, [c_void_p]),
+    "unet_allreduce_init": (c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_void_p)]),
+    "unet_allreduce_destroy": (None, [c_void_p]),
+    "unet_allreduce_bucket": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "unet_allreduce_mean": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
     "unet_grad_to_bf16": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
     "unet_grad_from_bf16": (c_int, [c_void_p, c_void_p, c_int64, c_float, c_void_p]),
     "unet_conv_fwd": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]
@@ -68,7 +73,7 @@ SIGNATURES = {
     "unet_conv_wgrad": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p] + [c_int] * 12 + [c_void_p]),
     "unet_conv3x3_fl": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p,
                                 c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
-                                c_void_p, c_void_p, c_void_p] + [c_int] * 8 + [c_void_p]),
+                                c_void_p, c_void_p, c_void_p] + [c_int] * 7 + [c_void_p]),
     "unet_f8_quantize": (c_int, [c_void_p, c_int, c_int, c_int64, c_void_p, c_void_p, c_int, c_void_p]),
     "unet_f8_pack_weight": (c_int, [c_void_p] + [c_int] * 4 + [c_void_p, c_void_p, c_int, c_void_p]),
     "unet_f8_roll": (c_int, [c_void_p, c_int, c_void_p]),

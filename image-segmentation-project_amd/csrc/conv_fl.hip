@@ -359,7 +359,14 @@ __global__ void __launch_bounds__(kNW * 64) conv3x3_fl_kernel(ConvFwdArgs a, int
   // items whose operands are prefetched at B_{NSUB-1}: all but for the
   // dgrad without addend, where half (the rest issued by the epilogue itself)
   // keeps the loader in registers (measured, profiles/r05/s2 conv_timing*)
-  constexpr int NP = (!RT && FLIP && !TWO && (EP & EP_FBWD) && !(EP & EP_ADD)) ? NI / 2 : NI;
+  // (round 6: the half prefetch of the FBWD-without-addend instance produced
+  // wrong BN-backward sums -- sum dZ * xhat came out 0 -- caught by
+  // tests/test_conv_fl_gpu.py; every instance now prefetches all NI items)
+  // two-BN epilogue (TWO): no prefetch -- its four operands per item (addend,
+  // mask, y, y2) for 8 items held across the sub-stage loop pushed the loader
+  // waves into scratch, and that instance produced wrong BN-backward sums; it
+  // now loads each group of 4 items' operands inside the epilogue
+  constexpr int NP = TWO ? 0 : NI;
   int ep_pix0 = 0;                 // the pending epilogue's tile origin pixel (N * P * Q < 2^31: launcher)
   auto pix_of = [&](int k) {
     const int px = px_of(k);
@@ -374,31 +381,46 @@ __global__ void __launch_bounds__(kNW * 64) conv3x3_fl_kernel(ConvFwdArgs a, int
     om = fbwd ? *reinterpret_cast<const uint4*>(a.bb.act + pp * a.bb.ldact + co) : make_uint4(0, 0, 0, 0);
     oy = fbwd ? *reinterpret_cast<const uint4*>(a.bb.y + pp * a.bb.ldy + co) : make_uint4(0, 0, 0, 0);
     if constexpr (TWO) oy2 = fbwd ? *reinterpret_cast<const uint4*>(a.bb.y2 + pp * a.bb.ldy2 + co) : make_uint4(0, 0, 0, 0);
+    else oy2 = make_uint4(0, 0, 0, 0);
   };
-  uint4 opa[NP], opm[NP], opy[NP], opy2[TWO ? NP : 1];
+  constexpr int NPA = NP > 0 ? NP : 1;
+  uint4 opa[NPA], opm[NPA], opy[NPA], opy2[TWO ? NPA : 1];
   // the epilogue of the item whose accumulators are in T (items < NP: operands
   // prefetched)
   auto epilogue = [&]() {
-    constexpr int NL = NI - NP > 0 ? NI - NP : 1;
-    uint4 la[NL], lm[NL], ly[NL], ly2[TWO ? NL : 1];
-#pragma unroll
-    for (int k = NP; k < NI; ++k) load_ops(k, la[k - NP], lm[k - NP], ly[k - NP], ly2[TWO ? k - NP : 0]);
-    // the thread's channel constants, once per epilogue
+    // the thread's channel constants, once per epilogue (mu / is unused by TWO,
+    // zeroed so that no path reads an uninitialised register)
     float kb[8], km[8], mu[8], is[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) kb[e] = km[e] = mu[e] = is[e] = 0.f;
     if (!TWO) fl_ld8(cst + q8, kb);
     if (fold) fl_ld8(cst + kCOT + q8, km);
     if (fbwd && !TWO) {
       fl_ld8(cst + kCOT + q8, mu);
       fl_ld8(cst + 2 * kCOT + q8, is);
     }
+    if constexpr (NP > 0) {
 #pragma unroll
-    for (int k = 0; k < NI; ++k) {
-      const bool pre = k < NP;
-      const int j = pre ? k : k - NP;
-      fl_item<FLIP, TWO>(a, smem + kOffW1, cst, kb, km, mu, is, q8, px_of(k), pix_of(k), cob, fold, want_add, fbwd,
-                         stats, relu, pre ? opa[j] : la[j], pre ? opm[j] : lm[j], pre ? opy[j] : ly[j],
-                         TWO ? (pre ? opy2[j] : ly2[j]) : opy2[0], s0, s1, s2);
-      asm volatile("" ::: "memory");  // one item at a time: bounded registers
+      for (int k = 0; k < NI; ++k) {
+        fl_item<FLIP, TWO>(a, smem + kOffW1, cst, kb, km, mu, is, q8, px_of(k), pix_of(k), cob, fold, want_add, fbwd,
+                           stats, relu, opa[k], opm[k], opy[k], opy2[TWO ? k : 0], s0, s1, s2);
+        asm volatile("" ::: "memory");  // one item at a time: bounded registers
+      }
+    } else {
+      // groups of G items: their operand loads all in flight, then the items
+      constexpr int G = 4;
+#pragma unroll
+      for (int k0 = 0; k0 < NI; k0 += G) {
+        uint4 la[G], lm[G], ly[G], ly2[G];
+#pragma unroll
+        for (int k = 0; k < G; ++k) load_ops(k0 + k, la[k], lm[k], ly[k], ly2[k]);
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+          fl_item<FLIP, TWO>(a, smem + kOffW1, cst, kb, km, mu, is, q8, px_of(k0 + k), pix_of(k0 + k), cob, fold,
+                             want_add, fbwd, stats, relu, la[k], lm[k], ly[k], ly2[k], s0, s1, s2);
+          asm volatile("" ::: "memory");
+        }
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's T rows are read before its DMA refills them
   };
@@ -412,6 +434,7 @@ __global__ void __launch_bounds__(kNW * 64) conv3x3_fl_kernel(ConvFwdArgs a, int
 #pragma unroll
     for (int k = 0; k < NP; ++k) load_ops(k, opa[k], opm[k], opy[k], opy2[TWO ? k : 0]);
   };
+  (void)opa; (void)opm; (void)opy; (void)opy2;
   bool pending = false;  // an epilogue waits for the next B_0 / Z
   int nit = 0;             // items done (timing stamps of the first two)
   for (;;) {

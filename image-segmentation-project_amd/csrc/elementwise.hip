@@ -1286,8 +1286,10 @@ __device__ __forceinline__ void loss_accum(float v, float y, int from_prob, floa
     const float ru = __builtin_amdgcn_rcpf(u);
     const float um1 = u - 1.f;
     const float l1p = um1 == 0.f ? e : __logf(u) * (e * __builtin_amdgcn_rcpf(um1));
-    const float ls = fminf(v, 0.f) - l1p;
-    s[0] += (1.f - y) * v - ls;
+    // (1 - y) v - log_sigmoid(v) = max(v, 0) - y v + log1p(e): the same value as
+    // torch's formulation without its cancellation for confident logits
+    // (e.g. v = -10, y = 0: -10 - (-10 - 4.5e-5) loses ~1 % in fp32)
+    s[0] += (fmaxf(v, 0.f) - y * v) + l1p;
     const float sg = (v >= 0.f ? 1.f : e) * ru;
     s[1] += sg * y;
     s[2] += sg;

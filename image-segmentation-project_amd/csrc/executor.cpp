@@ -7,7 +7,9 @@
 // buffers that the up-convs write into directly, BN sums, packed weights and
 // fp32 weight-gradient accumulators), and the launch sequence.  Python passes
 // raw device pointers; nothing here allocates device memory.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // types only: the functions are resolved at run time (unet_allreduce_init)
 
 #include <cstdio>
 #include <cstdlib>
@@ -460,11 +462,15 @@ static int build_plan(unet_plan* p) {
   {
     const int64_t dec_begin = p->params[enc_end_param].flat;
     p->buckets.push_back({dec_begin, p->grad_numel});
-    auto r4 = stage_range(3), r3 = stage_range(2);
+    auto r4 = stage_range(3), r3 = stage_range(2), r1 = stage_range(0);
     p->buckets.push_back({p->params[r4.first].flat, p->params[r4.second].flat + p->params[r4.second].numel});
     p->buckets.push_back({p->params[r3.first].flat, p->params[r3.second].flat + p->params[r3.second].numel});
-    p->buckets.push_back({0, p->params[r3.first].flat});
+    // enc2 + enc1 final before the stem's backward, so only the stem's 3.3 k
+    // parameters (bucket 4) trail the backward
+    p->buckets.push_back({p->params[r1.first].flat, p->params[r3.first].flat});
+    p->buckets.push_back({0, p->params[r1.first].flat});
   }
+  static_assert(sizeof(((unet_plan*)nullptr)->events) / sizeof(hipEvent_t) >= 5, "one event per bucket");
 
   // ---- workspace ----
   Alloc A;
@@ -780,10 +786,10 @@ static int build_plan(unet_plan* p) {
   }
 
   // unpack groups per bucket
-  p->bucket_convs.assign(4, {});
+  p->bucket_convs.assign(p->buckets.size(), {});
   for (int i = 0; i < (int)p->convs.size(); ++i) {
     const int64_t f = p->params[p->convs[i].w].flat;
-    for (int bk = 0; bk < 4; ++bk)
+    for (int bk = 0; bk < (int)p->buckets.size(); ++bk)
       if (f >= p->buckets[bk].first && f < p->buckets[bk].second) p->bucket_convs[bk].push_back(i);
   }
 
@@ -837,8 +843,9 @@ static int build_plan(unet_plan* p) {
 
 static int ensure_events(unet_plan* p) {
   if (p->nevents) return 0;
-  for (int i = 0; i < 4; ++i) CK(hipEventCreateWithFlags(&p->events[i], hipEventDisableTiming));
-  p->nevents = 4;
+  const int nb = (int)p->buckets.size();
+  for (int i = 0; i < nb; ++i) CK(hipEventCreateWithFlags(&p->events[i], hipEventDisableTiming));
+  p->nevents = nb;
   return 0;
 }
 
@@ -1300,7 +1307,7 @@ int unpack_bucket(const Ctx& x, int bk, float* grads) {
     else { e.kind = UP_STEM; e.Co = cv.Co; e.Ci = 1; e.R = 7; e.S = 7; }
     if (t.n == kMaxPack) { CK(launch_unpack(t, x.wst)); t.n = 0; }
   }
-  if (!defer || bk == 3) {  // bucket 3 (the stem's) is the backward's last
+  if (!defer || bk == (int)x.p->buckets.size() - 1) {  // the last bucket (the stem's) ends the backward
     CK(launch_unpack(t, x.wst));
     t.n = 0;
   }
@@ -1805,6 +1812,13 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
       if (p->nevents) CK(hipEventRecord(p->events[bk], x.wst));
     }
   }
+  // bucket 3 (enc2 + enc1) is final: its all-reduce overlaps the stem's backward
+  {
+    const int bk = (int)p->buckets.size() - 2;
+    RUN(stream_edge(p, st, x.wst));
+    RUN(unpack_bucket(x, bk, grads));
+    if (p->nevents) CK(hipEventRecord(p->events[bk], x.wst));
+  }
   // maxpool + stem
   if (p->stem_rc && fz) {
     // one pass: maxpool backward, stem BN backward, stem weight gradient
@@ -1864,8 +1878,11 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     a.x = reinterpret_cast<const bf16_t*>(image);
     RUN(wgrad_and_reduce(x, a, 1, "input_conv.weight", 2.0 * N * p->y0.H * p->y0.W * cv.Co * 49));
   }
-  RUN(unpack_bucket(x, 3, grads));
-  if (p->nevents) CK(hipEventRecord(p->events[3], x.wst));
+  {
+    const int bk = (int)p->buckets.size() - 1;
+    RUN(unpack_bucket(x, bk, grads));
+    if (p->nevents) CK(hipEventRecord(p->events[bk], x.wst));
+  }
   // join: the caller's stream (optimizer, next forward) sees every gradient
   RUN(stream_edge(p, x.wst, st));
   return 0;
@@ -2302,6 +2319,112 @@ int unet_filter2d_u8(const uint8_t* src, int N, int H, int W, const float* kerne
   if (!src || !dst || !kernels || !ksize) { set_err("unet_filter2d_u8: null buffer"); return 1; }
   CK(launch_filter2d(src, dst, N, H, W, kernels, ksize, stream));
   return 0;
+}
+
+// ---------------------------------------------------------------------------
+// DDP gradient reduction over RCCL for non-Python hosts (SURVEY.md §8(b):
+// "unet_allreduce_* ... communicator init from a ncclUniqueId byte blob";
+// insertion point /root/reference/train.py:48-49).  RCCL is resolved at run
+// time: the process's already-loaded RCCL (torch's, when a Python host loaded
+// it globally) or /opt/rocm's librccl.so.1, so the library itself has no
+// link-time RCCL dependency and plan-only / CPU users never load it.
+// ---------------------------------------------------------------------------
+}  // extern "C"
+
+namespace {
+struct Rccl {
+  decltype(&ncclGetUniqueId) get_id = nullptr;
+  decltype(&ncclCommInitRank) init = nullptr;
+  decltype(&ncclCommDestroy) destroy = nullptr;
+  decltype(&ncclAllReduce) allreduce = nullptr;
+  decltype(&ncclGetErrorString) errstr = nullptr;
+  bool ok = false;
+};
+const Rccl& rccl() {
+  static Rccl r = [] {
+    Rccl x;
+    void* h = nullptr;
+    if (!dlsym(RTLD_DEFAULT, "ncclCommInitRank")) {
+      h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+      if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    }
+    auto sym = [&](const char* n) { return h ? dlsym(h, n) : dlsym(RTLD_DEFAULT, n); };
+    x.get_id = reinterpret_cast<decltype(x.get_id)>(sym("ncclGetUniqueId"));
+    x.init = reinterpret_cast<decltype(x.init)>(sym("ncclCommInitRank"));
+    x.destroy = reinterpret_cast<decltype(x.destroy)>(sym("ncclCommDestroy"));
+    x.allreduce = reinterpret_cast<decltype(x.allreduce)>(sym("ncclAllReduce"));
+    x.errstr = reinterpret_cast<decltype(x.errstr)>(sym("ncclGetErrorString"));
+    x.ok = x.get_id && x.init && x.destroy && x.allreduce && x.errstr;
+    return x;
+  }();
+  return r;
+}
+int rccl_check(ncclResult_t r, const char* what) {
+  if (r == ncclSuccess) return 0;
+  set_err(std::string(what) + ": " + rccl().errstr(r));
+  return 1;
+}
+}  // namespace
+
+struct unet_comm {
+  ncclComm_t comm = nullptr;
+  int rank = 0, world = 1;
+};
+
+extern "C" {
+
+static_assert(UNET_UNIQUE_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "ncclUniqueId blob size");
+
+int unet_allreduce_unique_id(void* id) {
+  if (!id) { set_err("unet_allreduce_unique_id: null buffer"); return 1; }
+  if (!rccl().ok) { set_err("unet_allreduce_unique_id: RCCL (librccl.so.1) not found"); return 1; }
+  ncclUniqueId u;
+  if (rccl_check(rccl().get_id(&u), "ncclGetUniqueId")) return 1;
+  std::memcpy(id, &u, sizeof(u));
+  return 0;
+}
+
+int unet_allreduce_init(const void* id, int rank, int world, unet_comm** out) {
+  if (!id || !out || world < 1 || rank < 0 || rank >= world) {
+    set_err("unet_allreduce_init: null argument or rank outside [0, world)");
+    return 1;
+  }
+  if (!rccl().ok) { set_err("unet_allreduce_init: RCCL (librccl.so.1) not found"); return 1; }
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  unet_comm* c = new unet_comm();
+  c->rank = rank;
+  c->world = world;
+  if (rccl_check(rccl().init(&c->comm, world, u, rank), "ncclCommInitRank")) {
+    delete c;
+    return 1;
+  }
+  *out = c;
+  return 0;
+}
+
+void unet_allreduce_destroy(unet_comm* c) {
+  if (!c) return;
+  if (c->comm && rccl().ok) (void)rccl().destroy(c->comm);
+  delete c;
+}
+
+int unet_allreduce_mean(unet_comm* c, float* buf, int64_t n, hipStream_t stream) {
+  if (!c || n < 0 || (n > 0 && !buf)) { set_err("unet_allreduce_mean: null communicator / buffer"); return 1; }
+  if (n == 0) return 0;
+  return rccl_check(rccl().allreduce(buf, buf, (size_t)n, ncclFloat32, ncclAvg, c->comm, stream), "ncclAllReduce");
+}
+
+int unet_allreduce_bucket(unet_comm* c, unet_plan* p, float* grads, int bucket, hipStream_t comm_stream) {
+  if (!c || !p || !grads || bucket < 0 || bucket >= (int)p->buckets.size()) {
+    set_err("unet_allreduce_bucket: null argument or bad bucket");
+    return 1;
+  }
+  // after the bucket's event when the last backward recorded one (DDP overlap);
+  // otherwise the caller has ordered comm_stream after the whole backward
+  if (bucket < p->nevents) CK(hipStreamWaitEvent(comm_stream, p->events[bucket], 0));
+  const auto& r = p->buckets[(size_t)bucket];
+  return unet_allreduce_mean(c, grads + r.first, r.second - r.first, comm_stream);
 }
 
 int unet_maxpool_fwd(const void* x, int ldx, void* y, uint8_t* idx, int N, int H, int W, int C,

@@ -141,6 +141,30 @@ int unet_adam_step(float* params, const float* grads, float* exp_avg, float* exp
                    int64_t n, float lr, float beta1, float beta2, float eps, float weight_decay,
                    int advance_step, hipStream_t stream);
 
+/* ---- DDP gradient reduction over RCCL (non-Python hosts) ----
+ * The reference trains in one process; these sit at its DDP insertion point,
+ * between loss.backward() and optimizer.step() (train.py:48-49), and replace
+ * torch.distributed for a C / C++ / FFI host.  RCCL (the
+ * process's own, else /opt/rocm's librccl.so.1) is resolved at run time.
+ * Rank 0 calls unet_allreduce_unique_id and ships the UNET_UNIQUE_ID_BYTES blob
+ * to every rank out of band; each rank (one process per GPU, its device
+ * current) calls unet_allreduce_init -- collective over the world.
+ * unet_allreduce_bucket: mean all-reduce, in place in the flat fp32 gradient
+ * buffer, of bucket `bucket` (unet_plan_bucket_range) of the last
+ * unet_backward, enqueued on comm_stream after that bucket's hipEvent when
+ * unet_plan_use_bucket_events(p, 1) was on during that backward (the
+ * all-reduce then overlaps the rest of the backward); otherwise the caller
+ * orders comm_stream after the backward.  The caller orders its compute
+ * stream after comm_stream before optimizer.step().  Graph-capturable. */
+#define UNET_UNIQUE_ID_BYTES 128
+typedef struct unet_comm unet_comm;
+int unet_allreduce_unique_id(void* id);
+int unet_allreduce_init(const void* id, int rank, int world, unet_comm** out);
+void unet_allreduce_destroy(unet_comm* c);
+int unet_allreduce_bucket(unet_comm* c, unet_plan* p, float* grads, int bucket, hipStream_t comm_stream);
+/* mean all-reduce of n floats in place (any flat buffer) */
+int unet_allreduce_mean(unet_comm* c, float* buf, int64_t n, hipStream_t stream);
+
 /* ---- bf16 gradient exchange (opt-in DDP compression) ----
  * Replace nothing in the reference (it trains in one process); they sit at
  * the DDP insertion point train.py:48-49, around each bucket's all-reduce:

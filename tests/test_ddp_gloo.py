@@ -6,7 +6,7 @@
   all-reduce of every gradient between backward and step, train.py:48-49),
   pinned on the oracle model: two ranks each run the fp32 oracle U-Net on half
   of a batch, flatten their gradients in the native plan's parameter order and
-  reduce them with ``GradBucketReducer`` over the plan's four buckets; the
+  reduce them with ``GradBucketReducer`` over the plan's five buckets; the
   result equals the single-process mean of the two per-chunk oracle gradients
   (rtol 1e-6: an fp32 sum of two terms and a halving), and one Adam step from
   it leaves both ranks' parameters identical.
@@ -108,7 +108,10 @@ def _oracle_worker(rank, world, port, q):
         ref.load_state_dict(sd)
         expect = sum(_chunk_grads(ref, *c) for c in chunks) / world
         err = ((flat - expect).abs().max() / expect.abs().max()).item()
-        ok = torch.allclose(flat, expect, rtol=1e-6, atol=1e-9) and order == [0, 1, 2, 3]
+        ok = torch.allclose(flat, expect, rtol=1e-6, atol=1e-9) and order == list(range(len(ranges)))
+        # five buckets in backward completion order: decoder + head, enc4, enc3,
+        # enc2 + enc1, and the stem alone (only its 3.3 k parameters trail)
+        ok = ok and len(ranges) == 5 and ranges[-1] == (0, offsets[names.index("enc1.0.conv1.weight")])
         # one optimizer step from the reduced gradients keeps the replicas equal
         ref.load_state_dict(sd)
         opt = oracle.make_adam(ref)

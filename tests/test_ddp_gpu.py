@@ -70,7 +70,7 @@ def test_bucketed_allreduce_rccl_world1(pkg, cuda, attention, monkeypatch):
         for step in range(3):  # step 0: no bucket events yet; then event-ordered buckets
             got = grads()
             (red,) = m._ddp._reducers.values()
-            assert len(red.ranges) == 4 and red._stream is not None
+            assert len(red.ranges) == 5 and red._stream is not None
             worst = max(_rel(a, b) for a, b in zip(got, plain) if b.norm() > 0)
             print(f"step {step}: worst rel {worst:.2e}")
             assert worst <= 1e-5, (step, worst)
@@ -371,3 +371,108 @@ def test_bf16_exchange_rccl_world1(pkg, cuda, attention, monkeypatch):
             assert not bad, (step, bad[:5])
     finally:
         dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------------------
+# The C-ABI all-reduce (unet_allreduce_*): what a non-Python
+# host binds instead of torch.distributed.  One rank on the one GPU of the box
+# (RCCL world 1: the mean is the identity, so the results are exact).
+# ---------------------------------------------------------------------------
+def _comm(L):
+    import ctypes
+    uid = ctypes.create_string_buffer(128)
+    assert L.unet_allreduce_unique_id(uid) == 0, L.unet_last_error()
+    c = ctypes.c_void_p()
+    assert L.unet_allreduce_init(uid, 0, 1, ctypes.byref(c)) == 0, L.unet_last_error()
+    return c
+
+
+def test_c_abi_allreduce_world1(pkg, cuda):
+    """unique id -> init (rank 0 of 1) -> mean all-reduce of a ragged buffer
+    (bit-identical for one rank), eager and captured in a HIP graph (RCCL
+    collectives replay inside the graph: the capture the N > 1 graphed step
+    needs), then rejected arguments."""
+    L = importlib.import_module("image-segmentation-project_amd._lib").load()
+    c = _comm(L)
+    try:
+        buf = torch.randn(1_000_003, device="cuda")
+        ref = buf.clone()
+        st = torch.cuda.current_stream().cuda_stream
+        assert L.unet_allreduce_mean(c, buf.data_ptr(), buf.numel(), st) == 0, L.unet_last_error()
+        torch.cuda.synchronize()
+        assert torch.equal(buf, ref)
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                buf.mul_(3.0)
+                assert L.unet_allreduce_mean(c, buf.data_ptr(), buf.numel(), s.cuda_stream) == 0
+                buf.add_(1.0)
+        torch.cuda.current_stream().wait_stream(s)
+        buf.copy_(ref)
+        for _ in range(3):
+            g.replay()
+        torch.cuda.synchronize()
+        exp = ref.clone()
+        for _ in range(3):
+            exp = exp * 3.0 + 1.0
+        assert torch.equal(buf, exp)
+        assert L.unet_allreduce_mean(None, buf.data_ptr(), 4, st) != 0
+        assert L.unet_allreduce_bucket(c, None, buf.data_ptr(), 0, st) != 0
+    finally:
+        L.unet_allreduce_destroy(c)
+
+
+def test_c_abi_bucket_allreduce_after_native_backward(pkg, cuda):
+    """The native DDP sequence a C host runs: per-bucket hipEvents on, a training
+    forward + backward, then unet_allreduce_bucket for every bucket on a comm
+    stream (each waits on its bucket's event), the compute stream ordered after
+    it.  World 1: every gradient equal to the plain backward's (relative L2
+    <= 1e-5); the five buckets tile the flat gradient buffer."""
+    L = importlib.import_module("image-segmentation-project_amd._lib").load()
+    xs, ms = pkg.synthetic_cells(2, 128, 128, seed=5)
+    x, y = torch.from_numpy(xs).cuda(), torch.from_numpy(ms).cuda()
+    crit = pkg.get_loss_function({"loss_fn": "bce"})
+    torch.manual_seed(0)
+    m = pkg.UNetWithBackbone(pretrained=False, use_attention=False).cuda().train()
+
+    def step():
+        for p in m.parameters():
+            p.grad = None
+        crit(m(x), y).backward()
+
+    step()
+    torch.cuda.synchronize()
+    plain = [p.grad.detach().clone() for p in m.parameters()]
+    plan = m._last_plan
+    assert len(plan.buckets) == 5 and plan.buckets[-1][0] == 0
+    assert L.unet_plan_use_bucket_events(plan.handle, 1) == 0
+    c = _comm(L)
+
+    class NativeHook:  # the model's DDP hook (_run_backward), here bound straight to the C ABI
+        calls = 0
+
+        def reduce(self, pl, grads):
+            comm = torch.cuda.Stream()
+            grads.record_stream(comm)
+            for b in range(len(pl.buckets)):
+                assert L.unet_allreduce_bucket(c, pl.handle, grads.data_ptr(), b, comm.cuda_stream) == 0, \
+                    L.unet_last_error()
+            torch.cuda.current_stream().wait_stream(comm)
+            NativeHook.calls += 1
+
+    try:
+        m._ddp = NativeHook()
+        for _ in range(2):
+            step()
+            torch.cuda.synchronize()
+            # world 1: the mean is the identity; the rest is the backward's own
+            # run-to-run agreement (BN sums: fp64 replica atomics)
+            worst = max(_rel(a, b) for a, b in zip((p.grad for p in m.parameters()), plain) if b.norm() > 0)
+            assert worst <= 1e-5, worst
+        assert NativeHook.calls == 2
+    finally:
+        m._ddp = None
+        L.unet_allreduce_destroy(c)
+        L.unet_plan_use_bucket_events(plan.handle, 0)

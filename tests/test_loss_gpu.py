@@ -1,9 +1,11 @@
 """The loss sums kernel's fast transcendental path: BCE and the
 sigmoid terms in loss_accum use the hardware v_exp_f32 / v_log_f32 / v_rcp_f32
 with the exact-rounding log1p correction log1p(e) = log(u) * e / (u - 1).
-Checked here against an fp64 restatement of torch's formulation
-(losses.py:13-37,161-171: BCEWithLogits = (1 - y) x - log_sigmoid(x); Dice on
-sigmoid) where it is most delicate: confident logits |x| in [5, 20] (e =
+The BCE term is summed as max(x, 0) - y x + log1p(exp(-|x|)) -- torch's
+(1 - y) x - log_sigmoid(x) without its fp32 cancellation for confident
+logits (torch itself loses ~1 % at x = -10, y = 0).  Checked here against an
+fp64 restatement (losses.py:13-37,161-171: BCEWithLogits; Dice on sigmoid)
+where it is most delicate: confident logits |x| in [5, 20] (e =
 exp(-|x|) in [2e-9, 7e-3], u = 1 + e next to 1), both labels, so the summed
 terms range from ~1e-9 (confident and right) to ~20 (confident and wrong).
 Bars: every one of the 4 loss sums within 1e-6 relative of fp64 (fp32 terms
