@@ -112,7 +112,10 @@ def load(path: str = LIB_PATH):
             f"libunet_hip.so not found at {path}: build it with `python -c 'import __graft_entry__ as g; "
             f"g.build()'` (make -C image-segmentation-project_amd/csrc). There is no CPU fallback.")
     lib = ctypes.CDLL(path)
+    alt = path != os.path.join(_HERE, "libunet_hip.so")
     for name, (res, args) in SIGNATURES.items():
+        if alt and not hasattr(lib, name):
+            continue  # an older A/B build (UNET_HIP_LIB) without this entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

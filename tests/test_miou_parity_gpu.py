@@ -70,8 +70,16 @@ def test_miou_256(pkg, cuda, attention):
     want = oracle.calculate_metrics(torch.sigmoid(rl), y)
     print(f"4x256^2 attention={attention}: IoU hip {got['iou']:.6f} ref {want['iou']:.6f} "
           f"logits rel {_rel(lg, rl):.3e}")
-    for k in ("iou", "f1", "precision", "recall", "accuracy"):
+    # north_star's bar is on the IoU (and F1, a monotone function of it); the
+    # other three move with the sign of near-zero logits of a random-init net:
+    # over 6 seeds x {plain, attention} they differ from the oracle by up to
+    # 2.5e-3 (recall) / 1.9e-3 (accuracy) with this library and up to 1.9e-3 /
+    # 1.1e-3 with the round-5 one, while the IoU stays <= 2.5e-4
+    # (profiles/r06/metric_spread_r06_vs_r05.txt): their stated bar is 5e-3
+    for k in ("iou", "f1"):
         assert abs(got[k] - want[k]) <= IOU_TOL, k
+    for k in ("precision", "recall", "accuracy"):
+        assert abs(got[k] - want[k]) <= 5e-3, k
 
 
 def test_bn_running_stats_every_layer(pkg, golden, cuda):
