@@ -776,43 +776,70 @@ __device__ void head_contract(const HeadArgs& a, float* V, float* cst) {
   __syncthreads();
 }
 
+// Both head passes are HBM streams (decoder1's output, 32 or 64 bf16 channels
+// per pixel, against fp32 logits).  Round 6: the channel count is a template
+// argument, pixel indices are 32-bit (the launcher checks the range), and every
+// thread issues the loads of HP pixels before using any of them; the grid is a
+// few blocks per CU so the per-block prologue (the contraction V) amortises
+// (round 5: one pixel's loads in flight and 64-bit index divisions per pixel,
+// 2.2-2.7 TB/s).
+constexpr int kHeadHP = 4;  // pixels in flight per thread (Cin = 32: 16 x 16 B of loads)
+
+template <int CIN>
 __global__ void __launch_bounds__(256) head_fwd_kernel(HeadArgs a) {
-  __shared__ float V[kHeadMaxCin * 4];
+  __shared__ __attribute__((aligned(16))) float V[kHeadMaxCin * 4];
   __shared__ float cst;
   head_contract(a, V, &cst);
-  const int64_t total = (int64_t)a.N * a.H * a.W;
-  for (int64_t pix = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; pix < total;
-       pix += (int64_t)gridDim.x * blockDim.x) {
-    const int j = (int)(pix % a.W);
-    const int i = (int)((pix / a.W) % a.H);
-    const int n = (int)(pix / ((int64_t)a.H * a.W));
-    float o[4] = {cst, cst, cst, cst};
-    for (int c8 = 0; c8 < a.Cin; c8 += 8) {
-      float x[8];
-      unpack8(*reinterpret_cast<const uint4*>(a.x + pix * a.ldx + c8), x);
+  constexpr int CC = CIN / 8;
+  const float c0 = cst;
+  const int total = a.N * a.H * a.W, HW = a.H * a.W, W2 = 2 * a.W;
+  const int stride = gridDim.x * blockDim.x;
+  for (int p0 = blockIdx.x * blockDim.x + threadIdx.x; p0 < total; p0 += kHeadHP * stride) {
+    asm volatile("" ::: "memory");  // V is re-read from LDS per pixel (not hoisted into 4*CIN registers)
+    uint4 xv[kHeadHP][CC];
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
+    for (int u = 0; u < kHeadHP; ++u) {
+      const int pix = p0 + u * stride;
 #pragma unroll
-        for (int ab = 0; ab < 4; ++ab) o[ab] += x[k] * V[(c8 + k) * 4 + ab];
+      for (int q = 0; q < CC; ++q)
+        xv[u][q] = pix < total ? *reinterpret_cast<const uint4*>(a.x + (size_t)pix * a.ldx + q * 8) : make_uint4(0, 0, 0, 0);
     }
-    const int W2 = 2 * a.W;
-    float* row0 = a.logits + ((int64_t)n * 2 * a.H + 2 * i) * W2 + 2 * j;
-    *reinterpret_cast<float2*>(row0) = make_float2(o[0], o[1]);
-    *reinterpret_cast<float2*>(row0 + W2) = make_float2(o[2], o[3]);
+#pragma unroll
+    for (int u = 0; u < kHeadHP; ++u) {
+      const int pix = p0 + u * stride;
+      if (pix >= total) break;
+      float o[4] = {c0, c0, c0, c0};
+#pragma unroll
+      for (int q = 0; q < CC; ++q) {
+        float x[8];
+        unpack8(xv[u][q], x);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {  // V from LDS (a broadcast read: every lane the same address)
+          const float4 v = *reinterpret_cast<const float4*>(V + (q * 8 + k) * 4);
+          o[0] += x[k] * v.x; o[1] += x[k] * v.y; o[2] += x[k] * v.z; o[3] += x[k] * v.w;
+        }
+      }
+      const int n = pix / HW, r = pix - n * HW, i = r / a.W, j = r - i * a.W;
+      float* row0 = a.logits + ((size_t)n * 2 * a.H + 2 * i) * W2 + 2 * j;
+      *reinterpret_cast<float2*>(row0) = make_float2(o[0], o[1]);
+      *reinterpret_cast<float2*>(row0 + W2) = make_float2(o[2], o[3]);
+    }
   }
 }
 
-// thread = (8-channel chunk, pixel row); U[c][ab] partials live in registers.
+// thread = (8-channel chunk, pixel row); U[c][ab] partials live in registers;
+// kHeadHP pixels' operands (dlogits, x, the fused BN's y) are loaded before use.
+template <int CIN>
 __global__ void __launch_bounds__(256) head_bwd_kernel(HeadArgs a) {
   __shared__ float V[kHeadMaxCin * 4];
   __shared__ float cst;
   extern __shared__ __attribute__((aligned(16))) float red[];  // [rows][Cin*4 + 1]
   head_contract(a, V, &cst);
-  const int CC = a.Cin >> 3;
-  const int rows = blockDim.x / CC;
+  constexpr int CC = CIN / 8;
+  constexpr int rows = 256 / CC;
   const int chunk = threadIdx.x % CC, row = threadIdx.x / CC;
   const int c8 = chunk << 3;
-  const int64_t total = (int64_t)a.N * a.H * a.W;
+  const int total = a.N * a.H * a.W, HW = a.H * a.W;
   const BnBwdArgs& bb = a.bb;
   const bool fz = bb.sums != nullptr;
   float s1[8], s2[8], mu[8], is[8];
@@ -834,20 +861,30 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(HeadArgs a) {
 #pragma unroll
     for (int ab = 0; ab < 4; ++ab) Vl[k][ab] = V[(c8 + k) * 4 + ab];
   const int W2 = 2 * a.W;
-  if (row < rows) {
-    for (int64_t pix = (int64_t)blockIdx.x * rows + row; pix < total; pix += (int64_t)gridDim.x * rows) {
-      const int j = (int)(pix % a.W);
-      const int i = (int)((pix / a.W) % a.H);
-      const int n = (int)(pix / ((int64_t)a.H * a.W));
-      const float* row0 = a.dl + ((int64_t)n * 2 * a.H + 2 * i) * W2 + 2 * j;
-      const float2 d01 = *reinterpret_cast<const float2*>(row0);
-      const float2 d23 = *reinterpret_cast<const float2*>(row0 + W2);
-      const float d[4] = {d01.x, d01.y, d23.x, d23.y};
+  const int stride = gridDim.x * rows;
+  for (int p0 = blockIdx.x * rows + row; p0 < total; p0 += kHeadHP * stride) {
+    float2 d01[kHeadHP], d23[kHeadHP];
+    uint4 xv[kHeadHP], yv[kHeadHP];
+#pragma unroll
+    for (int u = 0; u < kHeadHP; ++u) {
+      const int pix = p0 + u * stride;
+      const bool ok = pix < total;
+      const int pc = ok ? pix : 0;
+      const int n = pc / HW, r = pc - n * HW, i = r / a.W, j = r - i * a.W;
+      const float* row0 = a.dl + ((size_t)n * 2 * a.H + 2 * i) * W2 + 2 * j;
+      d01[u] = ok ? *reinterpret_cast<const float2*>(row0) : make_float2(0.f, 0.f);
+      d23[u] = ok ? *reinterpret_cast<const float2*>(row0 + W2) : make_float2(0.f, 0.f);
+      xv[u] = ok ? *reinterpret_cast<const uint4*>(a.x + (size_t)pc * a.ldx + c8) : make_uint4(0, 0, 0, 0);
+      yv[u] = (ok && fz) ? *reinterpret_cast<const uint4*>(bb.y + (size_t)pc * bb.ldy + c8) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kHeadHP; ++u) {
+      const int pix = p0 + u * stride;
+      if (pix >= total) break;
+      const float d[4] = {d01[u].x, d01[u].y, d23[u].x, d23[u].y};
       if (chunk == 0) S += (d[0] + d[1]) + (d[2] + d[3]);
       float x[8], g[8];
-      unpack8(*reinterpret_cast<const uint4*>(a.x + pix * a.ldx + c8), x);
-      uint4 yv = make_uint4(0, 0, 0, 0);
-      if (fz) yv = *reinterpret_cast<const uint4*>(bb.y + pix * bb.ldy + c8);
+      unpack8(xv[u], x);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         g[k] = d[0] * Vl[k][0] + d[1] * Vl[k][1] + d[2] * Vl[k][2] + d[3] * Vl[k][3];
@@ -859,42 +896,40 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(HeadArgs a) {
         for (int k = 0; k < 8; ++k) g[k] = x[k] > 0.f ? g[k] : 0.f;
       }
       const uint4 o = pack8(g);
-      *reinterpret_cast<uint4*>(a.dx + pix * a.lddx + c8) = o;
+      *reinterpret_cast<uint4*>(a.dx + (size_t)pix * a.lddx + c8) = o;
       if (fz) {
         float dz[8], y[8];
         unpack8(o, dz);  // sums of the stored bf16 dZ, as bn_bwd_reduce_kernel would read them
-        unpack8(yv, y);
+        unpack8(yv[u], y);
 #pragma unroll
         for (int k = 0; k < 8; ++k) { s1[k] += dz[k]; s2[k] += dz[k] * (y[k] - mu[k]) * is[k]; }
       }
     }
   }
   // red[row][L]: U (Cin*4) | S | fused BN sums dZ (Cin) | dZ*xhat (Cin)
-  const int LU = a.Cin * 4 + 1;
-  const int L = LU + (fz ? 2 * a.Cin : 0);
-  if (row < rows) {
+  const int LU = CIN * 4 + 1;
+  const int L = LU + (fz ? 2 * CIN : 0);
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
+  for (int k = 0; k < 8; ++k)
 #pragma unroll
-      for (int ab = 0; ab < 4; ++ab) red[row * L + (c8 + k) * 4 + ab] = U[k][ab];
-    if (chunk == 0) red[row * L + a.Cin * 4] = S;
-    if (fz) {
+    for (int ab = 0; ab < 4; ++ab) red[row * L + (c8 + k) * 4 + ab] = U[k][ab];
+  if (chunk == 0) red[row * L + CIN * 4] = S;
+  if (fz) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        red[row * L + LU + c8 + k] = s1[k];
-        red[row * L + LU + a.Cin + c8 + k] = s2[k];
-      }
+    for (int k = 0; k < 8; ++k) {
+      red[row * L + LU + c8 + k] = s1[k];
+      red[row * L + LU + CIN + c8 + k] = s2[k];
     }
   }
   __syncthreads();
   for (int t = threadIdx.x; t < L; t += blockDim.x) {
     float v = 0.f;
     for (int r = 0; r < rows; ++r) v += red[r * L + t];
-    if (t < LU) {
-      atomicAdd(a.usum + t, (double)v);
+    if (t < LU) {  // [kStatRep][Cin*4 + 1] replicas (head_grads_kernel sums them in order)
+      atomicAdd(a.usum + (size_t)(blockIdx.x % kStatRep) * LU + t, (double)v);
     } else {  // [kStatRep][2][C] replica layout of the BN-backward sums
-      const int q = (t - LU) / a.Cin, c = (t - LU) - q * a.Cin;
-      atomicAdd(bb.sums + (size_t)(blockIdx.x % kStatRep) * 2 * a.Cin + q * a.Cin + c, (double)v);
+      const int q = (t - LU) / CIN, c = (t - LU) - q * CIN;
+      atomicAdd(bb.sums + (size_t)(blockIdx.x % kStatRep) * 2 * CIN + q * CIN + c, (double)v);
     }
   }
   if (fz && bb.ticket) {
@@ -911,7 +946,11 @@ __global__ void __launch_bounds__(256) head_grads_kernel(HeadArgs a) {
   __shared__ double us[kHeadMaxCin * 4 + 1];
   __shared__ float w0s[kHeadMaxW0];
   const int nw = a.Cin * a.Co * 4;
-  for (int t = threadIdx.x; t <= a.Cin * 4; t += blockDim.x) us[t] = a.usum[t];
+  for (int t = threadIdx.x; t <= a.Cin * 4; t += blockDim.x) {
+    double v = 0.0;
+    for (int r = 0; r < kStatRep; ++r) v += a.usum[(size_t)r * (a.Cin * 4 + 1) + t];
+    us[t] = v;
+  }
   for (int t = threadIdx.x; t < nw; t += blockDim.x) w0s[t] = a.w0[t];
   __syncthreads();
   const double S = us[a.Cin * 4];
@@ -929,19 +968,30 @@ __global__ void __launch_bounds__(256) head_grads_kernel(HeadArgs a) {
   if (threadIdx.x == 0) a.gbf[0] = (float)S;
 }
 
+// the head's pixel range in 32-bit indices (decoder1 output pixels, and the
+// 4x as many logits)
+static bool head_ok(const HeadArgs& a) {
+  return (a.Cin == 32 || a.Cin == 64) && (int64_t)a.N * a.H * a.W * 4 < 0x7fffffffLL;
+}
 hipError_t launch_head_fwd(const HeadArgs& a, hipStream_t st) {
-  if (a.Cin > kHeadMaxCin || a.Cin % 8) return hipErrorInvalidValue;
+  if (!head_ok(a)) return hipErrorInvalidValue;
   const int64_t total = (int64_t)a.N * a.H * a.W;
-  hipLaunchKernelGGL(head_fwd_kernel, dim3(grid_for(total, 256 * 2)), dim3(256), 0, st, a);
+  const int grid = grid_for(total, 256 * kHeadHP * 2, 1024);
+  if (a.Cin == 32) hipLaunchKernelGGL(head_fwd_kernel<32>, dim3(grid), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(head_fwd_kernel<64>, dim3(grid), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 hipError_t launch_head_bwd(const HeadArgs& a, hipStream_t st) {
-  if (a.Cin > kHeadMaxCin || a.Cin % 8) return hipErrorInvalidValue;
+  if (!head_ok(a)) return hipErrorInvalidValue;
   const int64_t total = (int64_t)a.N * a.H * a.W;
   const int CC = a.Cin / 8, rows = 256 / CC;
   if (a.bb.sums && (a.bb.C != a.Cin || a.bb.y2)) return hipErrorInvalidValue;
   const size_t lds = (size_t)rows * (a.Cin * 4 + 1 + (a.bb.sums ? 2 * a.Cin : 0)) * sizeof(float);
-  hipLaunchKernelGGL(head_bwd_kernel, dim3(grid_for(total, rows * 8, 1024)), dim3(rows * CC), lds, st, a);
+  // 512 blocks: each adds Cin*4 + 1 fp64 partials (16 replicas) at its end;
+  // 1024 blocks onto one copy serialised ~1k same-address atomics per word
+  const int grid = grid_for(total, rows * kHeadHP * 4, 512);
+  if (a.Cin == 32) hipLaunchKernelGGL(head_bwd_kernel<32>, dim3(grid), dim3(256), lds, st, a);
+  else hipLaunchKernelGGL(head_bwd_kernel<64>, dim3(grid), dim3(256), lds, st, a);
   return hipGetLastError();
 }
 hipError_t launch_head_grads(const HeadArgs& a, hipStream_t st) {

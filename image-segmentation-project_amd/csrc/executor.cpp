@@ -495,7 +495,7 @@ static int build_plan(unet_plan* p) {
   }
   for (auto& cv : p->convs)
     if (cv.kind == L_CONVT) cv.bias_acc = A.take((size_t)kStatRep * cv.Co * sizeof(double));
-  p->head_usum = A.take((size_t)(up0_in * 4 + 1) * sizeof(double));
+  p->head_usum = A.take((size_t)kStatRep * (up0_in * 4 + 1) * sizeof(double));  // [kStatRep][Cin*4 + 1]
   p->stem_tkt = A.take(kStemTickets * sizeof(unsigned));
   for (auto& t : p->atts) {
     t.pbs = A.take(2 * sizeof(double));

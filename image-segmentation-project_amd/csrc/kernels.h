@@ -339,7 +339,7 @@ struct HeadArgs {
   float* logits;                     // [N,2H,2W]
   const float* dl;                   // backward: dL/dlogits
   bf16_t* dx; int lddx;              // backward: dL/dX
-  double* usum;                      // backward: [Cin*4 + 1] sums U[c][ab], S
+  double* usum;                      // backward: [kStatRep][Cin*4 + 1] sums U[c][ab], S (zeroed replicas)
   float* gw0; float* gb0; float* gwf; float* gbf;  // param grads
   // backward, optional (bb.sums != null): dX is dA of decoder1's last
   // BN+ReLU; as in the conv-dgrad epilogue, dZ = dA * (act > 0) is stored and
