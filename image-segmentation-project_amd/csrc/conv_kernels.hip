@@ -589,7 +589,7 @@ conv_glds_kernel(ConvFwdArgs a) {
       int ih, iw;
       if constexpr (MODE != MODE_TRANS) {  // MODE_FWD, MODE_SHUF (1x1 over the input grid)
         ih = aa[j] * st - a.pad + r;
-        iw = ab[j] * st - a.pad + s;
+        iw = ab[j] * (a.stride_w ? a.stride_w : st) - a.pad + s;
       } else {
         ih = aa[j] + (py + a.pad - r) / st;
         iw = ab[j] + (px_ + a.pad - s) / st;
@@ -2413,6 +2413,8 @@ hipError_t launch_conv_fwd_f8(const ConvFwdArgs& a, hipStream_t st) {
 
 
 hipError_t launch_conv_fwd(const ConvFwdArgs& a0, int mode, hipStream_t st) {
+  // a separate column stride exists in the LDS-DMA implicit GEMM's forward only
+  if (a0.stride_w && (mode != MODE_FWD || a0.C % 64 || a0.x2 || a0.ysplit || a0.xform)) return hipErrorInvalidValue;
   // the folded downsample range exists only in the LDS-DMA transposed kernel
   if (a0.x2 && (mode != MODE_TRANS || a0.C2 != a0.C || a0.stride != 2 || a0.pad != 1))
     return hipErrorInvalidValue;

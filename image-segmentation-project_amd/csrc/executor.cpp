@@ -1017,6 +1017,17 @@ int conv_dgrad(const Ctx& x, int ci, const Act& dy, const Act& dx, const Act* ad
     CK(launch_conv3x3_fl(a, 1, x.st));
     return 0;
   }
+  if (cv.kind == L_CONVT && dy.ld == cv.Co && (2 * cv.Co) % 64 == 0 && dy.W % 2 == 0 && !a.x2 && !a.ysplit) {
+    // ConvTranspose2d(k2, s2) data gradient = the k2s2 conv of dY.  Output
+    // pixel (i, j) reads dY rows 2i, 2i+1 at columns 2j, 2j+1: in a dense dY
+    // those column pairs are one contiguous 2*Co-channel "pixel", so the conv
+    // runs as R = 2, S = 1, stride (2, 1) over W/2 merged pixels with K steps of
+    // whole 128-B lines (the round-5 form staged 64-B half lines per tap).  The
+    // PK_CONVT_DGRAD pack [Ci][a][b][Co] is already the [Ci][a][b*Co + c]
+    // layout this view reads.
+    a.W = dy.W / 2; a.C = 2 * cv.Co; a.ldx = 2 * dy.ld;
+    a.R = 2; a.S = 1; a.stride = 2; a.stride_w = 1; a.pad = 0;
+  }
   CK(launch_conv_fwd(a, cv.kind == L_CONVT ? MODE_FWD : MODE_TRANS, x.st));
   return 0;
 }

@@ -108,6 +108,11 @@ struct ConvFwdArgs {
   int N, H, W, C;                // input geometry (C = GEMM reduction channels)
   int P, Q, Cout;                // output geometry
   int R, S, stride, pad;
+  // MODE_FWD implicit GEMM only: a column stride other than `stride` (0 = the
+  // same).  The ConvTranspose data gradient runs as R = 2, S = 1, stride (2, 1)
+  // over a view of dY that merges each pair of adjacent pixels into one of 2C
+  // channels, so every K step stages whole 128-B lines (conv_dgrad)
+  int stride_w;
   int mblocks, nblocks, Pc, Qc;  // filled by the launcher
   // persistent kernels (conv3x3_fl_kernel): 0 = one block per CU; > 0 caps the
   // grid (single-op tests: several work items per block)
