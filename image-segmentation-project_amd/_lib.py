@@ -74,6 +74,8 @@ SIGNATURES = {
     "unet_conv3x3_fl": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p,
                                 c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                 c_void_p, c_void_p, c_void_p] + [c_int] * 7 + [c_void_p]),
+    "unet_convt2x2": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int,
+                              c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 7 + [c_void_p]),
     "unet_f8_quantize": (c_int, [c_void_p, c_int, c_int, c_int64, c_void_p, c_void_p, c_int, c_void_p]),
     "unet_f8_pack_weight": (c_int, [c_void_p] + [c_int] * 4 + [c_void_p, c_void_p, c_int, c_void_p]),
     "unet_f8_roll": (c_int, [c_void_p, c_int, c_void_p]),

@@ -961,6 +961,13 @@ int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for
     CK(launch_conv3x3_fl(a, 0, x.st));
     return 0;
   }
+  if (cv.kind == L_CONVT) {  // weight-stationary up-conv (convt.hip) where it covers the shape
+    const hipError_t e = launch_convt2x2(a, 0, x.st);
+    if (e != hipErrorNotSupported) {
+      CK(e);
+      return 0;
+    }
+  }
   CK(launch_conv_fwd(a, cv.kind == L_CONVT ? MODE_SHUF : MODE_FWD, x.st));
   return 0;
 }
@@ -984,9 +991,12 @@ bool xform_ok(const Ctx& x, int ci, const Act& yraw, const Act& h, const Act& ou
 // the epilogue stores dZ and runs the BN-backward reduction (ConvFwdArgs::bb).
 // ds >= 0: the block's 1x1/s2 downsample dgrad (dY = dyds) is folded into this
 // 3x3/s2 conv1 dgrad as a second reduction range of parity class 0.
+// convT only: bias_acc = the up-conv's bias-gradient replicas; *bias_done tells
+// whether the launch summed them (the weight-stationary kernel does, in the
+// same pass over dY)
 int conv_dgrad(const Ctx& x, int ci, const Act& dy, const Act& dx, const Act* add,
                const BnBwdArgs* fuse = nullptr, int ds = -1, const Act* dyds = nullptr,
-               const Act* dx_split = nullptr) {
+               const Act* dx_split = nullptr, double* bias_acc = nullptr, bool* bias_done = nullptr) {
   const Conv& cv = x.p->convs[ci];
   const double fl = conv_flops(x.p, cv, dy) + (ds >= 0 ? conv_flops(x.p, x.p->convs[ds], *dyds) : 0.0);
   ProfScope ps(x.p, x.st, "dgrad " + pname(x, cv.w) + (ds >= 0 ? " +ds" : ""), fl);
@@ -1016,6 +1026,19 @@ int conv_dgrad(const Ctx& x, int ci, const Act& dy, const Act& dx, const Act* ad
     a.w = nullptr;
     CK(launch_conv3x3_fl(a, 1, x.st));
     return 0;
+  }
+  if (bias_done) *bias_done = false;
+  if (cv.kind == L_CONVT) {  // weight-stationary up-conv (convt.hip): its own geometry, the input grid
+    ConvFwdArgs b = a;
+    b.H = dx.H; b.W = dx.W; b.C = cv.Ci; b.Cout = cv.Co;
+    b.P = dy.H; b.Q = dy.W;
+    b.bias_acc = bias_acc;
+    const hipError_t e = launch_convt2x2(b, 1, x.st);
+    if (e != hipErrorNotSupported) {
+      CK(e);
+      if (bias_done) *bias_done = bias_acc != nullptr;
+      return 0;
+    }
   }
   if (cv.kind == L_CONVT && dy.ld == cv.Co && (2 * cv.Co) % 64 == 0 && dy.W % 2 == 0 && !a.x2 && !a.ysplit) {
     // ConvTranspose2d(k2, s2) data gradient = the k2s2 conv of dY.  Output
@@ -1740,16 +1763,19 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     const Act du = att ? p->atts[l].du : d.dcat_up;
     RUN(fork());
     RUN(conv_wgrad(x, d.up, du, d.up_in));
-    {
-      ProfScope ps(p, x.wst, "bias_sum", 0);
-      // the replicas become the fp32 gradient in bucket 0's unpack launch (UP_D2F)
-      CK(launch_channel_sum(x.A(du), du.ld, (int64_t)N * du.H * du.W, up.Co, x.W<double>(up.bias_acc), x.wst));
-    }
     const BnBwdArgs fu = l > 0 ? dec_bn2(l - 1) : blk_bn2(nb - 1);
     // with attention the up-conv input of levels 3..1 is the channel-gated
     // output: its gradient is not dA of a BN
     const bool fuse_up = fz && (l == 0 || !att);
-    RUN(conv_dgrad(x, d.up, du, d.d_up_in, nullptr, fuse_up ? &fu : nullptr));
+    // the bias gradient (replicas -> fp32 in bucket 0's unpack launch, UP_D2F)
+    // rides in the data-gradient pass when its kernel covers the shape
+    bool bias_fused = false;
+    RUN(conv_dgrad(x, d.up, du, d.d_up_in, nullptr, fuse_up ? &fu : nullptr, -1, nullptr, nullptr,
+                   x.W<double>(up.bias_acc), &bias_fused));
+    if (!bias_fused) {
+      ProfScope ps(p, x.wst, "bias_sum", 0);
+      CK(launch_channel_sum(x.A(du), du.ld, (int64_t)N * du.H * du.W, up.Co, x.W<double>(up.bias_acc), x.wst));
+    }
   }
   // bucket 0 also holds the head's and the decoder biases' gradients (main stream)
   RUN(stream_edge(p, st, x.wst));
@@ -2138,6 +2164,36 @@ int unet_conv_fwd(const void* x, int ldx, const void* w, void* y, int ldy, const
   a.R = R; a.S = S; a.stride = stride; a.pad = pad;
   if (mode < 0 || mode > 2) { set_err("bad mode"); return 1; }
   CK(launch_conv_fwd(a, mode, stream));
+  return 0;
+}
+
+int unet_convt2x2(const void* x, int ldx, const void* w, void* y, int ldy, const float* bias, const void* act,
+                  int ldact, const void* yraw, int ldyraw, const float* mean, const float* invstd, double* bsums,
+                  double* bias_acc, int N, int H, int W, int Ci, int Co, int mode, int grid, hipStream_t stream) {
+  if (mode != 0 && mode != 1) { set_err("unet_convt2x2: mode must be 0 (forward) or 1 (data gradient)"); return 1; }
+  if (mode == 0 && (bsums || bias_acc)) { set_err("unet_convt2x2: bsums / bias_acc belong to the data gradient"); return 1; }
+  if (bsums && (!act || !yraw || !mean || !invstd)) {
+    set_err("unet_convt2x2: fused BN backward needs act, yraw, mean, invstd");
+    return 1;
+  }
+  ConvFwdArgs a = {};
+  a.x = (const bf16_t*)x; a.ldx = ldx; a.w = (const bf16_t*)w; a.y = (bf16_t*)y; a.ldy = ldy;
+  a.bias = mode == 0 ? bias : nullptr;
+  a.N = N; a.H = H; a.W = W; a.C = Ci; a.Cout = Co; a.P = 2 * H; a.Q = 2 * W;
+  a.R = 2; a.S = 2; a.stride = 2; a.pad = 0;
+  a.grid_cap = grid;
+  a.bias_acc = bias_acc;
+  if (bsums) {
+    a.bb.act = (const bf16_t*)act; a.bb.ldact = ldact; a.bb.y = (const bf16_t*)yraw; a.bb.ldy = ldyraw;
+    a.bb.mean = mean; a.bb.invstd = invstd; a.bb.sums = bsums;
+    a.bb.npix = (int64_t)N * H * W; a.bb.C = Ci; a.bb.relu = 1;
+  }
+  const hipError_t e = launch_convt2x2(a, mode, stream);
+  if (e == hipErrorNotSupported) {
+    set_err("unet_convt2x2: shape / alignment not covered ((Ci, Co) in {(64,32),(64,64),(128,64)}, N*H*W % 32)");
+    return 1;
+  }
+  CK(e);
   return 0;
 }
 

@@ -114,9 +114,13 @@ struct ConvFwdArgs {
   // channels, so every K step stages whole 128-B lines (conv_dgrad)
   int stride_w;
   int mblocks, nblocks, Pc, Qc;  // filled by the launcher
-  // persistent kernels (conv3x3_fl_kernel): 0 = one block per CU; > 0 caps the
-  // grid (single-op tests: several work items per block)
+  // persistent kernels (conv3x3_fl_kernel, convt2x2_kernel): 0 = one block per
+  // CU (two for the up-conv); > 0 caps the grid (single-op tests: several
+  // work items per block)
   int grid_cap;
+  // ConvTranspose data gradient (launch_convt2x2 mode 1): the up-conv's bias
+  // gradient, sum of dY, added into replicas [kStatRep][Co] (fp64), or null
+  double* bias_acc;
   // in-kernel phase stamps (debug build -DUNET_TIMING only, null otherwise):
   // [block < kTimBlocks][kTimSlots] s_memtime values (scripts/conv_timing.py)
   unsigned long long* tim;
@@ -182,6 +186,13 @@ bool conv3x3_fl_shape(int N, int C, int Cout, int P, int Q);
 // launch shapes that do not fill the chip)
 bool conv3x3_fl_geom(int C, int Cout, int P, int Q);
 hipError_t launch_conv3x3_fl(const ConvFwdArgs& a, int mode, hipStream_t st);
+// ConvTranspose2d(k2, s2) (convt.hip): N, H, W = the INPUT-resolution grid, C =
+// Ci, Cout = Co.  mode 0 forward: x = X [.., Ci], w = PK_CONVT_FWD pack, y = Y
+// [N, 2H, 2W] (+ bias); mode 1 data gradient: x = dY [N, 2H, 2W, Co], w =
+// PK_CONVT_DGRAD pack, y = dX (+ the fused BN backward bb, + bias_acc).
+// hipErrorNotSupported for shapes it does not cover (the caller falls back to
+// the implicit-GEMM path).
+hipError_t launch_convt2x2(const ConvFwdArgs& a, int mode, hipStream_t st);
 // weight-stationary full-line conv for C == 64 (conv_fl.hip), standard weight
 // pack; launch_conv3x3_ws uses it where conv3x3_ws2_ok holds (UNET_NO_WS2=1: never)
 bool conv3x3_ws2_ok(const ConvFwdArgs& a, bool flip);

@@ -215,6 +215,22 @@ int unet_conv3x3_fl(const void* x, int ldx, const void* wch, void* y, int ldy, c
                     int ldyraw, const float* mean, const float* invstd, const void* yraw2, int ldyraw2,
                     const float* mean2, const float* invstd2, double* bsums, double* bsums2, int N, int H,
                     int W, int C, int Cout, int mode, int grid, hipStream_t stream);
+/* The weight-stationary ConvTranspose2d(k2, s2) (convt2x2_kernel: the narrow
+ * decoder up-convs, advanced_models.py:96-99 upconv2 / upconv1, applied at
+ * :305,315) as a single op.  N, H, W = the INPUT-resolution grid; (Ci, Co) in
+ * {(64, 32), (64, 64), (128, 64)}; N*H*W % 32 == 0; 16-B aligned x / w, 8-B
+ * aligned y, ldx % 8 == 0, ldy % 4 == 0.
+ * mode 0 (forward): x = X [N,H,W] (ld ldx >= Ci), w = unet_pack_weight kind 2
+ *   of the [Ci][Co][2][2] weight, y = Y [N,2H,2W] (ld ldy) = convT(X) + bias.
+ * mode 1 (data gradient): x = dY [N,2H,2W] (ld ldx >= Co), w = kind 3 pack,
+ *   y = dX [N,H,W] (ld ldy); bsums != null: the fused BN(+ReLU) backward as
+ *   unet_conv3x3_fl mode 1 (act, yraw, mean, invstd over Ci channels,
+ *   bsums[16][2][Ci]); bias_acc != null: bias_acc[16][Co] += the bias
+ *   gradient sum of dY (fp64, caller zeroes).
+ * grid: 0 = the production persistent grid; > 0 caps it. */
+int unet_convt2x2(const void* x, int ldx, const void* w, void* y, int ldy, const float* bias, const void* act,
+                  int ldact, const void* yraw, int ldyraw, const float* mean, const float* invstd, double* bsums,
+                  double* bias_acc, int N, int H, int W, int Ci, int Co, int mode, int grid, hipStream_t stream);
 /* ---- fp8 e4m3 forward conv (BASELINE.json configs[4]; no reference counterpart:
  * the reference's convs are fp32 torch.nn.Conv2d, advanced_models.py:72-100) ----
  * state: 16-B scale state {amax prev (float bits), amax this step, e8m0 code,
