@@ -474,7 +474,13 @@ __device__ __forceinline__ int swz_chunk(int row, int p) {  // physical slot p -
   else return p ^ ((0x78 >> (((row >> 2) & 3) << 1)) & 3);
 }
 
-template <int MODE, int BM, int BN, int BK, int NS, int WM, int WN>
+// DS (MODE_FWD): the block's 1x1 / stride-2 downsample (ConvFwdArgs::wds) rides
+// along: its weight tile [BN][C] is staged once (cchunks sub-tiles behind the
+// pipeline stages) and multiplied with the centre tap's A stages, whose pixels
+// (2 oh, 2 ow) are exactly the downsample's input; a second accumulator set and
+// a second epilogue (yds, its BN sums).  The separate downsample launch and its
+// re-read of the input disappear.
+template <int MODE, int BM, int BN, int BK, int NS, int WM, int WN, bool DS = false>
 __global__ void __launch_bounds__(WM * WN * 64)
 conv_glds_kernel(ConvFwdArgs a) {
   constexpr int NW = WM * WN;          // 4 or 8 waves
@@ -520,6 +526,9 @@ conv_glds_kernel(ConvFwdArgs a) {
   const bool ext = MODE == MODE_TRANS && a.x2 != nullptr && cls == 0;
   const int KT = KT1 + (ext ? a.C2 / BK : 0);
   const int Ktot = a.R * a.S * a.C;
+  static_assert(!DS || MODE == MODE_FWD, "the downsample fold is a forward");
+  const int ctap = DS ? (a.R / 2) * a.S + a.S / 2 : -1;  // centre tap (stride-2, pad-1 3x3: pixel (2 oh, 2 ow))
+  char* const W2 = smem + NS * STAGE;                        // DS: [cchunks][B tile]
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, (unsigned)((size_t)a.N * a.H * a.W * a.ldx * 2));
   const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (unsigned)((size_t)a.Cout * Ktot * 2));
   const __amdgpu_buffer_rsrc_t x2r = make_rsrc(ext ? a.x2 : a.x, ext ? (unsigned)((size_t)a.N * a.H * a.W * a.ldx2 * 2) : 0u);
@@ -608,10 +617,29 @@ conv_glds_kernel(ConvFwdArgs a) {
   };
 
   f32x4 acc[FN][FM];
+  f32x4 acc2[DS ? FN : 1][DS ? FM : 1];
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
     for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (DS) {
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // the downsample weight tile, every K sub-tile, before the first stage
+    // (older than it: the first stage's counted wait covers these loads)
+    const __amdgpu_buffer_rsrc_t wdr = make_rsrc(a.wds, (unsigned)((size_t)a.Cout * a.C * 2));
+    for (int cc = 0; cc < cchunks; ++cc) {
+#pragma unroll
+      for (int j = 0; j < B_INS; ++j) {
+        const int row = (wave * B_INS + j) * RPI + lrow;  // downsample pack row n0 + row: [Cout][C]
+        const bool ok = row < BN && n0 + row < a.Cout;
+        const unsigned off = ok ? (unsigned)((n0 + row) * a.C + cc * BK + bch[j] * 8) * 2u : kOOB;
+        glds16(wdr, W2 + cc * B_BYTES + (wave * B_INS + j) * 1024, off);
+      }
+    }
+  }
 
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
@@ -641,11 +669,31 @@ conv_glds_kernel(ConvFwdArgs a) {
 #pragma unroll
         for (int j = 0; j < FM; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
+      if constexpr (DS) {
+        if (kt / cchunks == ctap) {  // the centre tap's A tile x the downsample weights
+          const char* Ws = W2 + (kt % cchunks) * B_BYTES;
+#pragma unroll
+          for (int i = 0; i < FN; ++i) {
+            const bf16x8 w2 = *reinterpret_cast<const bf16x8*>(Ws + frag_off<BK>(wn * WTN + i * 16 + (lane & 15), ch));
+#pragma unroll
+            for (int j = 0; j < FM; ++j)
+              acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2, xf[j], acc2[i][j], 0, 0, 0);
+          }
+        }
+      }
     }
   }
   wait_vmcnt<0>();
   __syncthreads();
   conv_epilogue<MODE, BN, WM, WN, FM, FN>(a, acc, smem, m0, n0, Mtot, py, px_);
+  if constexpr (DS) {
+    ConvFwdArgs d = a;  // the downsample's epilogue: its output and BN sums, no bias
+    d.y = a.yds; d.ldy = a.ldyds;
+    d.stats = a.stats_ds; d.bn = a.bnds;
+    d.bias = nullptr; d.add = nullptr; d.fold_on = 0;
+    __syncthreads();  // the first epilogue's LDS reduction is read
+    conv_epilogue<MODE, BN, WM, WN, FM, FN>(d, acc2, smem, m0, n0, Mtot, py, px_);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2259,7 +2307,7 @@ static hipError_t launch_fwd_cfg(const ConvFwdArgs& a0, int classes, hipStream_t
   return hipGetLastError();
 }
 
-template <int MODE, int BM, int BN, int BK, int NS, int WM, int WN>
+template <int MODE, int BM, int BN, int BK, int NS, int WM, int WN, bool DS = false>
 static hipError_t launch_glds_cfg(const ConvFwdArgs& a0, int classes, hipStream_t st) {
   ConvFwdArgs a = a0;
   a.nblocks = (a.Cout + BN - 1) / BN;
@@ -2275,12 +2323,15 @@ static hipError_t launch_glds_cfg(const ConvFwdArgs& a0, int classes, hipStream_
     const int kt = a.R * a.S * (a.C / BK);
     if (kt >= 1 && kt < stages) stages = kt;
   }
+  if (DS) stages = NS;  // the downsample tile sits behind all NS stages
   size_t lds = (size_t)stages * (BM + B_ROWS) * ROWB;
+  if (DS) lds += (size_t)(a.C / BK) * B_ROWS * ROWB;
   const size_t red = (size_t)WM * BN * 3 * sizeof(float) + 16;
   if (red > lds) lds = red;
   dim3 grid(a.mblocks * a.nblocks, 1, classes);
-  set_kernel_tag("conv_glds_kernel<%d, %d, %d, %d, %d, %d, %d>", MODE, BM, BN, BK, NS, WM, WN);
-  hipLaunchKernelGGL((conv_glds_kernel<MODE, BM, BN, BK, NS, WM, WN>), grid, dim3(NW * 64), lds, st, a);
+  set_kernel_tag(DS ? "conv_glds_kernel<%d, %d, %d, %d, %d, %d, %d> +ds" : "conv_glds_kernel<%d, %d, %d, %d, %d, %d, %d>",
+                 MODE, BM, BN, BK, NS, WM, WN);
+  hipLaunchKernelGGL((conv_glds_kernel<MODE, BM, BN, BK, NS, WM, WN, DS>), grid, dim3(NW * 64), lds, st, a);
   return hipGetLastError();
 }
 
@@ -2323,6 +2374,32 @@ static hipError_t launch_glds_fixed(const ConvFwdArgs& a, int classes, int cfg, 
     case 23: return bk64 ? launch_glds_cfg<MODE, 256, 128, 64, 3, 4, 2>(a, classes, st) : hipErrorNotSupported;
     case 24: return launch_glds_cfg<MODE, 256, 64, 32, 3, 4, 2>(a, classes, st);
     case 25: return bk64 ? launch_glds_cfg<MODE, 64, 64, 64, 3, 2, 4>(a, classes, st) : hipErrorNotSupported;
+    default: return hipErrorNotSupported;
+  }
+}
+
+// forward with the folded downsample (MODE_FWD, a.wds): the stride-2 conv1
+// tiles launch_glds picks for these shapes (enc3.0 / enc4.0 conv1).  0: not
+// folded; 1: 128 x 128 3-stage tiles; 2: 64 x 64 3-stage tiles.  enc2.0 (2-stage
+// 128 x 128 tiles, 512 blocks) is not: the second accumulator set (169 VGPRs)
+// halves its blocks per CU and the fused launch measured slower than the two
+// separate ones (61.9 vs 38.0 + 21.8 us)
+static int glds_ds_cfg(const ConvFwdArgs& a) {
+  if (a.C % 64 || a.R != 3 || a.S != 3 || a.stride != 2 || a.pad != 1 || a.stride_w || a.ldyds % 4 || a.add ||
+      a.fold_on || a.bb.sums || a.x2 || a.ysplit || a.xform || a.P * 2 != a.H + (a.H & 1) || a.Q * 2 != a.W + (a.W & 1))
+    return 0;
+  const long long M = (long long)a.N * a.P * a.Q;
+  auto nblk = [&](long long bm, long long bn) { return ((M + bm - 1) / bm) * ((a.Cout + bn - 1) / bn); };
+  if (a.Cout == 256 && nblk(128, 128) >= 240) return 1;
+  if (a.Cout > 64 && nblk(128, 128) >= 240) return 0;
+  return 2;
+}
+bool conv_fwd_ds_ok(const ConvFwdArgs& a) { return glds_ds_cfg(a) != 0; }
+static hipError_t launch_glds_ds(const ConvFwdArgs& a, hipStream_t st) {
+  if (!a.yds) return hipErrorInvalidValue;
+  switch (glds_ds_cfg(a)) {
+    case 1: return launch_glds_cfg<MODE_FWD, 128, 128, 64, 3, 2, 4, true>(a, 1, st);
+    case 2: return launch_glds_cfg<MODE_FWD, 64, 64, 64, 3, 2, 2, true>(a, 1, st);
     default: return hipErrorNotSupported;
   }
 }
@@ -2436,9 +2513,16 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a0, int mode, hipStream_t st) {
     a.Pc = a.H; a.Qc = a.W;
     return launch_glds<MODE_SHUF>(a, 1, st);
   }
+  if (a0.wds && (mode != MODE_FWD || a0.C % 64)) return hipErrorInvalidValue;
   if (mode != MODE_STEM && a0.C % 32 == 0) {
     ConvFwdArgs a = a0;
     if ((size_t)a.N * a.H * a.W * a.ldx * 2 >= 0x80000000ull) return hipErrorInvalidValue;
+    if (a.wds) {  // the folded downsample exists in the implicit-GEMM forward only
+      if ((size_t)a.N * a.P * a.Q * a.ldyds * 2 >= 0x80000000ull) return hipErrorInvalidValue;
+      a.Pc = a.P;
+      a.Qc = a.Q;
+      return launch_glds_ds(a, st);
+    }
     if (g_cfg_override <= 0) {
       const hipError_t e = launch_conv3x3_ws(a, mode == MODE_TRANS ? 1 : 0, st);
       if (e != hipErrorNotSupported) return e;

@@ -908,10 +908,31 @@ const std::string& pname(const Ctx& x, int param) { return x.p->params[param].na
 // xbn >= 0 (training): `in` is the RAW output of the previous conv; BN xbn +
 // ReLU is applied while staging and the activation is stored to *xh by the
 // conv itself (ConvFwdArgs::xform), replacing that BN's bn_apply pass
-int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for_stats, int fold_bn = -1,
-                 bool relu = false, const Act* res = nullptr, int xbn = -1, const Act* xh = nullptr) {
+// ds >= 0 (training, the 3x3 / stride-2 conv1 of a downsample block): that
+// 1x1 / stride-2 downsample (output *yds, BN dsbn's sums) rides in the same
+// launch when the implicit-GEMM forward takes it; *ds_done says whether it did
+bool ds_fold_fwd_ok(const Ctx& x, int ci, int ds) {
   const Conv& cv = x.p->convs[ci];
-  ProfScope ps(x.p, x.st, "fwd " + pname(x, cv.w) + (xbn >= 0 ? " +bn" : ""), conv_flops(x.p, cv, out));
+  if (ds < 0 || !x.training || cv.f8 || cv.fl_fwd || cv.kind != L_CONV) return false;
+  const Conv& dv = x.p->convs[ds];
+  return cv.R == 3 && cv.S == 3 && cv.stride == 2 && cv.pad == 1 && cv.Ci % 64 == 0 && !dv.f8 &&
+         dv.kind == L_CONV && dv.R == 1 && dv.S == 1 && dv.stride == 2 && dv.pad == 0 && dv.Co == cv.Co &&
+         dv.Ci == cv.Ci && dv.b < 0;
+}
+int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for_stats, int fold_bn = -1,
+                 bool relu = false, const Act* res = nullptr, int xbn = -1, const Act* xh = nullptr, int ds = -1,
+                 const Act* yds = nullptr, int dsbn = -1, bool* ds_done = nullptr) {
+  const Conv& cv = x.p->convs[ci];
+  if (ds_done) *ds_done = false;
+  bool dsf = yds && ds_fold_fwd_ok(x, ci, ds) && fold_bn < 0 && xbn < 0;
+  if (dsf) {  // the kernel's own geometry / tile test
+    ConvFwdArgs g = {};
+    g.N = x.p->cfg.N; g.H = in.H; g.W = in.W; g.C = cv.Ci; g.P = out.H; g.Q = out.W; g.Cout = cv.Co;
+    g.R = cv.R; g.S = cv.S; g.stride = cv.stride; g.pad = cv.pad; g.ldyds = yds->ld;
+    dsf = conv_fwd_ds_ok(g);
+  }
+  ProfScope ps(x.p, x.st, "fwd " + pname(x, cv.w) + (xbn >= 0 ? " +bn" : "") + (dsf ? " +ds" : ""),
+               conv_flops(x.p, cv, out) + (dsf ? conv_flops(x.p, x.p->convs[ds], *yds) : 0.0));
   ConvFwdArgs a = {};
   a.x = x.A(in); a.ldx = in.ld;
   a.w = x.W<bf16_t>(cv.pk_fwd);
@@ -960,6 +981,19 @@ int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for
     a.w = nullptr;
     CK(launch_conv3x3_fl(a, 0, x.st));
     return 0;
+  }
+  if (dsf) {
+    ConvFwdArgs b = a;
+    b.wds = x.W<bf16_t>(x.p->convs[ds].pk_fwd);
+    b.yds = x.A(*yds); b.ldyds = yds->ld;
+    b.stats_ds = dsbn >= 0 ? x.W<double>(x.p->bns[dsbn].stats) : nullptr;
+    if (b.stats_ds) b.bnds = bn_launch(x, dsbn, (int64_t)x.p->cfg.N * yds->H * yds->W);
+    const hipError_t e = launch_conv_fwd(b, MODE_FWD, x.st);
+    if (e != hipErrorNotSupported) {
+      CK(e);
+      if (ds_done) *ds_done = true;
+      return 0;
+    }
   }
   if (cv.kind == L_CONVT) {  // weight-stationary up-conv (convt.hip) where it covers the shape
     const hipError_t e = launch_convt2x2(a, 0, x.st);
@@ -1577,7 +1611,10 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
       RUN(conv_forward(x, b.conv2, b.h, b.out, -1, b.bn2, true, b.ds >= 0 ? &b.yds : &b.in));
       continue;
     }
-    RUN(conv_forward(x, b.conv1, b.in, b.y1, b.bn1));
+    // (a downsample block's 1x1 / stride-2 conv folded into conv1's launch)
+    bool ds_done = false;
+    RUN(conv_forward(x, b.conv1, b.in, b.y1, b.bn1, -1, false, nullptr, -1, nullptr, b.ds,
+                     b.ds >= 0 ? &b.yds : nullptr, b.dsbn, &ds_done));
     if (xform_ok(x, b.conv2, b.y1, b.h, b.y2)) {  // bn1 + ReLU inside conv2's staging
       RUN(conv_forward(x, b.conv2, b.y1, b.y2, b.bn2, -1, false, nullptr, b.bn1, &b.h));
     } else {
@@ -1585,7 +1622,7 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
       RUN(conv_forward(x, b.conv2, b.h, b.y2, b.bn2));
     }
     if (b.ds >= 0) {
-      RUN(conv_forward(x, b.ds, b.in, b.yds, b.dsbn));
+      if (!ds_done) RUN(conv_forward(x, b.ds, b.in, b.yds, b.dsbn));
       RUN(bn_apply(x, b.bn2, b.y2, b.out, 2, &b.yds, b.dsbn, true));
     } else {
       RUN(bn_apply(x, b.bn2, b.y2, b.out, 1, &b.in, -1, true));

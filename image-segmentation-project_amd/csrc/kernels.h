@@ -108,6 +108,11 @@ struct ConvFwdArgs {
   int N, H, W, C;                // input geometry (C = GEMM reduction channels)
   int P, Q, Cout;                // output geometry
   int R, S, stride, pad;
+  // forward 3x3 / stride-2 conv1 of a downsample block with its 1x1 / stride-2
+  // downsample folded in (MODE_FWD, launch_conv_fwd): wds = the downsample's
+  // packed weights [Cout][C]; its output yds (+ BN sums stats_ds / bnds as
+  // `stats` / `bn`) comes from the same staged input (the centre tap's K range)
+  const bf16_t* wds; bf16_t* yds; int ldyds; double* stats_ds; BnLaunch bnds;
   // MODE_FWD implicit GEMM only: a column stride other than `stride` (0 = the
   // same).  The ConvTranspose data gradient runs as R = 2, S = 1, stride (2, 1)
   // over a view of dY that merges each pair of adjacent pixels into one of 2C
@@ -193,6 +198,9 @@ hipError_t launch_conv3x3_fl(const ConvFwdArgs& a, int mode, hipStream_t st);
 // hipErrorNotSupported for shapes it does not cover (the caller falls back to
 // the implicit-GEMM path).
 hipError_t launch_convt2x2(const ConvFwdArgs& a, int mode, hipStream_t st);
+// does launch_conv_fwd fold the downsample (a.wds) into this 3x3 / stride-2
+// forward's launch (geometry, tile choice)?  false: launch them separately
+bool conv_fwd_ds_ok(const ConvFwdArgs& a);
 // weight-stationary full-line conv for C == 64 (conv_fl.hip), standard weight
 // pack; launch_conv3x3_ws uses it where conv3x3_ws2_ok holds (UNET_NO_WS2=1: never)
 bool conv3x3_ws2_ok(const ConvFwdArgs& a, bool flip);
