@@ -33,8 +33,6 @@
 // fragment (16 px of one output row x 32 c); each wave owns RW output rows x
 // COT channels (acc[RW][FN]).
 #include <cstdio>
-#include <cstdlib>
-
 #include "common.h"
 #include "kernels.h"
 
@@ -99,24 +97,32 @@ __device__ __forceinline__ void issue_weight_dma(const ConvFwdArgs& a, __amdgpu_
 // One 32-channel panel of a tile: 9 taps x RW rows x FN channel fragments.
 // W: the panel's weight image (tap stride WTS bytes, 16-co fragment stride
 // 1 KiB); H: the panel's halo image.
+// Per column shift s the RW + 2 halo rows the wave's RW output rows reach are
+// read once and serve all three tap rows r (output row j reads halo row j +
+// dr): 3 (RW + 2) B-fragment reads per panel instead of 9 RW (RW = 2: 12
+// instead of 18 -- the LDS port, not the MFMA, bounds these narrow convs).
 template <int FN, int RW, int WTS, bool FLIP>
 __device__ __forceinline__ void mfma_panel(f32x4 (&acc)[RW][FN], const char* W, const char* H, int aoff,
                                            const int (&boff)[RW + 2][3]) {
 #pragma unroll
-  for (int r = 0; r < 3; ++r)
+  for (int s = 0; s < 3; ++s) {
+    const int ds = FLIP ? 2 - s : s;
+    bf16x8 B[RW + 2];
 #pragma unroll
-    for (int s = 0; s < 3; ++s) {
+    for (int h = 0; h < RW + 2; ++h) B[h] = *reinterpret_cast<const bf16x8*>(H + boff[h][ds]);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
       bf16x8 A[FN];
 #pragma unroll
       for (int i = 0; i < FN; ++i) A[i] = *reinterpret_cast<const bf16x8*>(W + (r * 3 + s) * WTS + i * 1024 + aoff);
-      const int dr = FLIP ? 2 - r : r, ds = FLIP ? 2 - s : s;
+      const int dr = FLIP ? 2 - r : r;
 #pragma unroll
-      for (int j = 0; j < RW; ++j) {
-        const bf16x8 B = *reinterpret_cast<const bf16x8*>(H + boff[j + dr][ds]);
+      for (int j = 0; j < RW; ++j)
 #pragma unroll
-        for (int i = 0; i < FN; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B, acc[j][i], 0, 0, 0);
-      }
+        for (int i = 0; i < FN; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B[j + dr], acc[j][i], 0, 0, 0);
     }
+  }
 }
 
 // ---- full-line staging (64 reduction channels = one 128-B line per pixel /
@@ -1121,7 +1127,13 @@ static hipError_t launch_halo_shape(const ConvFwdArgs& a, hipStream_t st) {
     if (FLIP) return launch_ws<1, 2, 8, 8, FLIP>(a, st);
     return launch_ws<1, 2, 16, 4, FLIP>(a, st);
   }
-  if (C == 32 && Co == 96 && a.P % 16 == 0) return launch_ws<1, 2, 8, 8, FLIP>(a, st);
+  // decoder1.0's data gradient (32 -> 96): 16-row tiles on 4 waves, 4 rows
+  // each, with the per-shift halo-row reuse of mfma_panel (round 6 sweep:
+  // 118 -> 104 us; the same tiles for the forwards and decoder1.3 were slower)
+  if (C == 32 && Co == 96 && a.P % 16 == 0) {
+    if (FLIP) return launch_ws<1, 2, 16, 4, FLIP>(a, st);
+    return launch_ws<1, 2, 8, 8, FLIP>(a, st);
+  }
   if (C == 32 && Co % 64 == 0 && a.P % 16 == 0) return launch_ws<1, 4, 16, 8, FLIP>(a, st);
   if (C == 96 && Co == 32 && a.P % 8 == 0) return launch_ws<3, 2, 8, 8, FLIP>(a, st);
   // halo-streamed: 256-pixel tiles while they still give >= ~1 block per CU
