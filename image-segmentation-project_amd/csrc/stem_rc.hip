@@ -222,17 +222,16 @@ __global__ void __launch_bounds__(kRcNT) stem_rc_fwd_kernel(StemRcArgs a, int pe
   // 32-bit buffer offsets, kOOB zero-fill at the borders (no 64-bit address
   // arithmetic or branch per element)
   const __amdgpu_buffer_rsrc_t rimg = make_rsrc(a.img, (unsigned)((size_t)a.N * a.H * a.W * 4));
-  auto fetch = [&](int j) {
+  auto fetch = [&](FwdPatch& p, int j) {
     const int n = j / a.Pp, jp = j - n * a.Pp, ex = extra_of(j);
-    pf.fetch_counted(rimg, a.H, a.W, n, 4 * jp - 3 - 2 * ex, 9 + 2 * ex, -3);
+    p.fetch_counted(rimg, a.H, a.W, n, 4 * jp - 3 - 2 * ex, 9 + 2 * ex, -3);
   };
-  if (j0 < j1) fetch(j0);
-  TSTAMP(a.tim, 1);
-  for (int j = j0; j < j1; ++j) {
+  // pooled row j from patch p, which is then refilled with row j + AHEAD
+  auto row = [&](int j, FwdPatch& p, int ahead) {
     const int n = j / a.Pp, jp = j - n * a.Pp, ex = extra_of(j);
     lds_sync();  // previous pooled row: patch, Xs and ring slots consumed
-    pf.store(patch, 9 + 2 * ex);
-    if (j + 1 < j1) fetch(j + 1);
+    p.store(patch, 9 + 2 * ex);
+    if (j + ahead < j1) fetch(p, j + ahead);
     for (int t = -ex; t < 2; ++t) {
       const int h = 2 * jp + t;  // stem row
       lds_sync();           // patch stored / previous round's Xs consumed
@@ -338,6 +337,23 @@ __global__ void __launch_bounds__(kRcNT) stem_rc_fwd_kernel(StemRcArgs a, int pe
       }
     }
     if (j - j0 < 8) TSTAMP(a.tim, 3 + 2 * (j - j0));
+  };
+  if constexpr (MODE == 0) {
+    // statistics pass: no stores in the loop, so two rows' patches in flight
+    // (the fetch of row j lands under rows j - 2 and j - 1; with one row ahead
+    // every row waited ~8 k cycles for its patch, conv_timing.py)
+    FwdPatch pf2;
+    if (j0 < j1) fetch(pf, j0);
+    if (j0 + 1 < j1) fetch(pf2, j0 + 1);
+    TSTAMP(a.tim, 1);
+    for (int j = j0; j < j1; j += 2) {
+      row(j, pf, 2);
+      if (j + 1 < j1) row(j + 1, pf2, 2);
+    }
+  } else {
+    if (j0 < j1) fetch(pf, j0);
+    TSTAMP(a.tim, 1);
+    for (int j = j0; j < j1; ++j) row(j, pf, 1);
   }
   TSTAMP(a.tim, 20);
   if constexpr (MODE == 0) {
@@ -950,7 +966,10 @@ hipError_t launch_stem_rc_fwd(const StemRcArgs& a, int mode, hipStream_t st) {
   const int total = a.N * a.Pp;
   if (mode == 0) {
     if (!a.stats) return hipErrorInvalidValue;
-    const int want = 2 * rc_cus() / groups;
+    // one block per CU (183 VGPRs: one 512-thread block is resident per CU;
+    // twice as many blocks ran as two rounds, each paying the prologue and the
+    // statistics epilogue)
+    const int want = std::max(1, rc_cus() / groups);
     const int per = std::max(1, (total + want - 1) / want);
     const size_t lds = kRcXs + kRcPatchB + 2 * 64 * sizeof(float);
     conv_kernel_tag("stem_rc_fwd_kernel<0>");
