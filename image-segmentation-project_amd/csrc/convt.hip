@@ -37,8 +37,12 @@ void conv_kernel_tag(const char* tag);  // conv_kernels.hip: per-launch profiler
 
 constexpr int kCtWaves = 4;
 
-// byte offset of 16-B chunk c of LDS weight row r (rows of KB bytes)
-__device__ __forceinline__ int ct_off(int r, int c, int KB) { return r * KB + ((c ^ (r & 7)) << 4); }
+// byte offset of 16-B chunk c of LDS weight row r (rows of KB bytes): chunk
+// XOR (r mod the row's chunk count, at most 8), so it stays inside the row
+__device__ __forceinline__ int ct_off(int r, int c, int KB) {
+  const int m = (KB >> 4) >= 8 ? 7 : (KB >> 4) - 1;
+  return r * KB + ((c ^ (r & m)) << 4);
+}
 
 __device__ __forceinline__ void unpack4(uint2 u, float* f) {
   f[0] = __uint_as_float(u.x << 16); f[1] = __uint_as_float(u.x & 0xffff0000u);
@@ -350,6 +354,166 @@ hipError_t launch_convt2x2(const ConvFwdArgs& a, int mode, hipStream_t st) {
     if (Ci == 64 && Co == 64) return convt_fb<1, 4, 8>(a, st);
     if (Ci == 128 && Co == 64) return convt_fb<1, 8, 8>(a, st);
   }
+  return hipErrorNotSupported;
+}
+
+// ---------------------------------------------------------------------------
+// 1 x 1 / stride-1 convs of the narrow full-resolution attention gates
+// (AttentionGate W_g / W_x, advanced_models.py:10-18, applied at :30-31 on the
+// 128^2 / 256^2 decoder levels) with the same structure: weights [NN][K]
+// staged once per block, the pixel operand straight into the B fragments,
+// independent waves.  These launches move 0.1-0.3 GB at K, NN <= 64: the
+// implicit-GEMM tiles ran them at 1.5-2.5 TB/s.
+//   MODE 0 forward:        Y[m][co] = bias[co] + sum_ci W[co][ci] X[m][ci];
+//                          stats != null: BN sums of the fp32 values
+//                          (conv_epilogue's), last block finalises with a ticket
+//   MODE 1 data gradient:  dX[m][ci] = sum_co W[co][ci] dY[m][co] (+ add[m][ci])
+// Both read their pack ([Cout][Ci] forward, [Ci][Cout] dgrad) as [NN][K] rows.
+// ---------------------------------------------------------------------------
+template <int NT, int KS>
+__global__ void __launch_bounds__(kCtWaves * 64) conv1x1_kernel(ConvFwdArgs a, int ngroups) {
+  constexpr int NN = NT * 16, K = KS * 32, KB = K * 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* wl = smem;                                         // [NN][K] bf16
+  float* cst = reinterpret_cast<float*>(smem + NN * KB);  // bias [NN]
+  float* red = cst + NN;                                   // [kCtWaves][NN][2]
+  int* flag = reinterpret_cast<int*>(red + kCtWaves * NN * 2);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int pl = lane & 15, kq = lane >> 4;
+  const bool stats = a.stats != nullptr, add = a.add != nullptr;
+
+  // the group's pixel operand and (data gradient) its addend: one round trip
+  auto load_b = [&](int g, bf16x8 (&B)[KS], uint2 (&ad)[NT]) {
+    const size_t m = (size_t)g * 16 + pl;
+    const bf16_t* src = a.x + m * a.ldx + kq * 8;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) B[ks] = *reinterpret_cast<const bf16x8*>(src + ks * 32);
+    if (add) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) ad[nt] = *reinterpret_cast<const uint2*>(a.add + m * a.ldadd + nt * 16 + kq * 4);
+    }
+  };
+  const int nw = gridDim.x * kCtWaves;
+  int g = blockIdx.x * kCtWaves + wave;
+  bf16x8 B[KS];
+  uint2 ad[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) ad[nt] = make_uint2(0u, 0u);
+  if (g < ngroups) load_b(g, B, ad);  // before the weight staging (independent)
+  for (int idx = tid; idx < NN * KS * 4; idx += kCtWaves * 64) {
+    const int r = idx / (KS * 4), c = idx - r * (KS * 4);
+    *reinterpret_cast<uint4*>(wl + ct_off(r, c, KB)) = *reinterpret_cast<const uint4*>(a.w + (size_t)r * K + c * 8);
+  }
+  for (int c = tid; c < NN; c += kCtWaves * 64) cst[c] = a.bias ? a.bias[c] : 0.f;
+  __syncthreads();
+
+  float q0[NT][4], q1[NT][4];
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) q0[i][e] = q1[i][e] = 0.f;
+  for (; g < ngroups; g += nw) {
+    const size_t m = (size_t)g * 16 + pl;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 A = *reinterpret_cast<const bf16x8*>(wl + ct_off(nt * 16 + pl, ks * 4 + kq, KB));
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B[ks], acc, 0, 0, 0);
+      }
+      const int c = nt * 16 + kq * 4;
+      const f32x4 b = *reinterpret_cast<const f32x4*>(cst + c);
+      float v[4] = {acc[0] + b[0], acc[1] + b[1], acc[2] + b[2], acc[3] + b[3]};
+      if (add) {
+        float r[4];
+        unpack4(ad[nt], r);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += r[e];
+      }
+      uint2 o;
+      o.x = pack_bf2(v[0], v[1]);
+      o.y = pack_bf2(v[2], v[3]);
+      *reinterpret_cast<uint2*>(a.y + m * a.ldy + c) = o;
+      if (stats) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          q0[nt][e] += v[e];
+          q1[nt][e] += v[e] * v[e];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (g + nw < ngroups) load_b(g + nw, B, ad);
+  }
+  if (!stats) return;
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        q0[i][e] += __shfl_xor(q0[i][e], o, 64);
+        q1[i][e] += __shfl_xor(q1[i][e], o, 64);
+      }
+  if (pl == 0) {
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = i * 16 + kq * 4 + e;
+        red[(wave * NN + c) * 2] = q0[i][e];
+        red[(wave * NN + c) * 2 + 1] = q1[i][e];
+      }
+  }
+  __syncthreads();
+  const size_t rep = (size_t)(blockIdx.x % kStatRep) * 2 * NN;
+  for (int c = tid; c < NN; c += kCtWaves * 64) {
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int w = 0; w < kCtWaves; ++w) {
+      s0 += red[(w * NN + c) * 2];
+      s1 += red[(w * NN + c) * 2 + 1];
+    }
+    atomicAdd(a.stats + rep + c, (double)s0);
+    atomicAdd(a.stats + rep + NN + c, (double)s1);
+  }
+  if (a.bn.ticket && last_block_arrive(a.bn.ticket, gridDim.x, flag, true)) bn_finalize(a.bn);
+}
+
+template <int NT, int KS>
+static hipError_t conv1x1_cfg(const ConvFwdArgs& a, hipStream_t st) {
+  constexpr int NN = NT * 16, K = KS * 32;
+  const long long M = (long long)a.N * a.H * a.W;
+  if (M % 16) return hipErrorNotSupported;
+  const int ngroups = (int)(M / 16);
+  const size_t lds = (size_t)NN * K * 2 + NN * 4 + kCtWaves * NN * 2 * 4 + 16;
+  // with statistics two blocks per CU instead of four: the per-block
+  // reduction and its atomics amortise over more groups
+  const int per_cu = a.stats ? 2 : 4;
+  int grid = std::min((ngroups + kCtWaves - 1) / kCtWaves, per_cu * device_cu_count());
+  if (a.grid_cap > 0) grid = std::min(grid, a.grid_cap);
+  char tag[48];
+  std::snprintf(tag, sizeof(tag), "conv1x1_kernel<%d, %d>", NT, KS);
+  conv_kernel_tag(tag);
+  hipLaunchKernelGGL((conv1x1_kernel<NT, KS>), dim3(grid), dim3(kCtWaves * 64), lds, st, a, ngroups);
+  return hipGetLastError();
+}
+
+hipError_t launch_conv1x1(const ConvFwdArgs& a, int mode, hipStream_t st) {
+  if (mode != 0 && mode != 1) return hipErrorInvalidValue;
+  if (a.R != 1 || a.S != 1 || a.stride != 1 || a.pad != 0 || a.H != a.P || a.W != a.Q) return hipErrorNotSupported;
+  if (a.bb.sums || a.x2 || a.ysplit || a.fold_on || a.xform || a.wch || a.wds || a.stride_w) return hipErrorNotSupported;
+  if (mode == 1 && (a.stats || a.bias)) return hipErrorNotSupported;
+  if (mode == 0 && a.add) return hipErrorNotSupported;
+  if (!al16(a.x) || !al16(a.w) || a.ldx % 8 || !al8(a.y) || a.ldy % 4 || (a.add && (!al8(a.add) || a.ldadd % 4)))
+    return hipErrorNotSupported;
+  // NN = Cout (forward) / the dgrad's output channels; K = the reduction
+  const int NN = a.Cout, K = a.C;
+  if (NN == 32 && K == 32) return conv1x1_cfg<2, 1>(a, st);
+  if (NN == 32 && K == 64) return conv1x1_cfg<2, 2>(a, st);
+  if (NN == 64 && K == 32) return conv1x1_cfg<4, 1>(a, st);
+  if (NN == 64 && K == 64) return conv1x1_cfg<4, 2>(a, st);
   return hipErrorNotSupported;
 }
 

@@ -995,6 +995,13 @@ int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for
       return 0;
     }
   }
+  if (cv.kind == L_CONV && cv.R == 1 && cv.S == 1 && cv.stride == 1) {  // weight-stationary 1x1 where covered
+    const hipError_t e = launch_conv1x1(a, 0, x.st);
+    if (e != hipErrorNotSupported) {
+      CK(e);
+      return 0;
+    }
+  }
   if (cv.kind == L_CONVT) {  // weight-stationary up-conv (convt.hip) where it covers the shape
     const hipError_t e = launch_convt2x2(a, 0, x.st);
     if (e != hipErrorNotSupported) {
@@ -1062,6 +1069,13 @@ int conv_dgrad(const Ctx& x, int ci, const Act& dy, const Act& dx, const Act* ad
     return 0;
   }
   if (bias_done) *bias_done = false;
+  if (cv.kind == L_CONV && cv.R == 1 && cv.S == 1 && cv.stride == 1 && !fuse) {  // weight-stationary 1x1
+    const hipError_t e = launch_conv1x1(a, 1, x.st);
+    if (e != hipErrorNotSupported) {
+      CK(e);
+      return 0;
+    }
+  }
   if (cv.kind == L_CONVT) {  // weight-stationary up-conv (convt.hip): its own geometry, the input grid
     ConvFwdArgs b = a;
     b.H = dx.H; b.W = dx.W; b.C = cv.Ci; b.Cout = cv.Co;

@@ -198,6 +198,12 @@ hipError_t launch_conv3x3_fl(const ConvFwdArgs& a, int mode, hipStream_t st);
 // hipErrorNotSupported for shapes it does not cover (the caller falls back to
 // the implicit-GEMM path).
 hipError_t launch_convt2x2(const ConvFwdArgs& a, int mode, hipStream_t st);
+// 1 x 1 / stride-1 conv as a weight-stationary per-pixel GEMM (convt.hip): mode
+// 0 forward (w = forward pack [Cout][C], bias, BN sums `stats` / `bn`), mode 1
+// data gradient (w = dgrad pack [C_out_of_op][C], a.C = dY channels, a.Cout =
+// dX channels, optional `add`).  hipErrorNotSupported outside its (Cout, C)
+// table {32, 64}^2 or for other epilogues (the caller falls back).
+hipError_t launch_conv1x1(const ConvFwdArgs& a, int mode, hipStream_t st);
 // does launch_conv_fwd fold the downsample (a.wds) into this 3x3 / stride-2
 // forward's launch (geometry, tile choice)?  false: launch them separately
 bool conv_fwd_ds_ok(const ConvFwdArgs& a);
