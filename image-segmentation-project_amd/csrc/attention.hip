@@ -71,6 +71,10 @@ __device__ void bn1_coef(const AttGateArgs& a, float& scale, float& shift, float
 
 }  // namespace
 
+// pixels per lane group and loop pass in the gate kernels: their loads are all
+// issued before the pass's math (one pixel per pass kept one load in flight)
+constexpr int kAttU = 4;
+
 // sum over the CC lanes of one pixel group (CC | 64, groups lane-aligned)
 __device__ __forceinline__ float group_sum(float v, int CC) {
   for (int o = CC >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -89,17 +93,28 @@ __global__ void __launch_bounds__(256) att_psi_fwd_kernel(AttGateArgs a) {
 #pragma unroll
   for (int k = 0; k < 8; ++k) w[k] = a.psi_w[chunk * 8 + k];
   const float bias = a.psi_b[0];
-  for (int64_t px = (int64_t)blockIdx.x * ppb + prow; px < a.npix; px += (int64_t)gridDim.x * ppb) {
-    float v[8];
-    unpack8(*reinterpret_cast<const uint4*>(a.s + px * a.lds + chunk * 8), v);
-    float t = 0.f;
+  const int64_t stride = (int64_t)gridDim.x * ppb;
+  for (int64_t base = (int64_t)blockIdx.x * ppb + prow; base < a.npix; base += kAttU * stride) {
+    uint4 sv[kAttU];  // kAttU pixels' loads in flight before any math
 #pragma unroll
-    for (int k = 0; k < 8; ++k) t += v[k] * w[k];
-    const float acc = group_sum(t, CC) + bias;
-    if (chunk == 0) {
-      a.p[px] = acc;
-      ls += acc;
-      lq += (double)acc * acc;
+    for (int u = 0; u < kAttU; ++u) {
+      const int64_t px = base + u * stride;
+      sv[u] = px < a.npix ? *reinterpret_cast<const uint4*>(a.s + px * a.lds + chunk * 8) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kAttU; ++u) {
+      const int64_t px = base + u * stride;
+      float v[8];
+      unpack8(sv[u], v);
+      float t = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t += v[k] * w[k];
+      const float acc = group_sum(t, CC) + bias;  // the whole lane group shares px
+      if (chunk == 0 && px < a.npix) {
+        a.p[px] = acc;
+        ls += acc;
+        lq += (double)acc * acc;
+      }
     }
   }
   if (!a.training) return;
@@ -117,14 +132,29 @@ __global__ void __launch_bounds__(256) att_gate_fwd_kernel(AttGateArgs a) {
   bn1_coef(a, sc, sh, mean, inv, var);
   const int CC = a.Fl >> 3, ppb = 256 / CC;
   const int chunk = threadIdx.x % CC, prow = threadIdx.x / CC;
-  for (int64_t px = (int64_t)blockIdx.x * ppb + prow; px < a.npix; px += (int64_t)gridDim.x * ppb) {
-    const float ps = sigmoidf(a.p[px] * sc + sh);
-    if (chunk == 0) a.psi[px] = ps;
-    float v[8];
-    unpack8(*reinterpret_cast<const uint4*>(a.x + px * a.ldx + chunk * 8), v);
+  const int64_t stride = (int64_t)gridDim.x * ppb;
+  for (int64_t base = (int64_t)blockIdx.x * ppb + prow; base < a.npix; base += kAttU * stride) {
+    float pv[kAttU];
+    uint4 xv[kAttU];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] *= ps;
-    *reinterpret_cast<uint4*>(a.xatt + px * a.ldxatt + chunk * 8) = pack8(v);
+    for (int u = 0; u < kAttU; ++u) {
+      const int64_t px = base + u * stride;
+      const bool in = px < a.npix;
+      pv[u] = in ? a.p[px] : 0.f;
+      xv[u] = in ? *reinterpret_cast<const uint4*>(a.x + px * a.ldx + chunk * 8) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kAttU; ++u) {
+      const int64_t px = base + u * stride;
+      if (px >= a.npix) break;
+      const float ps = sigmoidf(pv[u] * sc + sh);
+      if (chunk == 0) a.psi[px] = ps;
+      float v[8];
+      unpack8(xv[u], v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] *= ps;
+      *reinterpret_cast<uint4*>(a.xatt + px * a.ldxatt + chunk * 8) = pack8(v);
+    }
   }
   if (a.training && blockIdx.x == 0 && threadIdx.x == 0) {
     a.save[0] = mean;
@@ -146,24 +176,41 @@ __global__ void __launch_bounds__(256) att_gate_bwd_reduce_kernel(AttGateArgs a)
   const int CC = a.Fl >> 3, ppb = 256 / CC;
   const int chunk = threadIdx.x % CC, prow = threadIdx.x / CC;
   double s1 = 0.0, s2 = 0.0;
-  for (int64_t px = (int64_t)blockIdx.x * ppb + prow; px < a.npix; px += (int64_t)gridDim.x * ppb) {
-    const float ps = a.psi[px];
-    float d[8], v[8];
-    unpack8(*reinterpret_cast<const uint4*>(a.dxatt + px * a.lddxatt + chunk * 8), d);
-    unpack8(*reinterpret_cast<const uint4*>(a.x + px * a.ldx + chunk * 8), v);
-    float t = 0.f;
+  const int64_t stride = (int64_t)gridDim.x * ppb;
+  for (int64_t base = (int64_t)blockIdx.x * ppb + prow; base < a.npix; base += kAttU * stride) {
+    float psv[kAttU], pv[kAttU];
+    uint4 dv[kAttU], xv[kAttU];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      t += d[k] * v[k];
-      d[k] *= ps;
+    for (int u = 0; u < kAttU; ++u) {
+      const int64_t px = base + u * stride;
+      const bool in = px < a.npix;
+      psv[u] = in ? a.psi[px] : 0.f;
+      pv[u] = in ? a.p[px] : 0.f;
+      dv[u] = in ? *reinterpret_cast<const uint4*>(a.dxatt + px * a.lddxatt + chunk * 8) : make_uint4(0, 0, 0, 0);
+      xv[u] = in ? *reinterpret_cast<const uint4*>(a.x + px * a.ldx + chunk * 8) : make_uint4(0, 0, 0, 0);
     }
-    *reinterpret_cast<uint4*>(a.dxpsi + px * a.lddxpsi + chunk * 8) = pack8(d);
-    const float dpsi = group_sum(t, CC);
-    if (chunk == 0) {
-      const float dz = dpsi * ps * (1.f - ps);
-      a.dbnp[px] = dz;
-      s1 += dz;
-      s2 += (double)dz * ((a.p[px] - mean) * inv);
+#pragma unroll
+    for (int u = 0; u < kAttU; ++u) {
+      const int64_t px = base + u * stride;
+      const bool in = px < a.npix;
+      const float ps = psv[u];
+      float d[8], v[8];
+      unpack8(dv[u], d);
+      unpack8(xv[u], v);
+      float t = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        t += d[k] * v[k];
+        d[k] *= ps;
+      }
+      if (in) *reinterpret_cast<uint4*>(a.dxpsi + px * a.lddxpsi + chunk * 8) = pack8(d);
+      const float dpsi = group_sum(t, CC);  // the whole lane group shares px
+      if (chunk == 0 && in) {
+        const float dz = dpsi * ps * (1.f - ps);
+        a.dbnp[px] = dz;
+        s1 += dz;
+        s2 += (double)dz * ((pv[u] - mean) * inv);
+      }
     }
   }
   block_sum2(s1, s2, red);
@@ -200,11 +247,29 @@ __global__ void __launch_bounds__(256) att_gate_bwd_apply_kernel(AttGateArgs a) 
     is2[k] = fuse ? bb.invstd2[c8 + k] : 0.f;
   }
   if (row < rows) {
-    for (int64_t px = (int64_t)blockIdx.x * rows + row; px < a.npix; px += (int64_t)gridDim.x * rows) {
-      const float phat = (a.p[px] - mean) * inv;
-      const float dp = k1 * (a.dbnp[px] - m1 - phat * m2);
+    const int64_t stride = (int64_t)gridDim.x * rows;
+    for (int64_t base = (int64_t)blockIdx.x * rows + row; base < a.npix; base += kAttU * stride) {
+    float pv[kAttU], dbv[kAttU];
+    uint4 sv[kAttU], gv[kAttU], xav[kAttU];
+#pragma unroll
+    for (int u = 0; u < kAttU; ++u) {  // kAttU pixels' operands in flight before any math
+      const int64_t px = base + u * stride;
+      const bool in = px < a.npix;
+      const uint4 z = make_uint4(0, 0, 0, 0);
+      pv[u] = in ? a.p[px] : 0.f;
+      dbv[u] = in ? a.dbnp[px] : 0.f;
+      sv[u] = in ? *reinterpret_cast<const uint4*>(a.s + px * a.lds + c8) : z;
+      gv[u] = (in && fuse) ? *reinterpret_cast<const uint4*>(bb.y + px * bb.ldy + c8) : z;
+      xav[u] = (in && fuse) ? *reinterpret_cast<const uint4*>(bb.y2 + px * bb.ldy2 + c8) : z;
+    }
+#pragma unroll
+    for (int u = 0; u < kAttU; ++u) {
+      const int64_t px = base + u * stride;
+      if (px >= a.npix) break;
+      const float phat = (pv[u] - mean) * inv;
+      const float dp = k1 * (dbv[u] - m1 - phat * m2);
       float v[8], o[8];
-      unpack8(*reinterpret_cast<const uint4*>(a.s + px * a.lds + c8), v);
+      unpack8(sv[u], v);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         gw[k] += dp * v[k];
@@ -212,8 +277,8 @@ __global__ void __launch_bounds__(256) att_gate_bwd_apply_kernel(AttGateArgs a) 
       }
       if (fuse) {
         float g[8], xa[8];
-        unpack8(*reinterpret_cast<const uint4*>(bb.y + px * bb.ldy + c8), g);
-        unpack8(*reinterpret_cast<const uint4*>(bb.y2 + px * bb.ldy2 + c8), xa);
+        unpack8(gv[u], g);
+        unpack8(xav[u], xa);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           o[k] = v[k] > 0.f ? o[k] : 0.f;
@@ -223,6 +288,7 @@ __global__ void __launch_bounds__(256) att_gate_bwd_apply_kernel(AttGateArgs a) 
         }
       }
       *reinterpret_cast<uint4*>(a.dS + px * a.lddS + c8) = pack8(o);
+    }
     }
   }
   const int nq = fuse ? 4 : 1;
