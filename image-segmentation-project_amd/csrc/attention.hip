@@ -332,15 +332,28 @@ __global__ void __launch_bounds__(256) ch_pool_kernel(ChAttArgs a) {
     bool any = false;
 #pragma unroll
     for (int k = 0; k < 8; ++k) { sum[k] = 0.f; mx[k] = 0.f; arg[k] = 0; }
-    for (int64_t hw = (int64_t)blockIdx.x * rows + row; hw < a.HW; hw += (int64_t)gridDim.x * rows) {
-      float v[8];
-      unpack8(*reinterpret_cast<const uint4*>(a.y + (n * a.HW + hw) * a.ldy + chunk * 8), v);
+    const int64_t stride = (int64_t)gridDim.x * rows;
+    for (int64_t base = (int64_t)blockIdx.x * rows + row; base < a.HW; base += kAttU * stride) {
+      uint4 yv[kAttU];  // the pass's loads first; the scan order (hw ascending) is unchanged
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        sum[k] += v[k];
-        if (!any || v[k] > mx[k]) { mx[k] = v[k]; arg[k] = (unsigned)hw; }
+      for (int u = 0; u < kAttU; ++u) {
+        const int64_t hw = base + u * stride;
+        yv[u] = hw < a.HW ? *reinterpret_cast<const uint4*>(a.y + (n * a.HW + hw) * a.ldy + chunk * 8)
+                          : make_uint4(0, 0, 0, 0);
       }
-      any = true;
+#pragma unroll
+      for (int u = 0; u < kAttU; ++u) {
+        const int64_t hw = base + u * stride;
+        if (hw >= a.HW) break;
+        float v[8];
+        unpack8(yv[u], v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          sum[k] += v[k];
+          if (!any || v[k] > mx[k]) { mx[k] = v[k]; arg[k] = (unsigned)hw; }
+        }
+        any = true;
+      }
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -406,13 +419,25 @@ __global__ void __launch_bounds__(256) ch_scale_kernel(ChAttArgs a) {
   float g[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) g[k] = a.gate[n * a.C + chunk * 8 + k];
-  for (int64_t hw = (int64_t)blockIdx.x * rows + row; hw < a.HW; hw += (int64_t)gridDim.x * rows) {
-    const int64_t px = n * a.HW + hw;
-    float v[8];
-    unpack8(*reinterpret_cast<const uint4*>(a.y + px * a.ldy + chunk * 8), v);
+  const int64_t stride = (int64_t)gridDim.x * rows;
+  for (int64_t base = (int64_t)blockIdx.x * rows + row; base < a.HW; base += kAttU * stride) {
+    uint4 yv[kAttU];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] *= g[k];
-    *reinterpret_cast<uint4*>(a.out + px * a.ldo + chunk * 8) = pack8(v);
+    for (int u = 0; u < kAttU; ++u) {
+      const int64_t hw = base + u * stride;
+      yv[u] = hw < a.HW ? *reinterpret_cast<const uint4*>(a.y + (n * a.HW + hw) * a.ldy + chunk * 8)
+                        : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kAttU; ++u) {
+      const int64_t hw = base + u * stride;
+      if (hw >= a.HW) break;
+      float v[8];
+      unpack8(yv[u], v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] *= g[k];
+      *reinterpret_cast<uint4*>(a.out + (n * a.HW + hw) * a.ldo + chunk * 8) = pack8(v);
+    }
   }
 }
 
@@ -426,12 +451,24 @@ __global__ void __launch_bounds__(256) ch_bwd_reduce_kernel(ChAttArgs a) {
     float t[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) t[k] = 0.f;
-    for (int64_t hw = (int64_t)blockIdx.x * rows + row; hw < a.HW; hw += (int64_t)gridDim.x * rows) {
-      float d[8], v[8];
-      unpack8(*reinterpret_cast<const uint4*>(a.dout2 + (n * a.HW + hw) * a.lddo2 + chunk * 8), d);
-      unpack8(*reinterpret_cast<const uint4*>(a.y + (n * a.HW + hw) * a.ldy + chunk * 8), v);
+    const int64_t stride = (int64_t)gridDim.x * rows;
+    for (int64_t base = (int64_t)blockIdx.x * rows + row; base < a.HW; base += kAttU * stride) {
+      uint4 dv[kAttU], yv[kAttU];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) t[k] += d[k] * v[k];
+      for (int u = 0; u < kAttU; ++u) {
+        const int64_t hw = base + u * stride;
+        const bool in = hw < a.HW;
+        dv[u] = in ? *reinterpret_cast<const uint4*>(a.dout2 + (n * a.HW + hw) * a.lddo2 + chunk * 8) : make_uint4(0, 0, 0, 0);
+        yv[u] = in ? *reinterpret_cast<const uint4*>(a.y + (n * a.HW + hw) * a.ldy + chunk * 8) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < kAttU; ++u) {  // out-of-range pixels loaded zeros: adding 0 * 0
+        float d[8], v[8];
+        unpack8(dv[u], d);
+        unpack8(yv[u], v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t[k] += d[k] * v[k];
+      }
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) sred[row * a.C + chunk * 8 + k] = t[k];
@@ -509,16 +546,30 @@ __global__ void __launch_bounds__(256) ch_bwd_apply_kernel(ChAttArgs a) {
     is[k] = fuse ? bb.invstd[c] : 0.f;
     s1[k] = s2[k] = 0.f;
   }
-  for (int64_t hw = (int64_t)blockIdx.x * rows + row; hw < a.HW; hw += (int64_t)gridDim.x * rows) {
-    const int64_t px = n * a.HW + hw;
+  const int64_t stride = (int64_t)gridDim.x * rows;
+  for (int64_t base = (int64_t)blockIdx.x * rows + row; base < a.HW; base += kAttU * stride) {
+  uint4 dv[kAttU], av[kAttU], yv[kAttU];
+#pragma unroll
+  for (int u = 0; u < kAttU; ++u) {  // the pass's operands first
+    const int64_t hw = base + u * stride, px = n * a.HW + hw;
+    const bool in = hw < a.HW;
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    dv[u] = in ? *reinterpret_cast<const uint4*>(a.dout2 + px * a.lddo2 + c8) : z;
+    av[u] = (in && fuse) ? *reinterpret_cast<const uint4*>(bb.act + px * bb.ldact + c8) : z;
+    yv[u] = (in && fuse) ? *reinterpret_cast<const uint4*>(bb.y + px * bb.ldy + c8) : z;
+  }
+#pragma unroll
+  for (int u = 0; u < kAttU; ++u) {
+    const int64_t hw = base + u * stride, px = n * a.HW + hw;
+    if (hw >= a.HW) break;
     float d[8];
-    unpack8(*reinterpret_cast<const uint4*>(a.dout2 + px * a.lddo2 + c8), d);
+    unpack8(dv[u], d);
 #pragma unroll
     for (int k = 0; k < 8; ++k) d[k] = d[k] * g[k] + da[k] + (arg[k] == (unsigned)hw ? dm[k] : 0.f);
     if (fuse) {
       float act[8], y[8];
-      unpack8(*reinterpret_cast<const uint4*>(bb.act + px * bb.ldact + c8), act);
-      unpack8(*reinterpret_cast<const uint4*>(bb.y + px * bb.ldy + c8), y);
+      unpack8(av[u], act);
+      unpack8(yv[u], y);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         d[k] = act[k] > 0.f ? d[k] : 0.f;
@@ -527,6 +578,7 @@ __global__ void __launch_bounds__(256) ch_bwd_apply_kernel(ChAttArgs a) {
       }
     }
     *reinterpret_cast<uint4*>(a.dout + px * a.lddo + c8) = pack8(d);
+  }
   }
   if (!fuse) return;
   const size_t rep = (size_t)((blockIdx.y * gridDim.x + blockIdx.x) % kStatRep) * 2 * a.C;
