@@ -785,10 +785,36 @@ __device__ void head_contract(const HeadArgs& a, float* V, float* cst) {
 // 2.2-2.7 TB/s).
 constexpr int kHeadHP = 4;  // pixels in flight per thread (Cin = 32: 16 x 16 B of loads)
 
+// Round 6: decoder1's last BN + ReLU folded into the head (a.bn_fold): the
+// head reads the raw conv output y and forms act = bf16(relu(y * sc + sh)),
+// the value bn_apply_kernel would have stored, in both passes (fmaf: the same
+// bits in the forward and the backward).  sc / sh per channel into LDS as
+// bn_apply_kernel computes them (the producer's finalised ss, or the replica
+// sums).
+__device__ __forceinline__ float head_act(float y, float sc, float sh) {
+  const float v = fmaf(y, sc, sh);
+  return bf2f(f2bf(v > 0.f ? v : 0.f));
+}
+__device__ void head_bn_coef(const HeadArgs& a, float2* ss) {
+  for (int c = threadIdx.x; c < a.Cin; c += blockDim.x) {
+    float sc, sh, m, inv, var;
+    if (a.bn.training && a.bn.ss) {
+      sc = a.bn.ss[c];
+      sh = a.bn.ss[a.Cin + c];
+    } else {
+      bn_scale_shift(a.bn, c, sc, sh, m, inv, var);
+    }
+    ss[c] = make_float2(sc, sh);
+  }
+}
+
 template <int CIN>
 __global__ void __launch_bounds__(256) head_fwd_kernel(HeadArgs a) {
   __shared__ __attribute__((aligned(16))) float V[kHeadMaxCin * 4];
+  __shared__ __attribute__((aligned(8))) float2 bss[kHeadMaxCin];
   __shared__ float cst;
+  const bool fold = a.bn_fold != 0;
+  if (fold) head_bn_coef(a, bss);  // (head_contract's barrier publishes it)
   head_contract(a, V, &cst);
   constexpr int CC = CIN / 8;
   const float c0 = cst;
@@ -813,6 +839,13 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(HeadArgs a) {
       for (int q = 0; q < CC; ++q) {
         float x[8];
         unpack8(xv[u][q], x);
+        if (fold) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float2 s = bss[q * 8 + k];
+            x[k] = head_act(x[k], s.x, s.y);
+          }
+        }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {  // V from LDS (a broadcast read: every lane the same address)
           const float4 v = *reinterpret_cast<const float4*>(V + (q * 8 + k) * 4);
@@ -825,6 +858,9 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(HeadArgs a) {
       *reinterpret_cast<float2*>(row0 + W2) = make_float2(o[2], o[3]);
     }
   }
+  // the folded BN's statistics: save_mean / save_invstd and the running stats
+  // (bn_apply_kernel's block 0 in the unfolded path)
+  if (fold && blockIdx.x == 0 && !a.bn.ss) bn_finalize_block0(a.bn, threadIdx.x, blockDim.x, 0, a.Cin);
 }
 
 // thread = (8-channel chunk, pixel row); U[c][ab] partials live in registers;
@@ -832,8 +868,11 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(HeadArgs a) {
 template <int CIN>
 __global__ void __launch_bounds__(256) head_bwd_kernel(HeadArgs a) {
   __shared__ float V[kHeadMaxCin * 4];
+  __shared__ __attribute__((aligned(8))) float2 bss[kHeadMaxCin];
   __shared__ float cst;
   extern __shared__ __attribute__((aligned(16))) float red[];  // [rows][Cin*4 + 1]
+  const bool fold = a.bn_fold != 0;  // x = y: act recomputed (the launcher checks bb.y == x)
+  if (fold) head_bn_coef(a, bss);
   head_contract(a, V, &cst);
   constexpr int CC = CIN / 8;
   constexpr int rows = 256 / CC;
@@ -842,12 +881,14 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(HeadArgs a) {
   const int total = a.N * a.H * a.W, HW = a.H * a.W;
   const BnBwdArgs& bb = a.bb;
   const bool fz = bb.sums != nullptr;
-  float s1[8], s2[8], mu[8], is[8];
+  float s1[8], s2[8], mu[8], is[8], bsc[8], bsh[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     s1[k] = s2[k] = 0.f;
     mu[k] = fz ? bb.mean[c8 + k] : 0.f;
     is[k] = fz ? bb.invstd[c8 + k] : 0.f;
+    bsc[k] = fold ? bss[c8 + k].x : 0.f;
+    bsh[k] = fold ? bss[c8 + k].y : 0.f;
   }
   float U[8][4];
   float S = 0.f;
@@ -874,7 +915,7 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(HeadArgs a) {
       const float* row0 = a.dl + ((size_t)n * 2 * a.H + 2 * i) * W2 + 2 * j;
       d01[u] = ok ? *reinterpret_cast<const float2*>(row0) : make_float2(0.f, 0.f);
       d23[u] = ok ? *reinterpret_cast<const float2*>(row0 + W2) : make_float2(0.f, 0.f);
-      xv[u] = ok ? *reinterpret_cast<const uint4*>(a.x + (size_t)pc * a.ldx + c8) : make_uint4(0, 0, 0, 0);
+      xv[u] = (ok && !fold) ? *reinterpret_cast<const uint4*>(a.x + (size_t)pc * a.ldx + c8) : make_uint4(0, 0, 0, 0);
       yv[u] = (ok && fz) ? *reinterpret_cast<const uint4*>(bb.y + (size_t)pc * bb.ldy + c8) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
@@ -884,7 +925,13 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(HeadArgs a) {
       const float d[4] = {d01[u].x, d01[u].y, d23[u].x, d23[u].y};
       if (chunk == 0) S += (d[0] + d[1]) + (d[2] + d[3]);
       float x[8], g[8];
-      unpack8(xv[u], x);
+      if (fold) {
+        unpack8(yv[u], x);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = head_act(x[k], bsc[k], bsh[k]);
+      } else {
+        unpack8(xv[u], x);
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         g[k] = d[0] * Vl[k][0] + d[1] * Vl[k][1] + d[2] * Vl[k][2] + d[3] * Vl[k][3];
@@ -974,7 +1021,7 @@ static bool head_ok(const HeadArgs& a) {
   return (a.Cin == 32 || a.Cin == 64) && (int64_t)a.N * a.H * a.W * 4 < 0x7fffffffLL;
 }
 hipError_t launch_head_fwd(const HeadArgs& a, hipStream_t st) {
-  if (!head_ok(a)) return hipErrorInvalidValue;
+  if (!head_ok(a) || (a.bn_fold && (a.bn.C != a.Cin || !a.bn.stats))) return hipErrorInvalidValue;
   const int64_t total = (int64_t)a.N * a.H * a.W;
   const int grid = grid_for(total, 256 * kHeadHP * 2, 1024);
   if (a.Cin == 32) hipLaunchKernelGGL(head_fwd_kernel<32>, dim3(grid), dim3(256), 0, st, a);
@@ -986,6 +1033,9 @@ hipError_t launch_head_bwd(const HeadArgs& a, hipStream_t st) {
   const int64_t total = (int64_t)a.N * a.H * a.W;
   const int CC = a.Cin / 8, rows = 256 / CC;
   if (a.bb.sums && (a.bb.C != a.Cin || a.bb.y2)) return hipErrorInvalidValue;
+  // the folded BN: act is recomputed from bb.y, which must be the head's x
+  if (a.bn_fold && (!a.bb.sums || a.bb.y != a.x || a.bb.ldy != a.ldx || a.bn.C != a.Cin || !a.bn.stats))
+    return hipErrorInvalidValue;
   const size_t lds = (size_t)rows * (a.Cin * 4 + 1 + (a.bb.sums ? 2 * a.Cin : 0)) * sizeof(float);
   // 512 blocks: each adds Cin*4 + 1 fp64 partials (16 replicas) at its end;
   // 1024 blocks onto one copy serialised ~1k same-address atomics per word

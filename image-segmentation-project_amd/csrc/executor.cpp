@@ -199,6 +199,11 @@ struct unet_plan {
   // BasicBlock downsample (1x1 / s2) weight gradient folded into the conv1
   // (3x3 / s2) halo weight gradient (UNET_NO_DS_FOLD=1: separate launch, A/B)
   bool ds_wgrad_fold = std::getenv("UNET_NO_DS_FOLD") == nullptr;
+  // training: decoder1's last BN + ReLU formed inside the head's two passes
+  // from the raw conv output (no bn_apply pass, decoder1's activation never
+  // stored; plain U-Net with the fused BN backward only).  UNET_NO_HEAD_BN_FOLD=1:
+  // separate pass (A/B only)
+  bool head_bn_fold = std::getenv("UNET_NO_HEAD_BN_FOLD") == nullptr;
   // single-stream backward: a weight gradient's split-K reduction rides in the
   // next BN-backward apply launch (UNET_NO_MERGE_REDUCE=1: separate launches)
   bool merge_reduce = std::getenv("UNET_NO_MERGE_REDUCE") == nullptr;
@@ -740,6 +745,12 @@ static int build_plan(unet_plan* p) {
   p->d_y0 = act(A, N, H2, W2, c0);
   p->ws_bytes = A.top;
 
+  {
+    const int hc = p->decs[3].out.C;
+    p->head_bn_fold = p->head_bn_fold && p->fuse_bwd && p->atts.empty() && (hc == 32 || hc == 64) &&
+                      p->decs[3].y2.C == hc;
+  }
+
   // named views for tests: forward activations and their gradients
   auto& nm = p->named;
   const bool y0_stored = !p->stem_rc || p->stem_keep;  // recompute: y0 / dZ only kept for tests
@@ -770,6 +781,7 @@ static int build_plan(unet_plan* p) {
     const std::string pre = "dec" + std::to_string(4 - l) + ".";
     nm.push_back({pre + "up", d.up_out}); nm.push_back({pre + "cat", d.cat});
     nm.push_back({pre + "y1", d.y1}); nm.push_back({pre + "h", d.h}); nm.push_back({pre + "y2", d.y2});
+    // (dec1.out: written by eval forwards; a training forward with head_bn_fold leaves it untouched)
     nm.push_back({pre + "out", d.out});
     nm.push_back({pre + "d.out", d.d_out}); nm.push_back({pre + "d.y2", d.dy2}); nm.push_back({pre + "d.h", d.dh});
     nm.push_back({pre + "d.y1", d.dy1});
@@ -1643,6 +1655,7 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
     }
   }
   const bool att = !p->atts.empty();
+  const bool hfold = training && p->head_bn_fold;
   for (int l = 0; l < (int)p->decs.size(); ++l) {
     Dec& d = p->decs[l];
     RUN(conv_forward(x, d.up, d.up_in, d.up_out, -1));
@@ -1658,7 +1671,7 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
         RUN(bn_apply(x, d.bn1, d.y1, d.h, 0, nullptr, -1, true));
         RUN(conv_forward(x, d.conv2, d.h, d.y2, d.bn2));
       }
-      RUN(bn_apply(x, d.bn2, d.y2, d.out, 0, nullptr, -1, true));
+      if (!(hfold && l == 3)) RUN(bn_apply(x, d.bn2, d.y2, d.out, 0, nullptr, -1, true));
     }
     if (att) RUN(ch_att_forward(x, l));
   }
@@ -1666,10 +1679,16 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
     const Act& o = att ? p->atts[3].out2 : p->decs[3].out;
     HeadArgs h = {};
     h.x = x.A(o); h.ldx = o.ld;
+    if (hfold) {  // the head reads decoder1's raw conv output and applies its last BN + ReLU
+      const Dec& d = p->decs[3];
+      h.x = x.A(d.y2); h.ldx = d.y2.ld;
+      h.bn = bn_launch(x, d.bn2, (int64_t)N * d.y2.H * d.y2.W);
+      h.bn_fold = 1;
+    }
     h.w0 = prm[p->up0_w]; h.b0 = prm[p->up0_b]; h.wf = prm[p->fin_w]; h.bf = prm[p->fin_b];
     h.logits = logits;
     h.N = N; h.H = o.H; h.W = o.W; h.Cin = o.C; h.Co = (int)p->params[p->up0_b].numel;
-    ProfScope ps(p, st, "head_fwd", 0);
+    ProfScope ps(p, st, hfold ? "head_fwd +bn" : "head_fwd", 0);
     CK(launch_head_fwd(h, st));
   }
   return 0;
@@ -1732,8 +1751,14 @@ static int run_backward(unet_plan* p, const float* image, const float* dlogits, 
     if (p->fuse_bwd && !att) {  // the head produces dA of decoder1's last BN: reduce it here
       const Dec& d = p->decs[3];
       h.bb = bwd_args(x, d.bn2, d.d_out, d.out, d.y2, d.dy2, -1, nullptr, nullptr, nullptr, grads);
+      if (p->head_bn_fold) {  // the forward never stored act: recomputed from y2 (same bits)
+        h.x = x.A(d.y2); h.ldx = d.y2.ld;
+        h.bb.act = nullptr;
+        h.bn = bn_launch(x, d.bn2, (int64_t)N * d.y2.H * d.y2.W);
+        h.bn_fold = 1;
+      }
     }
-    ProfScope ps(p, st, "head_bwd", 0);
+    ProfScope ps(p, st, h.bn_fold ? "head_bwd +bn" : "head_bwd", 0);
     CK(launch_head_bwd(h, st));
     CK(launch_head_grads(h, st));
   }

@@ -375,6 +375,13 @@ struct HeadArgs {
   // BN+ReLU; as in the conv-dgrad epilogue, dZ = dA * (act > 0) is stored and
   // the BN-backward sums (dZ, dZ*xhat) are reduced here (bn_bwd apply follows)
   BnBwdArgs bb;
+  // optional (bn_fold != 0): x is decoder1's raw conv output y and the head
+  // forms its input act = bf16(relu(bn(y))) itself, in both passes; decoder1's
+  // last BN apply pass and its activation buffer drop out.  The forward's
+  // block 0 finalises the batch statistics as bn_apply_kernel would; the
+  // backward needs bb (its fused sums) with bb.y == x.
+  BnLaunch bn;
+  int bn_fold;
   int N, H, W, Cin, Co;
 };
 hipError_t launch_head_fwd(const HeadArgs& a, hipStream_t st);

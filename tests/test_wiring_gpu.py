@@ -107,6 +107,15 @@ def _dcat(v, p):
     return torch.cat([v[p + "d.cat.skip"], v[p + "d.cat.up"]], 1)
 
 
+def dec1_act(v, bn):
+    """decoder1's output act = relu(bn2(y2)) in bf16.  A training forward does
+    not store it (HeadArgs.bn_fold: the head applies that BN + ReLU to y2 in
+    both of its passes), so the head rows are teacher-forced from y2; the
+    logits / dA / upconv0 / conv_final rows then check the fold itself."""
+    with torch.no_grad():
+        return F.relu(bn_train(v["dec1.y2"], bn)).to(torch.bfloat16).float()
+
+
 def _check(rows):
     for name, e in rows:
         print(f"{name:28s} {e:.3e}")
@@ -148,9 +157,11 @@ def test_forward_ops(run):
             rows.append((p + "y1", _rel(v[p + "y1"], F.conv2d(v[p + "cat"], W(dec[0]), dec[0].bias, padding=1))))
             rows.append((p + "h", _rel(v[p + "h"], F.relu(bn_train(v[p + "y1"], dec[1])))))
             rows.append((p + "y2", _rel(v[p + "y2"], F.conv2d(v[p + "h"], W(dec[3]), dec[3].bias, padding=1))))
+            if lvl == 1:
+                break  # decoder1's act is formed inside the head (dec1_act)
             rows.append((p + "out", _rel(v[p + "out"], F.relu(bn_train(v[p + "y2"], dec[4])))))
             prev = v[p + "out"]
-        head = ref.conv_final(ref.upconv0(v["dec1.out"]))
+        head = ref.conv_final(ref.upconv0(dec1_act(v, ref.decoder1[4])))
         rows.append(("logits", _rel(logits, head)))
     _check(rows)
 
@@ -162,13 +173,14 @@ def test_backward_ops(run):
     n = logits.numel()
     dl = (torch.sigmoid(logits) - y) / n
     # head: upconv0 + conv_final
-    d1 = v["dec1.out"].clone().requires_grad_(True)
+    a1 = dec1_act(v, ref.decoder1[4])
+    d1 = a1.clone().requires_grad_(True)
     u0w = ref.upconv0.weight.detach().clone().requires_grad_(True)
     u0b = ref.upconv0.bias.detach().clone().requires_grad_(True)
     fw = ref.conv_final.weight.detach().clone().requires_grad_(True)
     fb = ref.conv_final.bias.detach().clone().requires_grad_(True)
     F.conv2d(F.conv_transpose2d(d1, u0w, u0b, stride=2), fw, fb).backward(dl)
-    rows += [("dec1.d.out", _masked(v["dec1.d.out"], d1.grad, v["dec1.out"])), ("g upconv0.weight", _rel(grads["upconv0.weight"], u0w.grad)),
+    rows += [("dec1.d.out", _masked(v["dec1.d.out"], d1.grad, a1)), ("g upconv0.weight", _rel(grads["upconv0.weight"], u0w.grad)),
              ("g upconv0.bias", _rel(grads["upconv0.bias"], u0b.grad)),
              ("g conv_final.weight", _rel(grads["conv_final.weight"], fw.grad)),
              ("g conv_final.bias", _rel(grads["conv_final.bias"], fb.grad))]
@@ -177,7 +189,7 @@ def test_backward_ops(run):
     for lvl in (1, 2, 3, 4):
         dec, up, p = getattr(ref, f"decoder{lvl}"), getattr(ref, f"upconv{lvl}"), f"dec{lvl}."
         dout = v[p + "d.out"]
-        dy2, dg, db = local_bn_bwd(v[p + "y2"], dout, dec[4], out=v[p + "out"])
+        dy2, dg, db = local_bn_bwd(v[p + "y2"], dout, dec[4], out=a1 if lvl == 1 else v[p + "out"])
         rows += [(p + "d.y2", _rel(v[p + "d.y2"], dy2)), (f"g decoder{lvl}.4.weight", _rel(grads[f"decoder{lvl}.4.weight"], dg)),
                  (f"g decoder{lvl}.4.bias", _rel(grads[f"decoder{lvl}.4.bias"], db))]
         dh = torch.nn.grad.conv2d_input(v[p + "h"].shape, W(dec[3]), v[p + "d.y2"], padding=1)
