@@ -68,6 +68,8 @@ __global__ void __launch_bounds__(kCtWaves * 64) convt2x2_kernel(ConvFwdArgs a, 
   float* red = cst + 2 * NN;                               // [kCtWaves][NN][2], then bias sums [kCtWaves][Co]
   float* redb = red + kCtWaves * NN * 2;
   int* flag = reinterpret_cast<int*>(redb + kCtWaves * Co);
+  float* xss = reinterpret_cast<float*>(flag + 4);  // MODE 0 xform: [2][K] scale | shift
+  const bool xf = MODE == 0 && a.xform != 0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int pl = lane & 15, kq = lane >> 4;
   const bool bsum = MODE == 1 && a.bias_acc != nullptr;
@@ -130,6 +132,13 @@ __global__ void __launch_bounds__(kCtWaves * 64) convt2x2_kernel(ConvFwdArgs a, 
   }
   if constexpr (MODE == 0) {
     for (int c = tid; c < Co; c += kCtWaves * 64) cst[c] = a.bias ? a.bias[c] : 0.f;
+    if (xf) {  // the previous BN's affine map (bn_apply's coefficients, as the ws xform)
+      for (int c = tid; c < K; c += kCtWaves * 64) {
+        float m, is, var;
+        bn_scale_shift(a.xbn, c, xss[c], xss[K + c], m, is, var);
+      }
+      if (blockIdx.x == 0) bn_finalize(a.xbn);  // saved mean / invstd, running statistics
+    }
   } else if constexpr (FB) {
     for (int c = tid; c < NN; c += kCtWaves * 64) {
       cst[c] = a.bb.mean[c];
@@ -149,6 +158,26 @@ __global__ void __launch_bounds__(kCtWaves * 64) convt2x2_kernel(ConvFwdArgs a, 
     for (int e = 0; e < 8; ++e) bs[j][e] = 0.f;
 
   for (; g < ngroups; g += nw) {
+    if (xf) {  // B holds the raw y: relu(y * scale + shift) in place, stored as the activation
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int m = (g * MT + mt) * 16 + pl;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const int c0 = ks * 32 + kq * 8;
+          float v[8];
+          unpack8(__builtin_bit_cast(uint4, Bc[mt][ks]), v);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            v[k] = v[k] * xss[c0 + k] + xss[K + c0 + k];
+            v[k] = v[k] > 0.f ? v[k] : 0.f;
+          }
+          const uint4 o = pack8(v);
+          Bc[mt][ks] = __builtin_bit_cast(bf16x8, o);
+          *reinterpret_cast<uint4*>(a.xh + (size_t)m * a.ldxh + c0) = o;
+        }
+      }
+    }
     if (bsum) {  // bias gradient: lane's channels (ks % NBS) * 32 + 8 kq + e, every tap
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
@@ -310,7 +339,8 @@ static hipError_t convt_cfg(const ConvFwdArgs& a, hipStream_t st) {
   const long long M = (long long)a.N * a.H * a.W;
   if (M % (16 * MT)) return hipErrorNotSupported;
   const int ngroups = (int)(M / (16 * MT));
-  const size_t lds = (size_t)NN * K * 2 + 2 * NN * 4 + kCtWaves * NN * 2 * 4 + kCtWaves * Co * 4 + 16;
+  const size_t lds = (size_t)NN * K * 2 + 2 * NN * 4 + kCtWaves * NN * 2 * 4 + kCtWaves * Co * 4 + 16 +
+                     (MODE == 0 && a.xform ? 2 * K * 4 : 0);
   // the fused form keeps one block per CU: its per-block reduction and fp64
   // atomics amortise over more groups (micro: upconv1 38.6 -> 34.8 us,
   // upconv2 43.8 -> 34.1 us); otherwise as many as LDS allows, up to 4
@@ -335,9 +365,24 @@ static hipError_t convt_fb(const ConvFwdArgs& a, hipStream_t st) {
 static bool al16(const void* p) { return ((size_t)p & 15) == 0; }
 static bool al8(const void* p) { return ((size_t)p & 7) == 0; }
 
+static bool convt_fwd_covered(int Ci, int Co) {
+  return (Ci == 64 && Co == 32) || (Ci == 64 && Co == 64) || (Ci == 128 && Co == 64);
+}
+
+// forward with the previous BN + ReLU applied to the pixel operand (xform):
+// the shapes and strides launch_convt2x2 takes for it (pointers are checked there)
+bool convt2x2_xform_ok(const ConvFwdArgs& a) {
+  return convt_fwd_covered(a.C, a.Cout) && (long long)a.N * a.H * a.W % 16 == 0 && a.ldx % 8 == 0 &&
+         a.ldxh % 8 == 0 && a.ldy % 4 == 0 && a.N > 0 && a.H > 0 && a.W > 0;
+}
+
 hipError_t launch_convt2x2(const ConvFwdArgs& a, int mode, hipStream_t st) {
   if (mode != 0 && mode != 1) return hipErrorInvalidValue;
-  if (a.add || a.stats || a.x2 || a.ysplit || a.fold_on || a.xform || a.bb.y2 || a.wch) return hipErrorNotSupported;
+  if (a.add || a.stats || a.x2 || a.ysplit || a.fold_on || a.bb.y2 || a.wch) return hipErrorNotSupported;
+  if (a.xform) {  // forward only, every operand of the fold in place (no fallback takes it)
+    if (mode != 0 || !convt2x2_xform_ok(a) || !al16(a.xh) || !a.xbn.stats || a.xbn.C != a.C || a.xbn.ss)
+      return hipErrorInvalidValue;
+  }
   if (mode == 0 && (a.bb.sums || a.bias_acc)) return hipErrorInvalidValue;
   if (a.N <= 0 || a.H <= 0 || a.W <= 0) return hipErrorInvalidValue;
   // 16-B pixel-operand loads, 8-B result (and BN operand) accesses
@@ -345,6 +390,7 @@ hipError_t launch_convt2x2(const ConvFwdArgs& a, int mode, hipStream_t st) {
   if (a.bb.sums && (!al8(a.bb.act) || !al8(a.bb.y) || a.bb.ldact % 4 || a.bb.ldy % 4 || a.bb.C != a.C))
     return hipErrorNotSupported;
   const int Ci = a.C, Co = a.Cout;
+  if (mode == 0 && !convt_fwd_covered(Ci, Co)) return hipErrorNotSupported;
   if (mode == 0) {  // NN = 4 Co columns, K = Ci
     if (Ci == 64 && Co == 32) return convt_fb<0, 8, 2>(a, st);
     if (Ci == 64 && Co == 64) return convt_fb<0, 16, 2>(a, st);

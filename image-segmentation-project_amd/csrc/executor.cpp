@@ -1016,7 +1016,7 @@ int conv_forward(const Ctx& x, int ci, const Act& in, const Act& out, int bn_for
   }
   if (cv.kind == L_CONVT) {  // weight-stationary up-conv (convt.hip) where it covers the shape
     const hipError_t e = launch_convt2x2(a, 0, x.st);
-    if (e != hipErrorNotSupported) {
+    if (e != hipErrorNotSupported || a.xform) {  // (an xform launch has no fallback)
       CK(e);
       return 0;
     }
@@ -1038,6 +1038,25 @@ bool xform_ok(const Ctx& x, int ci, const Act& yraw, const Act& h, const Act& ou
   a.P = out.H; a.Q = out.W; a.Cout = cv.Co;
   a.R = cv.R; a.S = cv.S; a.stride = cv.stride; a.pad = cv.pad;
   return conv3x3_ws_xform_ok(a);
+}
+
+// the same for the next decoder level's up-conv (convt2x2_kernel forward):
+// decoder level l's last BN + ReLU applied to the up-conv's pixel operand and
+// the activation d.out stored by it (the plain U-Net: with attention the
+// channel-attention forward reads d.out first)
+bool up_xform_ok(const Ctx& x, int l) {
+  const unet_plan* p = x.p;
+  if (!x.training || !p->bn_xform || p->bn_ticket || !p->atts.empty() || l + 1 >= (int)p->decs.size()) return false;
+  const Dec& d = p->decs[l];
+  const Dec& n = p->decs[l + 1];
+  const Conv& cv = p->convs[n.up];
+  if (cv.f8 || cv.kind != L_CONVT || n.up_in.off != d.out.off || d.y2.C != d.out.C || d.y2.H != d.out.H ||
+      d.y2.W != d.out.W)
+    return false;
+  ConvFwdArgs a = {};
+  a.ldx = d.y2.ld; a.ldy = n.up_out.ld; a.ldxh = d.out.ld;
+  a.N = p->cfg.N; a.H = d.y2.H; a.W = d.y2.W; a.C = cv.Ci; a.Cout = cv.Co;
+  return cv.Ci == d.y2.C && convt2x2_xform_ok(a);
 }
 
 // conv dgrad: dx = dgrad(dy) (+ addend).  fuse: dx is dA of that BN(+ReLU);
@@ -1656,9 +1675,16 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
   }
   const bool att = !p->atts.empty();
   const bool hfold = training && p->head_bn_fold;
+  bool up_xf = false;  // the previous level's last BN + ReLU rides in this level's up-conv
   for (int l = 0; l < (int)p->decs.size(); ++l) {
     Dec& d = p->decs[l];
-    RUN(conv_forward(x, d.up, d.up_in, d.up_out, -1));
+    if (up_xf) {
+      const Dec& pd = p->decs[l - 1];
+      RUN(conv_forward(x, d.up, pd.y2, d.up_out, -1, -1, false, nullptr, pd.bn2, &pd.out));
+    } else {
+      RUN(conv_forward(x, d.up, d.up_in, d.up_out, -1));
+    }
+    up_xf = !fold && up_xform_ok(x, l);
     if (att) RUN(att_gate_forward(x, l));
     if (fold) {
       RUN(conv_forward(x, d.conv1, d.cat, d.h, -1, d.bn1, true));
@@ -1671,7 +1697,7 @@ static int run_forward(unet_plan* p, const float* image, const float* const* prm
         RUN(bn_apply(x, d.bn1, d.y1, d.h, 0, nullptr, -1, true));
         RUN(conv_forward(x, d.conv2, d.h, d.y2, d.bn2));
       }
-      if (!(hfold && l == 3)) RUN(bn_apply(x, d.bn2, d.y2, d.out, 0, nullptr, -1, true));
+      if (!(hfold && l == 3) && !up_xf) RUN(bn_apply(x, d.bn2, d.y2, d.out, 0, nullptr, -1, true));
     }
     if (att) RUN(ch_att_forward(x, l));
   }

@@ -198,6 +198,11 @@ hipError_t launch_conv3x3_fl(const ConvFwdArgs& a, int mode, hipStream_t st);
 // hipErrorNotSupported for shapes it does not cover (the caller falls back to
 // the implicit-GEMM path).
 hipError_t launch_convt2x2(const ConvFwdArgs& a, int mode, hipStream_t st);
+// forward with xform (the previous BN + ReLU applied to the pixel operand,
+// the activation stored to xh, block 0 finalising that BN; training, no
+// ticket): shape / stride test; the launch itself fails (no fallback) when an
+// xform launch is not taken
+bool convt2x2_xform_ok(const ConvFwdArgs& a);
 // 1 x 1 / stride-1 conv as a weight-stationary per-pixel GEMM (convt.hip): mode
 // 0 forward (w = forward pack [Cout][C], bias, BN sums `stats` / `bn`), mode 1
 // data gradient (w = dgrad pack [C_out_of_op][C], a.C = dY channels, a.Cout =
