@@ -125,7 +125,9 @@ def test_every_intermediate(pkg, golden, cuda):
     pkg.get_loss_function({"loss_fn": "bce"})(out, y.cuda()).backward()
     torch.cuda.synchronize()
     plan = m._last_plan
-    views = plan.tensor_views()
+    # decoder1's act is not stored by a training forward (the head applies that
+    # BN + ReLU to dec1.y2 itself, HeadArgs.bn_fold); its effect is in the logits
+    views = {k: t for k, t in plan.tensor_views().items() if k != "dec1.out"}
     fp32 = dict(_compare(views, results[False]))
     emu = dict(_compare(views, results[True]))
     for name in emu:
